@@ -1,0 +1,70 @@
+"""Closed-form (RNG-free) parameter init shared by the golden generator and the
+tests, so a model's weights can be regenerated on any box without shipping a
+checkpoint.  Keys are reference ``state_dict`` keys.
+
+value(name, shape) depends only on the key and the element index.
+"""
+import zlib
+
+import numpy as np
+import torch
+
+
+def _phase(name: str) -> float:
+    return (zlib.crc32(name.encode()) % 10007) / 10007.0 * 6.283185307179586
+
+
+def _wave(name, shape, freq, amp, offset):
+    n = int(np.prod(shape)) if len(shape) else 1
+    i = np.arange(n, dtype=np.float64)
+    v = offset + amp * np.sin(freq * i + _phase(name))
+    return torch.from_numpy(v.astype(np.float32)).reshape(shape)
+
+
+def formula_value(name: str, shape, trainable: bool) -> torch.Tensor:
+    leaf = name.split(".")[-1]
+    shape = tuple(shape)
+    if leaf == "weight_v":
+        return _wave(name, shape, 0.7137, 1.0, 0.0)
+    if leaf == "weight" and len(shape) == 4:  # plain conv (weight_norm=False)
+        return _wave(name, shape, 0.7137, float(np.prod(shape[1:])) ** -0.5, 0.0)
+    if leaf == "weight_g":
+        if not trainable:
+            return torch.ones(shape)
+        return _wave(name, shape, 1.31, 0.1, 0.5)
+    if leaf == "bias":
+        return _wave(name, shape, 0.913, 0.05, 0.0)
+    if leaf == "weight":                       # BatchNorm affine weight
+        return _wave(name, shape, 1.07, 0.1, 1.0)
+    if leaf == "scale":
+        return _wave(name, shape, 1.0, 0.1, 0.5)
+    if leaf == "scale_shift":
+        return _wave(name, shape, 1.0, 0.05, 0.0)
+    if leaf == "running_mean":
+        return torch.zeros(shape)
+    if leaf == "running_var":
+        return torch.ones(shape)
+    if leaf == "num_batches_tracked":
+        return torch.zeros(shape, dtype=torch.long)
+    raise KeyError(name)
+
+
+def formula_state(module: torch.nn.Module):
+    """A full state dict for ``module`` (reference or engine: same keys)."""
+    trainable = {n for n, p in module.named_parameters() if p.requires_grad}
+    out = {}
+    for k, v in module.state_dict().items():
+        out[k] = formula_value(k, v.shape, k in trainable).to(v.dtype)
+    return out
+
+
+def pixels(batch, channels, size, seed=0):
+    """Synthetic raw pixels k/255, k ~ U{0..255} (ToTensor semantics), numpy PCG64."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    k = rng.integers(0, 256, size=(batch, channels, size, size))
+    return torch.from_numpy((k / 255.0).astype(np.float32))
+
+
+def uniform_noise(batch, channels, size, seed=1):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    return torch.from_numpy(rng.random((batch, channels, size, size)).astype(np.float32))

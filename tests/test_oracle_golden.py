@@ -1,0 +1,175 @@
+"""Pin the CPU oracle to golden vectors generated from the reference itself
+(tools/make_goldens.py).  CPU only."""
+import numpy as np
+import pytest
+import torch
+
+import realnvp_oracle as O
+from conftest import load_golden
+from formula_init import formula_value
+
+COUPLINGS = [
+    # golden name, kind, in_out, mid, size, cfg, hp kwargs
+    ("ckbd_c3_m32_s32_cfg1", "ckbd", 3, 32, 32, 1.0, dict(base_dim=32, res_blocks=2)),
+    ("ckbd_c3_m32_s32_cfg0", "ckbd", 3, 32, 32, 0.0, dict(base_dim=32, res_blocks=2)),
+    ("chan_c12_m64_s16_cfg0", "chan", 12, 64, 16, 0.0, dict(base_dim=32, res_blocks=2)),
+    ("chan_c12_m64_s16_cfg1", "chan", 12, 64, 16, 1.0, dict(base_dim=32, res_blocks=2)),
+    ("ckbd_c48_m64_s4_cfg0", "ckbd", 48, 64, 4, 0.0, dict(base_dim=32, res_blocks=1)),
+    ("ckbd_nobott_cfg1", "ckbd", 3, 16, 8, 1.0, dict(base_dim=16, res_blocks=2, bottleneck=False)),
+    ("ckbd_r0_bott_cfg0", "ckbd", 3, 16, 8, 0.0, dict(base_dim=16, res_blocks=0)),
+    ("ckbd_r0_nobott_cfg1", "ckbd", 3, 16, 8, 1.0, dict(base_dim=16, res_blocks=0, bottleneck=False)),
+    ("chan_noskip_cfg1", "chan", 12, 16, 8, 1.0, dict(base_dim=16, res_blocks=2, skip=False)),
+    ("ckbd_nownorm_cfg1", "ckbd", 3, 16, 8, 1.0, dict(base_dim=16, res_blocks=1, weight_norm=False)),
+    ("chan_nocbn_cfg0", "chan", 12, 16, 8, 0.0, dict(base_dim=16, res_blocks=1, coupling_bn=False)),
+]
+
+MODELS = [("m32_d8_r1", 32, 8, 1), ("m32_d32_r2", 32, 32, 2)]
+
+
+def rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+
+
+def test_masks_bit_exact():
+    g = load_golden("index_maps.npz")
+    for size in (2, 4, 8, 16, 32, 64, 128):
+        for cfg in (0, 1):
+            assert np.array_equal(O.checkerboard_mask(size, cfg).numpy(), g["mask_%d_%d" % (size, cfg)])
+
+
+@pytest.mark.parametrize("shp", [(2, 3, 8, 8), (1, 6, 4, 4), (2, 12, 16, 16), (3, 24, 2, 2), (1, 3, 64, 64)])
+def test_permutations_bit_exact(shp):
+    g = load_golden("index_maps.npz")
+    tag = "x".join(map(str, shp))
+    x = torch.from_numpy(g["squeeze_in_" + tag])
+    assert np.array_equal(O.squeeze(x).numpy(), g["squeeze_out_" + tag])
+    assert np.array_equal(O.undo_squeeze(O.squeeze(x)).numpy(), g["undo_out_" + tag])
+    xs = torch.from_numpy(g["undo_direct_in_" + tag])
+    assert np.array_equal(O.undo_squeeze(xs).numpy(), g["undo_direct_out_" + tag])
+    on, off = O.factor_out(x)
+    assert np.array_equal(on.numpy(), g["factor_on_" + tag])
+    assert np.array_equal(off.numpy(), g["factor_off_" + tag])
+    assert np.array_equal(O.restore(on, off).numpy(), g["restore_out_" + tag])
+
+
+def test_logit_transform():
+    g = load_golden("logit.npz")
+    lx, ld = O.logit_transform(torch.from_numpy(g["x"]), torch.from_numpy(g["noise"]))
+    np.testing.assert_allclose(lx.numpy(), g["logit"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(ld.numpy(), g["logdet"], rtol=1e-6)
+    inv = O.logit_inverse(torch.from_numpy(g["inv_in"]))
+    np.testing.assert_allclose(inv.numpy(), g["inv_out"], rtol=1e-6, atol=1e-7)
+
+
+def coupling_state(kind, cio, mid, hp):
+    entries = O.coupling_spec("", kind, cio, mid, hp)
+    return O.build_state(entries, formula_value), entries
+
+
+@pytest.mark.parametrize("case", COUPLINGS, ids=[c[0] for c in COUPLINGS])
+def test_coupling_vs_reference(case):
+    name, kind, cio, mid, size, cfg, hk = case
+    g = load_golden("coupling_%s.npz" % name)
+    hp = O.HP(**hk)
+    S, entries = coupling_state(kind, cio, mid, hp)
+    fn = O.checkerboard_coupling if kind == "ckbd" else O.channelwise_coupling
+    x = torch.from_numpy(g["x"]).requires_grad_(True)
+    train = O.trainable_names(entries)
+    for n in train:
+        S[n].requires_grad_(True)
+    y, ldj = fn(S, "", x, cfg, hp, training=True)
+    np.testing.assert_allclose(y.detach().numpy(), g["train_y"], rtol=1e-4, atol=2e-5)
+    np.testing.assert_allclose(ldj.detach().numpy(), g["train_ldj"], rtol=1e-4, atol=2e-5)
+    loss = (y * torch.from_numpy(g["gy"]) + ldj * torch.from_numpy(g["gl"])).sum()
+    grads = torch.autograd.grad(loss, [x] + [S[n] for n in train], allow_unused=True)
+    assert rel(grads[0].numpy(), g["grad_x"]) < 1e-4
+    gnorm = np.sqrt(sum(float((g["grad." + n].astype(np.float64) ** 2).sum()) for n in train if "grad." + n in g))
+    for n, gr in zip(train, grads[1:]):
+        ref = g["grad." + n]
+        got = np.zeros_like(ref) if gr is None else gr.numpy()
+        err = np.linalg.norm(got.astype(np.float64) - ref)
+        assert err <= 1e-4 * np.linalg.norm(ref) + 1e-6 * gnorm, n
+    for k in g.files:
+        if k.startswith("after_train."):
+            np.testing.assert_allclose(S[k[len("after_train."):]].detach().numpy(), g[k], rtol=1e-4, atol=1e-6)
+    with torch.no_grad():
+        xr, _ = fn(S, "", torch.from_numpy(g["x"]), cfg, hp, training=True, reverse=True)
+    np.testing.assert_allclose(xr.numpy(), g["train_rev"], rtol=1e-4, atol=2e-5)
+    with torch.no_grad():
+        ye, le = fn(S, "", torch.from_numpy(g["x"]), cfg, hp, training=False)
+        xe, _ = fn(S, "", ye, cfg, hp, training=False, reverse=True)
+    np.testing.assert_allclose(ye.numpy(), g["eval_y"], rtol=1e-4, atol=2e-5)
+    np.testing.assert_allclose(le.numpy(), g["eval_ldj"], rtol=1e-4, atol=2e-5)
+    np.testing.assert_allclose(xe.numpy(), g["eval_rec"], rtol=1e-4, atol=2e-5)
+
+
+@pytest.mark.parametrize("case", MODELS, ids=[c[0] for c in MODELS])
+def test_model_vs_reference(case):
+    name, size, bd, rb = case
+    g = load_golden("model_%s.npz" % name)
+    spec = O.FlowSpec(3, size, O.HP(bd, rb))
+    entries = O.flow_spec_entries(spec)
+    S = O.build_state(entries, formula_value)
+    train = O.trainable_names(entries)
+    names = O.param_names(entries)
+    # the golden lists the parameters that received a gradient, in reference order
+    assert list(g["grad_names"]) == train
+    x = torch.from_numpy(g["x"])
+    logdet = torch.from_numpy(g["logdet"])
+    lx, ld = O.logit_transform(torch.from_numpy(g["pixels"]), torch.from_numpy(g["noise"]))
+    np.testing.assert_allclose(lx.numpy(), g["x"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(ld.numpy(), g["logdet"], rtol=1e-6)
+    for n in train:
+        S[n].requires_grad_(True)
+    xr = x.clone().requires_grad_(True)
+    lp = O.log_prob(S, spec, xr, training=True)
+    ws = O.weight_scale(S, names, lambda n: n in set(train))
+    np.testing.assert_allclose(lp.detach().numpy(), g["train_logprob"], rtol=1e-5)
+    np.testing.assert_allclose(float(ws.detach()), float(g["weight_scale"]), rtol=1e-5)
+    loss = -(lp + logdet).mean() + O.SCALE_REG * ws
+    np.testing.assert_allclose(float(loss), float(g["loss"]), rtol=1e-5)
+    grads = torch.autograd.grad(loss, [xr] + [S[n] for n in train])
+    # fp32 noise floor of dL/dx through 28 batch-stat couplings: fp32 vs fp64
+    # oracle differ by 2.9e-3 relative L2 at m32_d32_r2 (measured) -> 1e-2
+    assert rel(grads[0].numpy(), g["grad_x"]) < 1e-2
+    norms = np.array([float(t.norm()) for t in grads[1:]])
+    tot = np.linalg.norm(g["grad_norms"])
+    big = g["grad_norms"] > 1e-4 * tot
+    # per-tensor fp32 floor: oracle fp32 vs fp64 reach 3.9e-2 on single tensor
+    # norms at m32_d32_r2 (the reference itself 2.6e-2 vs fp64), measured.
+    assert rel(norms, g["grad_norms"]) < 5e-3
+    np.testing.assert_allclose(norms[big], g["grad_norms"][big], rtol=8e-2)
+    # eval mode after the same running-stat updates as the golden (fwd + f)
+    with torch.no_grad():
+        O.flow_f(S, spec, x, training=True)
+    for k in g.files:
+        if k.startswith("after_train."):
+            np.testing.assert_allclose(S[k[len("after_train."):]].numpy(), g[k], rtol=1e-4, atol=1e-5)
+    with torch.no_grad():
+        lpe = O.log_prob(S, spec, x, training=False)
+        ze, _ = O.flow_f(S, spec, x, training=False)
+        xrec = O.flow_g(S, spec, ze, training=False)
+        xs = O.flow_g(S, spec, torch.from_numpy(g["sample_z"]), training=False)
+    np.testing.assert_allclose(lpe.numpy(), g["eval_logprob"], rtol=1e-5)
+    assert np.abs(xrec.numpy() - g["eval_rec"]).max() / np.abs(g["eval_rec"]).max() < 1e-5
+    assert rel(xs.numpy(), g["sample_x"]) < 1e-4
+
+
+@pytest.mark.parametrize("case", MODELS[:1], ids=[MODELS[0][0]])
+def test_trainer_trajectory(case):
+    from formula_init import pixels, uniform_noise
+    name, size, bd, rb = case
+    g = load_golden("model_%s.npz" % name)
+    spec = O.FlowSpec(3, size, O.HP(bd, rb))
+    entries = O.flow_spec_entries(spec)
+    S = O.build_state(entries, formula_value)
+    tr = O.OracleTrainer(S, spec, O.param_names(entries), O.trainable_names(entries))
+    B = g["x"].shape[0]
+    for s in range(len(g["traj_loss"])):
+        x, ld = O.logit_transform(pixels(B, 3, size, seed=100 + s), uniform_noise(B, 3, size, seed=200 + s))
+        loss, ll = tr.step(x, ld)
+        np.testing.assert_allclose(loss, g["traj_loss"][s], rtol=2e-5)
+    with torch.no_grad():
+        lp = O.log_prob(S, spec, torch.from_numpy(g["x"]), training=False)
+    np.testing.assert_allclose(lp.numpy(), g["traj_eval_logprob_after"], rtol=1e-4)
