@@ -1,0 +1,110 @@
+// Shared device helpers for the RealNVP MI355X (gfx950) kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "realnvp_hip.h"
+
+typedef uint16_t bf16_t;                                        // bf16 storage
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));      // MFMA operand
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+#define RNVP_LDS __attribute__((address_space(3)))
+
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+__device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+
+// scalar load/store of a net-activation element as float
+__device__ __forceinline__ float ldv(const float* p) { return *p; }
+__device__ __forceinline__ float ldv(const bf16_t* p) { return bf2f(*p); }
+__device__ __forceinline__ void stv(float* p, float v) { *p = v; }
+__device__ __forceinline__ void stv(bf16_t* p, float v) { *p = f2bf(v); }
+
+// elements per 16-byte chunk
+template <typename T> struct Chunk;
+template <> struct Chunk<float> { static constexpr int N = 4; };
+template <> struct Chunk<bf16_t> { static constexpr int N = 8; };
+
+// unpack / pack one 16-byte chunk
+__device__ __forceinline__ void unpack(const u32x4& c, float* v, float) {
+    v[0] = __uint_as_float(c.x); v[1] = __uint_as_float(c.y);
+    v[2] = __uint_as_float(c.z); v[3] = __uint_as_float(c.w);
+}
+__device__ __forceinline__ void unpack(const u32x4& c, float* v, bf16_t) {
+    uint32_t w[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        v[2 * i] = __uint_as_float(w[i] << 16);
+        v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+}
+__device__ __forceinline__ u32x4 pack(const float* v, float) {
+    u32x4 c;
+    c.x = __float_as_uint(v[0]); c.y = __float_as_uint(v[1]);
+    c.z = __float_as_uint(v[2]); c.w = __float_as_uint(v[3]);
+    return c;
+}
+__device__ __forceinline__ u32x4 pack(const float* v, bf16_t) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+    u32x4 c;
+    c.x = w[0]; c.y = w[1]; c.z = w[2]; c.w = w[3];
+    return c;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// block-wide sum (blockDim.x multiple of 64, <= 1024); every thread gets the result
+template <typename F>
+__device__ __forceinline__ F block_sum(F v, F* red /* >= 16 entries of LDS */) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    v = wave_sum(v);
+    __syncthreads();
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    F t = 0;
+    for (int i = 0; i < nw; ++i) t += red[i];
+    return t;
+}
+
+// per-channel BN affine (scale, shift) such that bn(x) = x*scale + shift
+__device__ __forceinline__ void bn_affine(const rnvp_bn_src& s, int C, int c, float& scale, float& shift,
+                                          float* mean_out = nullptr, float* rstd_out = nullptr) {
+    double mean, var;
+    if (s.sums) {
+        mean = s.sums[c] / s.count;
+        var = s.sums[C + c] / s.count - mean * mean;
+        if (var < 0) var = 0;
+    } else {
+        mean = s.mean[c];
+        var = s.var[c];
+    }
+    float rstd = (float)(1.0 / sqrt(var + (double)s.eps));
+    float g = s.gamma ? s.gamma[c] : 1.f;
+    float b = s.beta ? s.beta[c] : 0.f;
+    scale = g * rstd;
+    shift = b - (float)mean * g * rstd;
+    if (mean_out) *mean_out = (float)mean;
+    if (rstd_out) *rstd_out = rstd;
+}
+
+static inline int rnvp_grid(long long n, int block, int cap = 4096) {
+    long long g = (n + block - 1) / block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (int)g;
+}
+
+#define RNVP_LAUNCH_CHECK() do { hipError_t e__ = hipGetLastError(); if (e__ != hipSuccess) return (int)e__; } while (0)

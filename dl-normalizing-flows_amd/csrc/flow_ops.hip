@@ -1,0 +1,360 @@
+// Flow-level kernels: index maps, logit transform, prior log-prob, regulariser,
+// BN running stats, fused Adam.  All HBM-bound elementwise / reduction work.
+#include <math.h>
+
+#include "common.h"
+
+extern "C" int rnvp_version(void) { return 100; }
+
+extern "C" const char* rnvp_status_string(int s) {
+    if (s == RNVP_OK) return "ok";
+    if (s == RNVP_E_INVALID) return "invalid argument";
+    if (s == RNVP_E_UNSUPPORTED) return "unsupported configuration";
+    return hipGetErrorString((hipError_t)s);
+}
+
+// ---------------------------------------------------------------------------
+// index maps  (modules_realnvp.py:211-226, flow_realnvp.py:121-193)
+// ---------------------------------------------------------------------------
+__global__ void k_mask(float* m, int S, int cfg) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < S * S) m[i] = (float)((cfg + i / S + i % S) & 1);
+}
+
+extern "C" int rnvp_checkerboard_mask(float* mask, int size, int config, void* stream) {
+    if (!mask || size <= 0) return RNVP_E_INVALID;
+    k_mask<<<rnvp_grid((long long)size * size, 256, 1 << 20), 256, 0, (hipStream_t)stream>>>(mask, size, config & 1);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+// squeeze: y[b, 4c+2i+j, h, w] = x[b, c, 2h+i, 2w+j].  One thread per x element
+// (coalesced read), indices in 64-bit.
+__global__ void k_squeeze(const float* __restrict__ x, float* __restrict__ y, int C, int H, int W, long long n) {
+    const int h2 = H >> 1, w2 = W >> 1;
+    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+        int xx = (int)(e % W);
+        long long t = e / W;
+        int yy = (int)(t % H);
+        t /= H;
+        int c = (int)(t % C);
+        long long b = t / C;
+        int i = yy & 1, j = xx & 1;
+        long long o = (((b * 4 * C + 4 * c + 2 * i + j) * h2 + (yy >> 1)) * w2 + (xx >> 1));
+        y[o] = x[e];
+    }
+}
+// undo: x[b, c, 2h+i, 2w+j] = y[b, 4c+2i+j, h, w]  (gather, one thread per x element)
+__global__ void k_undo_squeeze(const float* __restrict__ y, float* __restrict__ x, int C, int H, int W, long long n) {
+    const int h2 = H >> 1, w2 = W >> 1;
+    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+        int xx = (int)(e % W);
+        long long t = e / W;
+        int yy = (int)(t % H);
+        t /= H;
+        int c = (int)(t % C);
+        long long b = t / C;
+        int i = yy & 1, j = xx & 1;
+        x[e] = y[(((b * 4 * C + 4 * c + 2 * i + j) * h2 + (yy >> 1)) * w2 + (xx >> 1))];
+    }
+}
+
+extern "C" int rnvp_squeeze(const float* x, float* y, int B, int C, int H, int W, void* stream) {
+    if (!x || !y || B < 0 || C <= 0 || (H & 1) || (W & 1)) return RNVP_E_INVALID;
+    long long n = (long long)B * C * H * W;
+    if (n == 0) return RNVP_OK;
+    k_squeeze<<<rnvp_grid(n, 256), 256, 0, (hipStream_t)stream>>>(x, y, C, H, W, n);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+extern "C" int rnvp_undo_squeeze(const float* y, float* x, int B, int C, int H, int W, void* stream) {
+    if (!x || !y || B < 0 || C <= 0 || (H & 1) || (W & 1)) return RNVP_E_INVALID;
+    long long n = (long long)B * C * H * W;
+    if (n == 0) return RNVP_OK;
+    k_undo_squeeze<<<rnvp_grid(n, 256), 256, 0, (hipStream_t)stream>>>(y, x, C, H, W, n);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+// factor_out: (y&1, x&1) = (0,0) -> on[c], (1,1) -> on[C+c], (0,1) -> off[c], (1,0) -> off[C+c]
+__global__ void k_factor_out(const float* __restrict__ x, float* __restrict__ on, float* __restrict__ off,
+                             int C, int H, int W, long long n) {
+    const int h2 = H >> 1, w2 = W >> 1;
+    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+        int xx = (int)(e % W);
+        long long t = e / W;
+        int yy = (int)(t % H);
+        t /= H;
+        int c = (int)(t % C);
+        long long b = t / C;
+        int i = yy & 1, j = xx & 1;
+        float* dst = (i == j) ? on : off;
+        int cc = (i == 0) ? c : C + c;
+        dst[((b * 2 * C + cc) * h2 + (yy >> 1)) * w2 + (xx >> 1)] = x[e];
+    }
+}
+__global__ void k_restore(const float* __restrict__ on, const float* __restrict__ off, float* __restrict__ x,
+                          int C, int H, int W, long long n) {
+    const int h2 = H >> 1, w2 = W >> 1;
+    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+        int xx = (int)(e % W);
+        long long t = e / W;
+        int yy = (int)(t % H);
+        t /= H;
+        int c = (int)(t % C);
+        long long b = t / C;
+        int i = yy & 1, j = xx & 1;
+        const float* src = (i == j) ? on : off;
+        int cc = (i == 0) ? c : C + c;
+        x[e] = src[((b * 2 * C + cc) * h2 + (yy >> 1)) * w2 + (xx >> 1)];
+    }
+}
+
+extern "C" int rnvp_factor_out(const float* x, float* on, float* off, int B, int C, int H, int W, void* stream) {
+    if (!x || !on || !off || B < 0 || C <= 0 || (H & 1) || (W & 1)) return RNVP_E_INVALID;
+    long long n = (long long)B * C * H * W;
+    if (n == 0) return RNVP_OK;
+    k_factor_out<<<rnvp_grid(n, 256), 256, 0, (hipStream_t)stream>>>(x, on, off, C, H, W, n);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+extern "C" int rnvp_restore(const float* on, const float* off, float* x, int B, int C, int H, int W, void* stream) {
+    if (!x || !on || !off || B < 0 || C <= 0 || (H & 1) || (W & 1)) return RNVP_E_INVALID;
+    long long n = (long long)B * C * H * W;
+    if (n == 0) return RNVP_OK;
+    k_restore<<<rnvp_grid(n, 256), 256, 0, (hipStream_t)stream>>>(on, off, x, C, H, W, n);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// logit transform (utils.py:33-72)
+// ---------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al. 2011), counter = (offset+i, 0, 0, 0), key = seed
+__device__ __forceinline__ float philox_uniform(uint64_t seed, uint64_t ctr) {
+    uint32_t c0 = (uint32_t)ctr, c1 = (uint32_t)(ctr >> 32), c2 = 0, c3 = 0;
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c1 = (uint32_t)p1;
+        c3 = (uint32_t)p0;
+        c0 = n0;
+        c2 = n2;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return (c0 >> 8) * (1.0f / 16777216.0f);   // [0, 1)
+}
+
+__device__ __forceinline__ float softplusf(float v) { return v > 20.f ? v : log1pf(expf(v)); }
+
+__global__ void k_logit_fwd(const float* __restrict__ x, const float* __restrict__ noise, uint64_t seed, uint64_t offset,
+                            float cst, float* __restrict__ y, float* __restrict__ logdet, int n) {
+    __shared__ double red[16];
+    const int b = blockIdx.x;
+    const long long base = (long long)b * n;
+    const float sp_pre = softplusf(-(float)(log((double)cst) - log(1.0 - (double)cst)));
+    double acc = 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        long long e = base + i;
+        float u = noise ? noise[e] : philox_uniform(seed, offset + (uint64_t)e);
+        float v = (x[e] * 255.f + u) / 256.f;
+        v = ((v * 2.f - 1.f) * cst + 1.f) / 2.f;
+        float l = logf(v) - logf(1.f - v);
+        y[e] = l;
+        acc += (double)(softplusf(l) + softplusf(-l) - sp_pre);
+    }
+    acc = block_sum(acc, red);
+    if (threadIdx.x == 0) logdet[b] = (float)acc;
+}
+
+extern "C" int rnvp_logit_fwd(const float* x, const float* noise, uint64_t seed, uint64_t offset, float constraint,
+                              float* y, float* logdet, int B, int n_per_sample, void* stream) {
+    if (!x || !y || !logdet || B < 0 || n_per_sample <= 0) return RNVP_E_INVALID;
+    if (B == 0) return RNVP_OK;
+    k_logit_fwd<<<B, 512, 0, (hipStream_t)stream>>>(x, noise, seed, offset, constraint, y, logdet, n_per_sample);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+__global__ void k_logit_inv(const float* __restrict__ x, float* __restrict__ y, float cst, long long n) {
+    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+        float v = 1.f / (expf(-x[e]) + 1.f);
+        y[e] = ((v * 2.f - 1.f) / cst + 1.f) / 2.f;
+    }
+}
+
+extern "C" int rnvp_logit_inv(const float* x, float* y, float constraint, long long n, void* stream) {
+    if (!x || !y || n < 0) return RNVP_E_INVALID;
+    if (n == 0) return RNVP_OK;
+    k_logit_inv<<<rnvp_grid(n, 256), 256, 0, (hipStream_t)stream>>>(x, y, constraint, n);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// prior log-prob (flow_realnvp.py:329-340; train.py:109 prior = N(0,1))
+// ---------------------------------------------------------------------------
+__global__ void k_prior(const float* __restrict__ z, const float* __restrict__ ldj, float* __restrict__ out, int n) {
+    __shared__ double red[16];
+    const int b = blockIdx.x;
+    const float* zb = z + (long long)b * n;
+    double acc = 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        float v = zb[i];
+        acc += (double)(-0.5f * v * v - 0.91893853320467274178f);
+    }
+    acc = block_sum(acc, red);
+    if (threadIdx.x == 0) out[b] = (float)(acc + (ldj ? (double)ldj[b] : 0.0));
+}
+
+extern "C" int rnvp_prior_logprob(const float* z, const float* ldj, float* out, int B, int n, void* stream) {
+    if (!z || !out || B < 0 || n <= 0) return RNVP_E_INVALID;
+    if (B == 0) return RNVP_OK;
+    k_prior<<<B, 512, 0, (hipStream_t)stream>>>(z, ldj, out, n);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+__global__ void k_prior_bwd(const float* __restrict__ z, const float* __restrict__ gout, float* __restrict__ gz, int n,
+                            long long total) {
+    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x)
+        gz[e] = -z[e] * gout[e / n];
+}
+
+extern "C" int rnvp_prior_logprob_bwd(const float* z, const float* gout, float* gz, int B, int n, void* stream) {
+    if (!z || !gout || !gz || B < 0 || n <= 0) return RNVP_E_INVALID;
+    long long total = (long long)B * n;
+    if (total == 0) return RNVP_OK;
+    k_prior_bwd<<<rnvp_grid(total, 256), 256, 0, (hipStream_t)stream>>>(z, gout, gz, n, total);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// BatchNorm running statistics (torch BatchNorm2d train-mode semantics)
+// ---------------------------------------------------------------------------
+__global__ void k_bn_running(const rnvp_bn_running* __restrict__ d, float mom) {
+    const rnvp_bn_running r = d[blockIdx.x];
+    for (int c = threadIdx.x; c < r.C; c += blockDim.x) {
+        double mean = r.sums[c] / r.count;
+        double var = r.sums[r.C + c] / r.count - mean * mean;
+        if (var < 0) var = 0;
+        double unb = r.count > 1 ? var * r.count / (r.count - 1) : var;
+        r.rmean[c] = (1.f - mom) * r.rmean[c] + mom * (float)mean;
+        r.rvar[c] = (1.f - mom) * r.rvar[c] + mom * (float)unb;
+    }
+    if (threadIdx.x == 0 && r.nbt) r.nbt[0] += 1;
+}
+
+extern "C" int rnvp_bn_running_update(const rnvp_bn_running* d, int n, float momentum, void* stream) {
+    if (n < 0 || (n > 0 && !d)) return RNVP_E_INVALID;
+    if (n == 0) return RNVP_OK;
+    k_bn_running<<<n, 256, 0, (hipStream_t)stream>>>(d, momentum);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// weight_scale regulariser (flow_realnvp.py:362-369): multi-tensor sum of squares
+// ---------------------------------------------------------------------------
+__global__ void k_sumsq(const rnvp_tensor_ref* __restrict__ refs, float* out) {
+    __shared__ double red[16];
+    const rnvp_tensor_ref r = refs[blockIdx.x];
+    double acc = 0;
+    for (long long i = threadIdx.x; i < r.n; i += blockDim.x) acc += (double)r.p[i] * r.p[i];
+    acc = block_sum(acc, red);
+    if (threadIdx.x == 0) atomicAdd(out, (float)acc);
+}
+
+extern "C" int rnvp_sumsq_multi(const rnvp_tensor_ref* refs, int n_refs, float* out, void* stream) {
+    if (!out || n_refs < 0 || (n_refs > 0 && !refs)) return RNVP_E_INVALID;
+    if (n_refs == 0) return RNVP_OK;
+    k_sumsq<<<n_refs, 256, 0, (hipStream_t)stream>>>(refs, out);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+__global__ void k_sumsq_bwd(const rnvp_tensor_ref* __restrict__ refs, const float* gout, float coef) {
+    const rnvp_tensor_ref r = refs[blockIdx.x];
+    const float s = 2.f * coef * gout[0];
+    for (long long i = threadIdx.x; i < r.n; i += blockDim.x) r.g[i] += s * r.p[i];
+}
+
+extern "C" int rnvp_sumsq_bwd_multi(const rnvp_tensor_ref* refs, int n_refs, const float* gout, float coef, void* stream) {
+    if (!gout || n_refs < 0 || (n_refs > 0 && !refs)) return RNVP_E_INVALID;
+    if (n_refs == 0) return RNVP_OK;
+    k_sumsq_bwd<<<n_refs, 256, 0, (hipStream_t)stream>>>(refs, gout, coef);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// fused Adam (torch.optim.Adam single-tensor semantics, coupled weight decay)
+// ---------------------------------------------------------------------------
+__global__ void k_step_inc(long long* step) { step[0] += 1; }
+
+__global__ void k_adam(float4* __restrict__ p, const float4* __restrict__ g, float4* __restrict__ m,
+                       float4* __restrict__ v, long long n4, const long long* step, float lr, float b1, float b2,
+                       float eps, float wd, const uint32_t* __restrict__ regm, float reg) {
+    __shared__ float sh[2];
+    if (threadIdx.x == 0) {
+        double t = (double)step[0];
+        double bc1 = 1.0 - pow((double)b1, t), bc2 = 1.0 - pow((double)b2, t);
+        sh[0] = (float)(lr / bc1);
+        sh[1] = (float)(1.0 / sqrt(bc2));
+    }
+    __syncthreads();
+    const float step_size = sh[0], inv_bc2s = sh[1];
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+        float4 pp = p[i], gg = g[i], mm = m[i], vv = v[i];
+        uint32_t rm = regm ? regm[i] : 0u;
+        float* pa = (float*)&pp; float* ga = (float*)&gg; float* ma = (float*)&mm; float* va = (float*)&vv;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float gr = ga[j] + wd * pa[j];
+            if ((rm >> (8 * j)) & 0xff) gr += 2.f * reg * pa[j];
+            ma[j] = ma[j] + (1.f - b1) * (gr - ma[j]);
+            va[j] = va[j] * b2 + (1.f - b2) * gr * gr;
+            float den = sqrtf(va[j]) * inv_bc2s + eps;
+            pa[j] = pa[j] - step_size * ma[j] / den;
+        }
+        p[i] = pp; m[i] = mm; v[i] = vv;
+    }
+}
+
+extern "C" int rnvp_adam_step(float* param, float* grad, float* exp_avg, float* exp_avg_sq, long long n,
+                              long long* step, float lr, float beta1, float beta2, float eps, float weight_decay,
+                              const uint8_t* reg_mask, float reg_coef, void* stream) {
+    if (!param || !grad || !exp_avg || !exp_avg_sq || !step || n < 0 || (n & 3)) return RNVP_E_INVALID;
+    if ((((uintptr_t)param) | ((uintptr_t)grad) | ((uintptr_t)exp_avg) | ((uintptr_t)exp_avg_sq)) & 15) return RNVP_E_INVALID;
+    if (reg_mask && (((uintptr_t)reg_mask) & 3)) return RNVP_E_INVALID;
+    hipStream_t s = (hipStream_t)stream;
+    k_step_inc<<<1, 1, 0, s>>>(step);
+    RNVP_LAUNCH_CHECK();
+    if (n == 0) return RNVP_OK;
+    long long n4 = n / 4;
+    k_adam<<<rnvp_grid(n4, 256, 8192), 256, 0, s>>>((float4*)param, (const float4*)grad, (float4*)exp_avg,
+                                                   (float4*)exp_avg_sq, n4, step, lr, beta1, beta2, eps, weight_decay,
+                                                   (const uint32_t*)reg_mask, reg_coef);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+__global__ void k_fill64(double* p, long long n, double v) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) p[i] = v;
+}
+
+extern "C" int rnvp_fill_f64(double* p, long long n, double v, void* stream) {
+    if (!p || n < 0) return RNVP_E_INVALID;
+    if (n == 0) return RNVP_OK;
+    k_fill64<<<rnvp_grid(n, 256), 256, 0, (hipStream_t)stream>>>(p, n, v);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}

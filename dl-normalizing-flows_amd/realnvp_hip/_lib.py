@@ -1,0 +1,149 @@
+"""ctypes binding of include/realnvp_hip.h (the C ABI of the HIP engine).
+
+The shared object is built in-tree (``csrc/Makefile`` -> ``librealnvp_hip.so``
+next to this file).  There is no fallback: if the library is missing or a
+call fails, a RuntimeError is raised.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librealnvp_hip.so")
+
+RNVP_F32, RNVP_BF16 = 0, 1
+
+vp = C.c_void_p
+i32 = C.c_int
+i64 = C.c_longlong
+f32 = C.c_float
+f64 = C.c_double
+
+
+class BNSrc(C.Structure):
+    _fields_ = [("sums", vp), ("count", f64), ("mean", vp), ("var", vp), ("gamma", vp), ("beta", vp), ("eps", f32)]
+
+
+class BNRunning(C.Structure):
+    _fields_ = [("sums", vp), ("count", f64), ("C", i32), ("pad", i32), ("rmean", vp), ("rvar", vp), ("nbt", vp)]
+
+
+class ConvArgs(C.Structure):
+    _fields_ = [("dtype", i32), ("B", i32), ("H", i32), ("W", i32), ("ks", i32),
+                ("x", vp), ("cs_in", i32), ("cin", i32),
+                ("w", vp), ("kp", i32),
+                ("y", vp), ("cs_out", i32), ("n", i32),
+                ("bias", vp), ("residual", vp), ("accumulate", i32),
+                ("pro_bn_relu", i32), ("pro", BNSrc),
+                ("out_sums", vp),
+                ("epi_relu_bn_bwd", i32), ("epi_x", vp), ("epi", BNSrc), ("epi_sums", vp)]
+
+
+class WgradArgs(C.Structure):
+    _fields_ = [("dtype", i32), ("B", i32), ("H", i32), ("W", i32), ("ks", i32),
+                ("x", vp), ("cs_in", i32), ("cin", i32),
+                ("pro_bn_relu", i32), ("pro", BNSrc),
+                ("dy", vp), ("cs_dy", i32), ("n", i32),
+                ("dw", vp), ("kp", i32), ("dbias", vp)]
+
+
+class BNBwdArgs(C.Structure):
+    _fields_ = [("dtype", i32), ("M", i64), ("C", i32), ("cs", i32),
+                ("g", vp), ("x", vp), ("bn", BNSrc), ("sums", vp),
+                ("dx", vp), ("residual", vp), ("accumulate", i32),
+                ("dgamma", vp), ("dbeta", vp)]
+
+
+class WNDesc(C.Structure):
+    _fields_ = [("v", vp), ("g", vp), ("wf", vp), ("wd", vp), ("norm", vp),
+                ("dw", vp), ("dv_off", i64), ("dg_off", i64),
+                ("cout", i32), ("cin", i32), ("ks", i32), ("cs_in", i32), ("kp_f", i32),
+                ("cs_out", i32), ("kp_d", i32), ("row0", i32)]
+
+
+class CouplingArgs(C.Structure):
+    _fields_ = [("kind", i32), ("B", i32), ("C", i32), ("H", i32), ("W", i32), ("mask_config", i32),
+                ("coupling_bn", i32), ("training", i32), ("dtype", i32),
+                ("momentum", f32), ("eps", f32),
+                ("x", vp),
+                ("in_gamma", vp), ("in_beta", vp), ("in_rmean", vp), ("in_rvar", vp), ("in_nbt", vp),
+                ("in_sums", vp),
+                ("h0", vp), ("cs_h0", i32),
+                ("st", vp), ("cs_st", i32),
+                ("scale", vp), ("scale_shift", vp),
+                ("u", vp), ("z", vp), ("out_sums", vp),
+                ("out_rmean", vp), ("out_rvar", vp), ("out_nbt", vp),
+                ("ldj_sample", vp), ("ldj_full", vp),
+                ("gz", vp), ("gl_full", vp), ("gl_sample", vp), ("gx", vp),
+                ("gst", vp), ("cs_gst", i32),
+                ("bwd_sums", vp), ("g_scale", vp), ("g_scale_shift", vp),
+                ("gh0", vp), ("cs_gh0", i32),
+                ("in_bwd_sums", vp), ("g_in_gamma", vp), ("g_in_beta", vp)]
+
+
+class TensorRef(C.Structure):
+    _fields_ = [("p", vp), ("g", vp), ("n", i64)]
+
+
+_SIGS = {
+    "rnvp_version": (i32, []),
+    "rnvp_status_string": (C.c_char_p, [i32]),
+    "rnvp_checkerboard_mask": (i32, [vp, i32, i32, vp]),
+    "rnvp_squeeze": (i32, [vp, vp, i32, i32, i32, i32, vp]),
+    "rnvp_undo_squeeze": (i32, [vp, vp, i32, i32, i32, i32, vp]),
+    "rnvp_factor_out": (i32, [vp, vp, vp, i32, i32, i32, i32, vp]),
+    "rnvp_restore": (i32, [vp, vp, vp, i32, i32, i32, i32, vp]),
+    "rnvp_logit_fwd": (i32, [vp, vp, C.c_uint64, C.c_uint64, f32, vp, vp, i32, i32, vp]),
+    "rnvp_logit_inv": (i32, [vp, vp, f32, i64, vp]),
+    "rnvp_prior_logprob": (i32, [vp, vp, vp, i32, i32, vp]),
+    "rnvp_prior_logprob_bwd": (i32, [vp, vp, vp, i32, i32, vp]),
+    "rnvp_bn_running_update": (i32, [vp, i32, f32, vp]),
+    "rnvp_conv2d": (i32, [C.POINTER(ConvArgs), vp]),
+    "rnvp_conv2d_wgrad": (i32, [C.POINTER(WgradArgs), vp]),
+    "rnvp_bn_bwd_apply": (i32, [C.POINTER(BNBwdArgs), vp]),
+    "rnvp_weight_norm_fwd": (i32, [vp, i32, i32, i32, vp]),
+    "rnvp_weight_norm_bwd": (i32, [vp, i32, i32, vp, vp]),
+    "rnvp_coupling_in_fwd": (i32, [C.POINTER(CouplingArgs), vp]),
+    "rnvp_coupling_out_fwd": (i32, [C.POINTER(CouplingArgs), vp]),
+    "rnvp_coupling_reverse": (i32, [C.POINTER(CouplingArgs), vp]),
+    "rnvp_coupling_out_bwd": (i32, [C.POINTER(CouplingArgs), vp]),
+    "rnvp_coupling_in_bwd": (i32, [C.POINTER(CouplingArgs), vp]),
+    "rnvp_sumsq_multi": (i32, [vp, i32, vp, vp]),
+    "rnvp_sumsq_bwd_multi": (i32, [vp, i32, vp, f32, vp]),
+    "rnvp_adam_step": (i32, [vp, vp, vp, vp, i64, vp, f32, f32, f32, f32, f32, vp, f32, vp]),
+    "rnvp_fill_f64": (i32, [vp, i64, f64, vp]),
+}
+
+EXPORTED = sorted(_SIGS)
+
+
+class _Lib:
+    def __init__(self, path=LIB_PATH):
+        if not os.path.exists(path):
+            raise RuntimeError("librealnvp_hip.so not built (%s); run __graft_entry__.build()" % path)
+        self.dll = C.CDLL(path)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(self.dll, name)
+            fn.restype = res
+            fn.argtypes = args
+            setattr(self, name[len("rnvp_"):], self._wrap(name, fn) if res is i32 and name != "rnvp_version" else fn)
+
+    def _wrap(self, name, fn):
+        dll = self.dll
+
+        def call(*args):
+            st = fn(*args)
+            if st != 0:
+                msg = dll.rnvp_status_string(st)
+                raise RuntimeError("%s failed: status %d (%s)" % (name, st, msg.decode() if msg else "?"))
+        call.__name__ = name
+        return call
+
+
+_lib = None
+
+
+def lib() -> _Lib:
+    global _lib
+    if _lib is None:
+        _lib = _Lib()
+    return _lib

@@ -1,0 +1,430 @@
+"""Per-coupling executor: sequences the C-ABI kernels of one affine coupling
+(modules_realnvp.py:239-370) and its s/t ResNet (36-194), forward, backward
+and inverse.
+
+Memory (all device, owned by torch tensors):
+  * WeightSet  (per engine x dtype, persistent): packed weight images wf/wd,
+    per-row norms, weight-norm descriptor table.
+  * Saved      (per forward call, or persistent in the trainer): net input h0,
+    every activation the backward needs, pre-out_bn u, fp64 BN batch sums.
+  * Scratch    (per engine x shape, persistent): activation gradients, the
+    pre-BN-apply temp, packed fp32 weight gradients, backward reductions.
+Parameter gradients go to a flat fp32 "grad block" laid out like the
+coupling's named_parameters() (frozen weight_g included, never written).
+"""
+import ctypes as C
+from collections import OrderedDict
+
+import torch
+
+from . import _lib
+from ._lib import (BNBwdArgs, BNRunning, BNSrc, ConvArgs, CouplingArgs, WgradArgs, WNDesc, RNVP_BF16, RNVP_F32)
+from .net import backward_program, build_program, chan_stride, round_up
+
+BN_EPS = 1e-5
+BN_MOMENTUM = 0.1
+
+DTYPES = {"fp32": (RNVP_F32, 4, torch.float32), "bf16": (RNVP_BF16, 2, torch.bfloat16)}
+
+
+def stream_ptr():
+    return torch.cuda.current_stream().cuda_stream
+
+
+class Arena:
+    """Bump allocator over one device tensor (256-B aligned slots)."""
+
+    def __init__(self):
+        self.slots = OrderedDict()
+        self.total = 0
+        self.buf = None
+
+    def add(self, name, nbytes):
+        assert name not in self.slots, name
+        self.slots[name] = (self.total, int(nbytes))
+        self.total = round_up(self.total + int(nbytes), 256)
+
+    def alloc(self, device, zero=False):
+        n = max(self.total, 256)
+        self.buf = (torch.zeros if zero else torch.empty)(n, dtype=torch.uint8, device=device)
+        self.base = self.buf.data_ptr()
+        return self
+
+    def ptr(self, name):
+        return self.base + self.slots[name][0]
+
+    def has(self, name):
+        return name in self.slots
+
+    def view(self, name, dtype, shape=None):
+        off, nb = self.slots[name]
+        t = self.buf[off:off + nb].view(dtype)
+        return t.view(shape) if shape is not None else t
+
+    def range_bytes(self, first, last):
+        """[start, end) byte range spanning slots first..last (in insertion order)."""
+        s = self.slots[first][0]
+        o, nb = self.slots[last]
+        return s, o + nb
+
+
+def _bn_src(sums, count, mean, var, gamma, beta):
+    return BNSrc(sums or None, float(count), mean or None, var or None, gamma or None, beta or None, BN_EPS)
+
+
+class CouplingEngine:
+    """Executor for one Checkerboard/Channelwise affine coupling module."""
+
+    def __init__(self, mod):
+        self.mod = mod
+        self.kind = 0 if mod.KIND == "ckbd" else 1
+        self.C = mod.in_out_dim
+        self.Cb = self.C if self.kind == 0 else self.C // 2
+        cin = 2 * self.C + 1 if self.kind == 0 else self.C
+        cout = 2 * self.Cb
+        hp = mod.hps
+        self.hp = hp
+        self.P = build_program("block.1.", cin, mod.mid_dim, cout, hp.res_blocks, hp.bottleneck, hp.skip,
+                               hp.weight_norm)
+        self.steps = backward_program(self.P)
+        self.cfg = 1 if mod.mask_config else 0
+        # grad-block layout == named_parameters() order
+        self.layout = OrderedDict()
+        off = 0
+        for n, p in mod.named_parameters():
+            self.layout[n] = (off, p.numel())
+            off += p.numel()
+        self.n_params = off
+        self._weights = {}
+        self._scratch = {}
+
+    # ------------------------------------------------------------------ params
+    def _tensors(self):
+        d = dict(self.mod.named_parameters())
+        d.update(dict(self.mod.named_buffers()))
+        return d
+
+    def _conv_names(self, spec):
+        p = spec.name + "conv."
+        if spec.wn:
+            return p + "weight_v", p + "weight_g", (p + "bias" if spec.bias else None)
+        return p + "weight", None, (p + "bias" if spec.bias else None)
+
+    def weights(self, dtype):
+        """WeightSet for dtype, (re)built when parameter storage moved."""
+        T = self._tensors()
+        key = tuple(T[n].data_ptr() for n in self.layout)
+        ws = self._weights.get(dtype)
+        if ws is not None and ws["key"] == key:
+            return ws
+        dt, esz, _ = DTYPES[dtype]
+        dev = next(iter(T.values())).device
+        ar = Arena()
+        geo = OrderedDict()
+        for name, spec in self.P.convs.items():
+            cs_in, cs_out = chan_stride(spec.cin), chan_stride(spec.cout)
+            kp_f = round_up(spec.ks * spec.ks * cs_in, 32)
+            kp_d = round_up(spec.ks * spec.ks * cs_out, 32)
+            geo[name] = (cs_in, cs_out, kp_f, kp_d)
+            ar.add("wf:" + name, spec.cout * kp_f * esz)
+            ar.add("wd:" + name, spec.cin * kp_d * esz)
+            ar.add("norm:" + name, spec.cout * 4)
+        ar.alloc(dev, zero=True)   # zero padding of the packed images, once
+        descs = []
+        row0 = 0
+        for name, spec in self.P.convs.items():
+            cs_in, cs_out, kp_f, kp_d = geo[name]
+            vn, gn, _ = self._conv_names(spec)
+            d = WNDesc()
+            d.v = T[vn].data_ptr()
+            d.g = T[gn].data_ptr() if gn else None
+            d.wf, d.wd, d.norm = ar.ptr("wf:" + name), ar.ptr("wd:" + name), ar.ptr("norm:" + name)
+            d.dw = None
+            d.dv_off = self.layout[vn][0]
+            d.dg_off = self.layout[gn][0] if (gn and spec.scale) else -1
+            d.cout, d.cin, d.ks, d.cs_in, d.kp_f, d.cs_out, d.kp_d, d.row0 = (
+                spec.cout, spec.cin, spec.ks, cs_in, kp_f, cs_out, kp_d, row0)
+            row0 += spec.cout
+            descs.append(d)
+        table = (WNDesc * len(descs))(*descs)
+        dtab = torch.frombuffer(bytearray(bytes(table)), dtype=torch.uint8).to(dev)
+        ws = dict(key=key, arena=ar, geo=geo, descs=descs, table=dtab, rows=row0, dtype=dtype)
+        self._weights[dtype] = ws
+        return ws
+
+    def prepare_weights(self, dtype):
+        ws = self.weights(dtype)
+        _lib.lib().weight_norm_fwd(ws["table"].data_ptr(), len(ws["descs"]), ws["rows"], DTYPES[dtype][0],
+                                   stream_ptr())
+        return ws
+
+    # ------------------------------------------------------------ workspaces
+    def alloc_saved(self, B, H, W, dtype, device, training):
+        esz = DTYPES[dtype][1]
+        M = B * H * W
+        ar = Arena()
+        ar.add("h0", M * chan_stride(self.P.buf_ch["h0"]) * esz)
+        for b, ch in self.P.buf_ch.items():
+            if b != "h0":
+                ar.add(b, M * chan_stride(ch) * esz)
+        ar.add("u", B * self.C * H * W * 4)
+        ar.add("in_sums", 2 * self.Cb * 8)
+        ar.add("out_sums", 2 * self.Cb * 8)
+        for bn, spec in self.P.bns.items():
+            ar.add("s:" + bn, 2 * spec.c * 8)
+        ar.alloc(device)
+        sv = dict(arena=ar, B=B, H=H, W=W, dtype=dtype, training=training)
+        # running-stat update table for the net BNs
+        if training and self.P.bns:
+            T = self._tensors()
+            rows = []
+            for bn, spec in self.P.bns.items():
+                r = BNRunning(ar.ptr("s:" + bn), float(M), spec.c, 0, T[bn + "running_mean"].data_ptr(),
+                              T[bn + "running_var"].data_ptr(), T[bn + "num_batches_tracked"].data_ptr())
+                rows.append(r)
+            tab = (BNRunning * len(rows))(*rows)
+            sv["bn_table"] = torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(device)
+            sv["bn_n"] = len(rows)
+        return sv
+
+    def scratch(self, B, H, W, dtype, device):
+        key = (B, H, W, dtype, str(device))
+        sc = self._scratch.get(key)
+        if sc is not None:
+            return sc
+        esz = DTYPES[dtype][1]
+        M = B * H * W
+        ar = Arena()
+        # zeroed every backward: dW images and the reductions (kept contiguous)
+        wsz = self.weights(dtype)
+        first = last = None
+        for name, spec in self.P.convs.items():
+            kp_f = wsz["geo"][name][2]
+            ar.add("dw:" + name, spec.cout * kp_f * 4)
+            first = first or "dw:" + name
+            last = "dw:" + name
+        ar.add("bwd_sums", 3 * self.Cb * 8)
+        ar.add("in_bwd_sums", 2 * self.Cb * 8)
+        last = "in_bwd_sums"
+        for bn, spec in self.P.bns.items():
+            ar.add("e:" + bn, 2 * spec.c * 8)
+            last = "e:" + bn
+        zr = ar.range_bytes(first, last)
+        for b, ch in self.P.buf_ch.items():
+            ar.add("g:" + b, M * chan_stride(ch) * esz)
+        cmax = max([chan_stride(s.cin) for s in self.P.convs.values()])
+        ar.add("gtmp", M * cmax * esz)
+        ar.alloc(device)
+        # weight-norm backward table (dw pointers into this scratch)
+        descs = []
+        for d, (name, spec) in zip(wsz["descs"], self.P.convs.items()):
+            e = WNDesc()
+            C.memmove(C.addressof(e), C.addressof(d), C.sizeof(WNDesc))
+            e.dw = ar.ptr("dw:" + name)
+            descs.append(e)
+        tab = (WNDesc * len(descs))(*descs)
+        sc = dict(arena=ar, zero=zr, wn_table=torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(device),
+                  wn_key=wsz["key"], wn_rows=wsz["rows"], n_wn=len(descs))
+        self._scratch[key] = sc
+        return sc
+
+    # --------------------------------------------------------------- helpers
+    def _coupling_args(self, T, x, B, H, W, dtype, training):
+        a = CouplingArgs()
+        a.kind, a.B, a.C, a.H, a.W = self.kind, B, self.C, H, W
+        a.mask_config, a.coupling_bn, a.training = self.cfg, int(self.hp.coupling_bn), int(training)
+        a.dtype = DTYPES[dtype][0]
+        a.momentum, a.eps = BN_MOMENTUM, BN_EPS
+        a.x = x.data_ptr()
+        a.in_gamma, a.in_beta = T["in_bn.weight"].data_ptr(), T["in_bn.bias"].data_ptr()
+        a.in_rmean, a.in_rvar = T["in_bn.running_mean"].data_ptr(), T["in_bn.running_var"].data_ptr()
+        a.in_nbt = T["in_bn.num_batches_tracked"].data_ptr()
+        a.scale, a.scale_shift = T["scale"].data_ptr(), T["scale_shift"].data_ptr()
+        a.out_rmean, a.out_rvar = T["out_bn.running_mean"].data_ptr(), T["out_bn.running_var"].data_ptr()
+        a.out_nbt = T["out_bn.num_batches_tracked"].data_ptr()
+        a.cs_h0 = chan_stride(self.P.buf_ch["h0"])
+        a.cs_st = chan_stride(self.P.buf_ch["st"])
+        return a
+
+    def _bn(self, T, bn, training, sums_ptr, M):
+        return _bn_src(sums_ptr if training else None, M, T[bn + "running_mean"].data_ptr(),
+                       T[bn + "running_var"].data_ptr(), T[bn + "weight"].data_ptr(), T[bn + "bias"].data_ptr())
+
+    def _net_forward(self, T, sv, ws, training, s):
+        L = _lib.lib()
+        ar = sv["arena"]
+        B, H, W = sv["B"], sv["H"], sv["W"]
+        M = B * H * W
+        dt = DTYPES[sv["dtype"]][0]
+        war = ws["arena"]
+        for op in self.P.ops:
+            spec = self.P.convs[op.conv]
+            cs_in, cs_out, kp_f, _ = ws["geo"][op.conv]
+            a = ConvArgs()
+            a.dtype, a.B, a.H, a.W, a.ks = dt, B, H, W, spec.ks
+            a.x, a.cs_in, a.cin = ar.ptr(op.x), cs_in, spec.cin
+            a.w, a.kp = war.ptr("wf:" + op.conv), kp_f
+            a.y, a.cs_out, a.n = ar.ptr(op.y), cs_out, spec.cout
+            _, _, bn_ = self._conv_names(spec)
+            a.bias = T[bn_].data_ptr() if bn_ else None
+            a.residual = ar.ptr(op.residual) if op.residual else None
+            a.accumulate = int(op.accumulate)
+            if op.pro_bn:
+                a.pro_bn_relu = 1
+                a.pro = self._bn(T, op.pro_bn, training, ar.ptr("s:" + op.pro_bn), M)
+            a.out_sums = ar.ptr("s:" + op.stats_bn) if (op.stats_bn and training) else None
+            L.conv2d(C.byref(a), s)
+
+    # ---------------------------------------------------------------- forward
+    def forward(self, x, training, dtype, full_ldj, saved=None, prepare=True, ldj_sample=None):
+        """x: [B,C,H,W] fp32 device tensor.  Returns (z, ldj, saved) where ldj
+        is the elementwise log_diag_J [B,C,H,W] (full_ldj) or this coupling's
+        per-sample sum [B] (accumulated into ldj_sample when given)."""
+        L = _lib.lib()
+        B, Cc, H, W = x.shape
+        assert Cc == self.C, "channel mismatch"
+        dev = x.device
+        s = stream_ptr()
+        ws = self.prepare_weights(dtype) if prepare else self.weights(dtype)
+        sv = saved if saved is not None else self.alloc_saved(B, H, W, dtype, dev, training)
+        ar = sv["arena"]
+        T = self._tensors()
+        z = torch.empty_like(x)
+        if ldj_sample is None:
+            ldj_sample = torch.zeros(B, device=dev, dtype=torch.float32)
+        ldj_full = torch.empty_like(x) if full_ldj else None
+        if training:
+            s0, e0 = ar.range_bytes("in_sums", list(ar.slots)[-1])
+            ar.buf[s0:e0].zero_()
+        a = self._coupling_args(T, x, B, H, W, dtype, training)
+        a.in_sums = ar.ptr("in_sums")
+        a.h0 = ar.ptr("h0")
+        L.coupling_in_fwd(C.byref(a), s)
+        self._net_forward(T, sv, ws, training, s)
+        if training and "bn_table" in sv:
+            L.bn_running_update(sv["bn_table"].data_ptr(), sv["bn_n"], BN_MOMENTUM, s)
+        a.st = ar.ptr("st")
+        a.u, a.z = ar.ptr("u"), z.data_ptr()
+        a.out_sums = ar.ptr("out_sums")
+        a.ldj_sample = ldj_sample.data_ptr()
+        a.ldj_full = ldj_full.data_ptr() if full_ldj else None
+        L.coupling_out_fwd(C.byref(a), s)
+        sv["x"] = x
+        return z, (ldj_full if full_ldj else ldj_sample), sv
+
+    # ---------------------------------------------------------------- inverse
+    def reverse(self, x, training, dtype):
+        L = _lib.lib()
+        B, Cc, H, W = x.shape
+        s = stream_ptr()
+        ws = self.prepare_weights(dtype)
+        sv = self.alloc_saved(B, H, W, dtype, x.device, training)
+        ar = sv["arena"]
+        T = self._tensors()
+        if training:
+            s0, e0 = ar.range_bytes("in_sums", list(ar.slots)[-1])
+            ar.buf[s0:e0].zero_()
+        a = self._coupling_args(T, x, B, H, W, dtype, training)
+        a.in_sums = ar.ptr("in_sums")
+        a.h0 = ar.ptr("h0")
+        L.coupling_in_fwd(C.byref(a), s)
+        self._net_forward(T, sv, ws, training, s)
+        if training and "bn_table" in sv:
+            L.bn_running_update(sv["bn_table"].data_ptr(), sv["bn_n"], BN_MOMENTUM, s)
+        out = torch.empty_like(x)
+        ldj = torch.empty_like(x)
+        a.st = ar.ptr("st")
+        a.z = out.data_ptr()
+        a.ldj_full = ldj.data_ptr()
+        L.coupling_reverse(C.byref(a), s)
+        return out, ldj
+
+    # --------------------------------------------------------------- backward
+    def backward(self, sv, gz, gl_full, gl_sample, grad_block, gx=None):
+        """Returns dL/dx; parameter gradients are written into grad_block
+        (flat fp32, zeroed by the caller; scale/bias grads accumulate)."""
+        L = _lib.lib()
+        x = sv["x"]
+        B, H, W, dtype, training = sv["B"], sv["H"], sv["W"], sv["dtype"], sv["training"]
+        M = B * H * W
+        dt = DTYPES[dtype][0]
+        s = stream_ptr()
+        T = self._tensors()
+        ws = self.weights(dtype)
+        sc = self.scratch(B, H, W, dtype, x.device)
+        if sc["wn_key"] != ws["key"]:
+            self._scratch.pop((B, H, W, dtype, str(x.device)))
+            sc = self.scratch(B, H, W, dtype, x.device)
+        ar, sar, war = sv["arena"], sc["arena"], ws["arena"]
+        z0, z1 = sc["zero"]
+        sar.buf[z0:z1].zero_()
+        gbase = grad_block.data_ptr()
+
+        def gp(name):
+            return gbase + 4 * self.layout[name][0]
+
+        if gx is None:
+            gx = torch.empty_like(x)
+        a = self._coupling_args(T, x, B, H, W, dtype, training)
+        a.in_sums = ar.ptr("in_sums")
+        a.st = ar.ptr("st")
+        a.u = ar.ptr("u")
+        a.out_sums = ar.ptr("out_sums")
+        a.gz = gz.data_ptr()
+        a.gl_full = gl_full.data_ptr() if gl_full is not None else None
+        a.gl_sample = gl_sample.data_ptr() if gl_sample is not None else None
+        a.gx = gx.data_ptr()
+        a.gst, a.cs_gst = sar.ptr("g:st"), chan_stride(self.P.buf_ch["st"])
+        a.bwd_sums = sar.ptr("bwd_sums")
+        a.g_scale, a.g_scale_shift = gp("scale"), gp("scale_shift")
+        L.coupling_out_bwd(C.byref(a), s)
+
+        for st in self.steps:
+            op = st.op
+            spec = self.P.convs[op.conv]
+            cs_in, cs_out, kp_f, kp_d = ws["geo"][op.conv]
+            _, _, bname = self._conv_names(spec)
+            if st.kind == "dgrad":
+                c = ConvArgs()
+                c.dtype, c.B, c.H, c.W, c.ks = dt, B, H, W, spec.ks
+                c.x, c.cs_in, c.cin = sar.ptr(st.gy), cs_out, spec.cout
+                c.w, c.kp = war.ptr("wd:" + op.conv), kp_d
+                c.y = sar.ptr(st.tmp if st.tmp else st.gx)
+                c.cs_out, c.n = cs_in, spec.cin
+                c.residual = sar.ptr(st.residual) if st.residual else None
+                c.accumulate = int(st.accumulate)
+                if op.pro_bn:
+                    c.epi_relu_bn_bwd = 1
+                    c.epi_x = ar.ptr(op.x)
+                    c.epi = self._bn(T, op.pro_bn, training, ar.ptr("s:" + op.pro_bn), M)
+                    c.epi_sums = sar.ptr("e:" + op.pro_bn)
+                L.conv2d(C.byref(c), s)
+            elif st.kind == "bn_apply":
+                bn = op.pro_bn
+                c = BNBwdArgs()
+                c.dtype, c.M, c.C, c.cs = dt, M, spec.cin, cs_in
+                c.g, c.x = sar.ptr(st.tmp), ar.ptr(op.x)
+                c.bn = self._bn(T, bn, training, ar.ptr("s:" + bn), M)
+                c.sums = sar.ptr("e:" + bn)
+                c.dx = sar.ptr(st.gx)
+                c.residual = sar.ptr(st.residual) if st.residual else None
+                c.accumulate = int(st.accumulate)
+                c.dgamma, c.dbeta = gp(bn + "weight"), gp(bn + "bias")
+                L.bn_bwd_apply(C.byref(c), s)
+            else:
+                c = WgradArgs()
+                c.dtype, c.B, c.H, c.W, c.ks = dt, B, H, W, spec.ks
+                c.x, c.cs_in, c.cin = ar.ptr(op.x), cs_in, spec.cin
+                if op.pro_bn:
+                    c.pro_bn_relu = 1
+                    c.pro = self._bn(T, op.pro_bn, training, ar.ptr("s:" + op.pro_bn), M)
+                c.dy, c.cs_dy, c.n = sar.ptr(st.gy), cs_out, spec.cout
+                c.dw, c.kp = sar.ptr("dw:" + op.conv), kp_f
+                c.dbias = gp(bname) if bname else None
+                L.conv2d_wgrad(C.byref(c), s)
+        L.weight_norm_bwd(sc["wn_table"].data_ptr(), sc["n_wn"], sc["wn_rows"], gbase, s)
+        a.gh0, a.cs_gh0 = sar.ptr("g:h0"), chan_stride(self.P.buf_ch["h0"])
+        a.in_bwd_sums = sar.ptr("in_bwd_sums")
+        a.g_in_gamma, a.g_in_beta = gp("in_bn.weight"), gp("in_bn.bias")
+        L.coupling_in_bwd(C.byref(a), s)
+        return gx

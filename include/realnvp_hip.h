@@ -1,0 +1,213 @@
+/*
+ * realnvp_hip.h -- C ABI of the MI355X (gfx950) RealNVP coupling-layer engine.
+ *
+ * The reference (alisher-turubayev/dl-normalizing-flows) has no FFI: its hot
+ * path is the Python nn.Module API of flow_realnvp.RealNVP and
+ * modules_realnvp.{Checkerboard,Channelwise}AffineCoupling.  This header is
+ * the boundary those modules bind to (via ctypes): plain
+ * pointers, sizes and a hipStream_t passed as void*.  Every entry point
+ *   - is stream-ordered: no host synchronisation, no allocation (HIP-graph
+ *     capture safe);
+ *   - returns 0 on success, a positive hipError_t from the launch, or a
+ *     negative RNVP_E_* code for invalid arguments (nothing is launched then);
+ *   - never takes ownership: the caller (PyTorch's caching allocator in the
+ *     Python host) owns every buffer, including workspaces.
+ *
+ * Layouts: "flow" tensors (x, z, log|det J|) are NCHW fp32 exactly as in the
+ * reference.  "net" tensors (the s/t ResNet activations) are NHWC with a
+ * padded channel stride `cs` (multiple of 8), dtype RNVP_F32 (parity mode)
+ * or RNVP_BF16 (perf mode, fp32 accumulation).  Reductions that feed batch
+ * statistics accumulate fp64 sums: layout [2*C] = {sum x, sum x^2}.
+ */
+#ifndef REALNVP_HIP_H
+#define REALNVP_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { RNVP_F32 = 0, RNVP_BF16 = 1 };
+enum { RNVP_OK = 0, RNVP_E_INVALID = -1, RNVP_E_UNSUPPORTED = -2 };
+
+/* ---- version / capabilities ------------------------------------------- */
+int rnvp_version(void);
+const char* rnvp_status_string(int status);
+
+/* ---- index maps (bit-exact permutations) --------------------------------
+ * replace AbstractCoupling.build_mask   modules_realnvp.py:211-226
+ *         RealNVP.squeeze/undo_squeeze  flow_realnvp.py:121-135
+ *         RealNVP.factor_out/restore    flow_realnvp.py:167-193 (the 0/1
+ *         order_matrix conv of 139-165 is the permutation implemented here)
+ * Shapes are those of the *larger* tensor: squeeze/undo_squeeze take the
+ * [B,C,H,W] un-squeezed shape; factor_out/restore the [B,C,H,W] full shape
+ * (on/off are [B,2C,H/2,W/2]). */
+int rnvp_checkerboard_mask(float* mask, int size, int config, void* stream);
+int rnvp_squeeze(const float* x, float* y, int B, int C, int H, int W, void* stream);
+int rnvp_undo_squeeze(const float* y, float* x, int B, int C, int H, int W, void* stream);
+int rnvp_factor_out(const float* x, float* on, float* off, int B, int C, int H, int W, void* stream);
+int rnvp_restore(const float* on, const float* off, float* x, int B, int C, int H, int W, void* stream);
+
+/* ---- logit transform (utils.py:33-72) ----------------------------------
+ * y = logit(((x*255+u)/256*2-1)*c+1)/2), logdet[b] = sum softplus(y)+softplus(-y)-softplus(-logit(c)).
+ * u = noise[i] when noise != NULL, else a counter-based Philox4x32-10 uniform
+ * in [0,1) keyed by (seed, offset + i).  n_per_sample = C*H*W. */
+int rnvp_logit_fwd(const float* x, const float* noise, uint64_t seed, uint64_t offset, float constraint,
+                   float* y, float* logdet, int B, int n_per_sample, void* stream);
+int rnvp_logit_inv(const float* x, float* y, float constraint, long long n, void* stream);
+
+/* ---- prior log-prob and per-sample reduction (flow_realnvp.py:329-340) --
+ * out[b] = ldj[b] + sum_i (-z_i^2/2 - log(2 pi)/2)       (N(0,1) prior)
+ * bwd: gz_i = -z_i * gout[b] */
+int rnvp_prior_logprob(const float* z, const float* ldj, float* out, int B, int n_per_sample, void* stream);
+int rnvp_prior_logprob_bwd(const float* z, const float* gout, float* gz, int B, int n_per_sample, void* stream);
+
+/* ---- batch-norm statistic sources -------------------------------------- */
+typedef struct rnvp_bn_src {
+    const double* sums;   /* [2*C] {sum, sum of squares} of the batch, or NULL */
+    double count;         /* elements per channel behind sums */
+    const float* mean;    /* running mean (used when sums == NULL) */
+    const float* var;     /* running var */
+    const float* gamma;   /* affine weight, NULL = 1 */
+    const float* beta;    /* affine bias, NULL = 0 */
+    float eps;
+} rnvp_bn_src;
+
+/* running-stat update of nn.BatchNorm2d in train mode, for n BN sites at once.
+ * rm = (1-mom) rm + mom mean; rv = (1-mom) rv + mom var*count/(count-1); nbt += 1 */
+typedef struct rnvp_bn_running {
+    const double* sums; double count; int C; int pad;
+    float* rmean; float* rvar; long long* nbt;
+} rnvp_bn_running;
+int rnvp_bn_running_update(const rnvp_bn_running* descs_device, int n, float momentum, void* stream);
+
+/* ---- s/t ResNet convolution (MFMA implicit GEMM) -----------------------
+ * replaces WeightNormConv2d.forward (modules_realnvp.py:64-71) inside
+ * ResidualModule/ResidualBlock (73-194) with the surrounding
+ * BatchNorm2d+ReLU fused into the operand load and bias / residual add /
+ * skip accumulation / BN statistics fused into the epilogue.
+ * y[m, n] (+)= sum_k act(x)[m + tap(k), ci(k)] * w[n, k] (+ bias[n]) (+ residual[m, n])
+ * act = relu(bn(x)) when pro_bn_relu, identity otherwise; zero padding is
+ * applied AFTER act (as nn.Conv2d pads its input).  k = (ky*ks+kx)*cs_in + ci.
+ * epi_relu_bn_bwd (used for the data gradient): the result g is multiplied
+ * by [relu(bn(epi_x)) > 0] before being stored, and epi_sums accumulates
+ * {sum g, sum g*xhat} per output channel. */
+typedef struct rnvp_conv_args {
+    int dtype;
+    int B, H, W, ks;
+    const void* x; int cs_in; int cin;
+    const void* w; int kp;              /* packed weights [n][kp], kp % 32 == 0 */
+    void* y; int cs_out; int n;
+    const float* bias;
+    const void* residual;
+    int accumulate;
+    int pro_bn_relu; rnvp_bn_src pro;
+    double* out_sums;
+    int epi_relu_bn_bwd; const void* epi_x; rnvp_bn_src epi; double* epi_sums;
+} rnvp_conv_args;
+int rnvp_conv2d(const rnvp_conv_args* a, void* stream);
+
+/* weight gradient: dw[n, k] += sum_m dy[m, n] * act(x)[m + tap(k), ci(k)]
+ * (fp32 atomics, dw must be zeroed by the caller), dbias[n] += sum_m dy[m, n]. */
+typedef struct rnvp_wgrad_args {
+    int dtype;
+    int B, H, W, ks;
+    const void* x; int cs_in; int cin;
+    int pro_bn_relu; rnvp_bn_src pro;
+    const void* dy; int cs_dy; int n;
+    float* dw; int kp;
+    float* dbias;
+} rnvp_wgrad_args;
+int rnvp_conv2d_wgrad(const rnvp_wgrad_args* a, void* stream);
+
+/* batch-norm backward apply (train mode), the second half of BN backward:
+ * dx = gamma*rstd*(g - sum_g/M - xhat * sum_gxhat/M) (+ residual) (+= dx if accumulate)
+ * also writes dgamma = sum_gxhat, dbeta = sum_g (when non-NULL) */
+typedef struct rnvp_bn_bwd_args {
+    int dtype; long long M; int C; int cs;
+    const void* g; const void* x; rnvp_bn_src bn; const double* sums;
+    void* dx; const void* residual; int accumulate;
+    float* dgamma; float* dbeta;
+} rnvp_bn_bwd_args;
+int rnvp_bn_bwd_apply(const rnvp_bn_bwd_args* a, void* stream);
+
+/* weight normalisation (torch.nn.utils.weight_norm dim=0, modules_realnvp.py:53-59)
+ * w = g * v / ||v||, packed into the forward layout wf[co][(ky*ks+kx)*cs_in+ci]
+ * and the flipped, transposed data-gradient layout wd[ci][(ky'*ks+kx')*cs_out+co]
+ * (w[co][ci][ks-1-ky'][ks-1-kx']).  g == NULL means a plain conv (w = v).
+ * bwd: dv = (g/|v|)(dw - (v.dw/|v|^2) v), dg = v.dw/|v| from the packed dw,
+ * written at grad_base + dv_off / dg_off (elements; dg_off < 0 = frozen g). */
+typedef struct rnvp_wn_desc {
+    const float* v; const float* g;
+    void* wf; void* wd; float* norm;
+    const float* dw;                   /* packed [cout][kp_f] fp32 (bwd) */
+    long long dv_off; long long dg_off;
+    int cout, cin, ks, cs_in, kp_f, cs_out, kp_d;
+    int row0;                          /* first global row (prefix sum of cout) */
+} rnvp_wn_desc;
+int rnvp_weight_norm_fwd(const rnvp_wn_desc* descs_device, int n_desc, int total_rows, int dtype, void* stream);
+int rnvp_weight_norm_bwd(const rnvp_wn_desc* descs_device, int n_desc, int total_rows, float* grad_base, void* stream);
+
+/* ---- affine coupling (modules_realnvp.py:239-370) -----------------------
+ * kind 0 = CheckerboardAffineCoupling, 1 = ChannelwiseAffineCoupling.
+ * Cb = channels seen by in_bn/out_bn: C (ckbd) or C/2 (chan).
+ * Net input h0 = relu(cat(bn_in(xm), -bn_in(xm)[, mask])) with xm = x*mask
+ * (ckbd, 2C+1 channels) or the "off" half (chan, C channels).  Net output
+ * st = [shift | log_rescale] (2*Cb channels). */
+typedef struct rnvp_coupling_args {
+    int kind, B, C, H, W, mask_config, coupling_bn, training, dtype;
+    float momentum, eps;
+    const float* x;                       /* coupling input (reverse: the output) */
+    const float* in_gamma; const float* in_beta;
+    float* in_rmean; float* in_rvar; long long* in_nbt;
+    double* in_sums;                      /* [2*Cb] */
+    void* h0; int cs_h0;
+    const void* st; int cs_st;
+    const float* scale; const float* scale_shift;
+    float* u;                             /* pre-out_bn value, [B,C,H,W] */
+    float* z;                             /* output [B,C,H,W] */
+    double* out_sums;                     /* [2*Cb] */
+    float* out_rmean; float* out_rvar; long long* out_nbt;
+    float* ldj_sample;                    /* [B], += */
+    float* ldj_full;                      /* [B,C,H,W] or NULL, written */
+    /* backward */
+    const float* gz;                      /* [B,C,H,W] */
+    const float* gl_full;                 /* [B,C,H,W] or NULL */
+    const float* gl_sample;               /* [B] used when gl_full == NULL */
+    float* gx;                            /* [B,C,H,W] */
+    void* gst; int cs_gst;
+    double* bwd_sums;                     /* [3*Cb] */
+    float* g_scale; float* g_scale_shift; /* += */
+    const void* gh0; int cs_gh0;
+    double* in_bwd_sums;                  /* [2*Cb] */
+    float* g_in_gamma; float* g_in_beta;  /* written */
+} rnvp_coupling_args;
+int rnvp_coupling_in_fwd(const rnvp_coupling_args* a, void* stream);   /* in_sums must be zeroed */
+int rnvp_coupling_out_fwd(const rnvp_coupling_args* a, void* stream);  /* out_sums must be zeroed */
+int rnvp_coupling_reverse(const rnvp_coupling_args* a, void* stream);  /* z = inverse(x) */
+int rnvp_coupling_out_bwd(const rnvp_coupling_args* a, void* stream);  /* bwd_sums zeroed; writes gx, gst */
+int rnvp_coupling_in_bwd(const rnvp_coupling_args* a, void* stream);   /* in_bwd_sums zeroed; gx += */
+
+/* ---- regulariser and optimizer ------------------------------------------
+ * weight_scale = sum over tensors of sum p^2  (flow_realnvp.py:362-369);
+ * out must be zeroed.  bwd: grad_i += 2 * gout * p_i. */
+typedef struct rnvp_tensor_ref { float* p; float* g; long long n; } rnvp_tensor_ref;
+int rnvp_sumsq_multi(const rnvp_tensor_ref* refs_device, int n_refs, float* out, void* stream);
+int rnvp_sumsq_bwd_multi(const rnvp_tensor_ref* refs_device, int n_refs, const float* gout, float coef, void* stream);
+
+/* torch.optim.Adam step (coupled L2 weight decay, train.py:134) over a flat
+ * fp32 parameter arena.  step is a device int64 incremented by this call;
+ * reg_mask (optional, uint8 per element) adds reg_coef*2*p to the gradient
+ * of the weight_g/scale parameters (the 5e-5*weight_scale term, train.py:194). */
+int rnvp_adam_step(float* param, float* grad, float* exp_avg, float* exp_avg_sq, long long n,
+                   long long* step, float lr, float beta1, float beta2, float eps, float weight_decay,
+                   const uint8_t* reg_mask, float reg_coef, void* stream);
+
+/* misc */
+int rnvp_fill_f64(double* p, long long n, double v, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,115 @@
+"""CPU-side checks of the drop-in boundary (no GPU needed)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT, load_golden
+
+HEADER = os.path.join(ROOT, "include", "realnvp_hip.h")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(rnvp_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    from realnvp_hip._lib import LIB_PATH, EXPORTED
+    assert os.path.exists(LIB_PATH), "build the HIP library first (__graft_entry__.build())"
+    dll = ctypes.CDLL(LIB_PATH)
+    decl = declared_symbols()
+    assert len(decl) >= 25
+    for s in decl:
+        assert hasattr(dll, s), s
+    # the ctypes binding covers exactly the declared ABI
+    assert sorted(EXPORTED) == decl
+    assert dll.rnvp_version() >= 100
+
+
+def test_invalid_arguments_return_status_without_launch():
+    from realnvp_hip._lib import LIB_PATH
+    dll = ctypes.CDLL(LIB_PATH)
+    dll.rnvp_squeeze.restype = ctypes.c_int
+    # NULL pointers / odd sizes are rejected before any HIP call
+    assert dll.rnvp_squeeze(None, None, 1, 1, 2, 2, None) == -1
+    x = ctypes.c_float(0)
+    assert dll.rnvp_squeeze(ctypes.byref(x), ctypes.byref(x), 1, 1, 3, 2, None) == -1
+    dll.rnvp_status_string.restype = ctypes.c_char_p
+    assert dll.rnvp_status_string(-1) == b"invalid argument"
+
+
+def _hp(bd, rb, bott=True, skip=True, wn=True, cbn=True):
+    import utils
+    return utils.Hyperparameters(bd, rb, bott, skip, wn, cbn)
+
+
+def test_state_dict_layout_matches_reference_spec():
+    import flow_realnvp
+    import realnvp_oracle as O
+    for size, bd, rb in ((32, 8, 1), (64, 32, 4), (32, 4, 0)):
+        m = flow_realnvp.RealNVP(3, size, torch.distributions.Normal(torch.tensor(0.), torch.tensor(1.)), _hp(bd, rb))
+        e = O.flow_spec_entries(O.FlowSpec(3, size, O.HP(bd, rb)))
+        sd = m.state_dict()
+        assert list(sd.keys()) == [k for k, _, _ in e]
+        assert all(tuple(sd[k].shape) == tuple(s) for k, s, _ in e)
+        assert [n for n, _ in m.named_parameters()] == O.param_names(e)
+        assert [n for n, p in m.named_parameters() if p.requires_grad] == O.trainable_names(e)
+
+
+def test_default_init_draws_like_reference():
+    import flow_realnvp
+    g = load_golden("init_seed0.npz")
+    for name, size, bd, rb, bott in (("m32_d8_r1", 32, 8, 1, True), ("m16_d4_r2_nobott", 16, 4, 2, False)):
+        torch.manual_seed(0)
+        m = flow_realnvp.RealNVP(3, size, torch.distributions.Normal(torch.tensor(0.), torch.tensor(1.)),
+                                 _hp(bd, rb, bott))
+        sd = m.state_dict()
+        assert list(sd.keys()) == list(g[name + ".keys"])
+        s = np.array([float(v.double().sum()) for v in sd.values()])
+        s2 = np.array([float(v.double().pow(2).sum()) for v in sd.values()])
+        np.testing.assert_allclose(s, g[name + ".sum"], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(s2, g[name + ".sumsq"], rtol=1e-5, atol=1e-6)
+
+
+def test_order_matrix_and_mask_match_reference():
+    import flow_realnvp
+    import modules_realnvp
+    g = load_golden("index_maps.npz")
+    m = flow_realnvp.RealNVP.__new__(flow_realnvp.RealNVP)
+    for C in (3, 6, 12, 24):
+        assert np.array_equal(flow_realnvp.RealNVP.order_matrix(m, C).numpy(), g["order_matrix_%d" % C])
+    c = modules_realnvp.CheckerboardAffineCoupling(3, 8, 8, 1., _hp(8, 1))
+    for size in (2, 4, 8, 64):
+        for cfg in (0, 1):
+            assert np.array_equal(c.build_mask(size, float(cfg)).numpy(), g["mask_%d_%d" % (size, cfg)])
+
+
+def test_cpu_tensors_fail_loudly():
+    import modules_realnvp
+    c = modules_realnvp.CheckerboardAffineCoupling(3, 8, 8, 1., _hp(8, 1))
+    with pytest.raises(RuntimeError, match="HIP device"):
+        c(torch.zeros(2, 3, 8, 8))
+
+
+def test_backward_program_is_well_formed():
+    from realnvp_hip.net import backward_program, build_program
+    for rb in (0, 1, 4):
+        for bott in (True, False):
+            for skip in (True, False):
+                P = build_program("block.1.", 7, 32, 6, rb, bott, skip, True)
+                steps = backward_program(P)
+                # every conv gets one wgrad and one dgrad
+                assert sum(s.kind == "wgrad" for s in steps) == len(P.ops)
+                assert sum(s.kind == "dgrad" for s in steps) == len(P.ops)
+                # every gradient buffer is written before it is read as dy
+                written = {"g:st"}
+                for s in steps:
+                    if s.kind in ("dgrad", "wgrad"):
+                        assert s.gy in written, (rb, bott, skip, s)
+                    if s.gx:
+                        written.add(s.gx)
+                assert "g:h0" in written

@@ -263,3 +263,22 @@ if __name__ == "__main__":
         coupling_goldens()
     if "model" in which:
         model_goldens()
+
+
+def init_golden():
+    """Per-key checksums of the reference's default init under torch.manual_seed(0)."""
+    d = {}
+    for name, size, bd, rb in (("m32_d8_r1", 32, 8, 1), ("m16_d4_r2_nobott", 16, 4, 2)):
+        hp = hps(bd, rb, bottleneck=(name.find("nobott") < 0))
+        torch.manual_seed(0)
+        prior = D.Normal(torch.tensor(0.0), torch.tensor(1.0), validate_args=False)
+        model = flow_realnvp.RealNVP(3, size, prior, hp)
+        keys = list(model.state_dict().keys())
+        d[name + ".keys"] = np.array(keys)
+        d[name + ".sum"] = np.array([float(v.double().sum()) for v in model.state_dict().values()])
+        d[name + ".sumsq"] = np.array([float(v.double().pow(2).sum()) for v in model.state_dict().values()])
+    save("init_seed0.npz", d)
+
+
+if __name__ == "__main__" and "init" in sys.argv[1:]:
+    init_golden()
