@@ -1,0 +1,241 @@
+"""RealNVP 64x64x3 NLL training throughput on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+One step = the train.py:176-200 body on synthetic data: logit_transform of a
+pixel batch (device noise), RealNVP forward (log_prob + weight_scale),
+loss = -mean(log_prob+logdet) + 5e-5*weight_scale, backward, Adam.  Config 1
+of BASELINE.json: 64x64x3, 4 res-blocks, base-dim 32, batch 64 per GPU,
+s/t network in bf16 with fp32 accumulation (couplings, log-det, BN stats,
+master weights and Adam in fp32).  Data parallel over RCCL for N > 1 (weak
+scaling: 64 images per GPU).
+
+Prints ONE JSON line (rank 0) with images/sec (whole job), bits/dim, the
+per-kernel roofline of the dominant kernel family and the CPU oracle timed
+on this host.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "dl-normalizing-flows_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA
+F32_PEAK_TFLOPS = 157.3        # f32 MFMA
+# algorithmic bytes / image / training step at config 1
+ALG_BYTES_PER_IMG = 292.33e6
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=64, help="images per GPU")
+    p.add_argument("--size", type=int, default=64)
+    p.add_argument("--res-blocks", type=int, default=4)
+    p.add_argument("--base-dim", type=int, default=32)
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-batch", type=int, default=16)
+    p.add_argument("--cpu-steps", type=int, default=2)
+    p.add_argument("--seed", type=int, default=0)
+    return p.parse_args()
+
+
+def synthetic_pixels(B, C, S, seed):
+    """raw pixels k/255, k ~ U{0..255} (ToTensor semantics)"""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    k = rng.integers(0, 256, size=(B, C, S, S))
+    return torch.from_numpy((k / 255.0).astype(np.float32))
+
+
+def kernel_roofline(trainer):
+    """One instrumented eager step: HIP events around every engine launch
+    (recorded on the launch stream).  Returns per-family totals and the
+    roofline object of the dominant (largest total time) family."""
+    from realnvp_hip import engine as E
+    E.PROFILE = []
+    torch.cuda.synchronize()
+    trainer.step_eager()
+    torch.cuda.synchronize()
+    fam = {}
+    for f, nb, fl, e0, e1 in E.PROFILE:
+        ms = e0.elapsed_time(e1)
+        d = fam.setdefault(f, dict(ms=0.0, bytes=0.0, flops=0.0, launches=0))
+        d["ms"] += ms
+        d["bytes"] += nb
+        d["flops"] += fl
+        d["launches"] += 1
+    E.PROFILE = None
+    dom = max(fam, key=lambda k: fam[k]["ms"])
+    d = fam[dom]
+    avg_ms = d["ms"] / d["launches"]
+    bytes_per_launch = d["bytes"] / d["launches"]
+    flops_per_launch = d["flops"] / d["launches"]
+    gbs = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+    tfs = flops_per_launch / (avg_ms * 1e-3) / 1e12
+    peak_tf = BF16_PEAK_TFLOPS if trainer.dtype == "bf16" else F32_PEAK_TFLOPS
+    # bound: whichever roof the family's arithmetic intensity sits under
+    ai = d["flops"] / max(d["bytes"], 1.0)
+    ridge = peak_tf * 1e12 / (HBM_PEAK_GBS * 1e9)
+    if ai < ridge:
+        roof = dict(bound="hbm", achieved=round(gbs, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                    frac=round(gbs / HBM_PEAK_GBS, 4))
+    else:
+        roof = dict(bound="mfma", achieved=round(tfs, 2), peak=peak_tf, unit="TFLOP/s",
+                    frac=round(tfs / peak_tf, 4))
+    roof.update(kernel=dom, launches_per_step=d["launches"], avg_launch_us=round(avg_ms * 1e3, 2),
+                alg_bytes_per_launch=int(bytes_per_launch), flops_per_launch=int(flops_per_launch),
+                traffic=None)
+    families = {k: dict(ms=round(v["ms"], 3), launches=v["launches"],
+                        gbs=round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1),
+                        tflops=round(v["flops"] / max(v["ms"], 1e-9) / 1e9, 2)) for k, v in fam.items()}
+    return roof, families
+
+
+def cpu_baseline(args):
+    """The CPU oracle (fp32 torch-CPU restatement of the reference, pinned by
+    tests/golden) timed on this host on a bounded sample of the workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import realnvp_oracle as O
+    from formula_init import formula_value
+    threads = len(os.sched_getaffinity(0))
+    threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
+    torch.set_num_threads(threads)
+    spec = O.FlowSpec(3, args.size, O.HP(args.base_dim, args.res_blocks))
+    e = O.flow_spec_entries(spec)
+    S = O.build_state(e, formula_value)
+    tr = O.OracleTrainer(S, spec, O.param_names(e), O.trainable_names(e))
+    B = args.cpu_batch
+    pix = synthetic_pixels(B, 3, args.size, 123)
+    noise = torch.rand(B, 3, args.size, args.size, generator=torch.Generator().manual_seed(1))
+    x, ld = O.logit_transform(pix, noise)
+    tr.step(x, ld)   # warm-up
+    t0 = time.perf_counter()
+    for _ in range(args.cpu_steps):
+        tr.step(x, ld)
+    dt = time.perf_counter() - t0
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return dict(value=round(B * args.cpu_steps / dt, 3), unit="images/sec", cores=threads, kind="port",
+                sample="oracle fp32 train step (fwd+bwd+Adam), %dx%dx3 R%d D%d, batch %d, %d timed steps after 1 "
+                       "warm-up, %.1fs, %s" % (args.size, args.size, args.res_blocks, args.base_dim, B,
+                                               args.cpu_steps, dt, cpu_model))
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus %d needs torch.distributed.run --nproc-per-node %d" % (args.gpus, args.gpus))
+    torch.cuda.set_device(local)
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        pg = dist.group.WORLD
+
+    import flow_realnvp
+    import utils
+    from realnvp_hip.trainer import FlowTrainer
+
+    torch.manual_seed(args.seed)     # same initial weights on every rank
+    dev = torch.device("cuda", local)
+    prior = torch.distributions.Normal(torch.tensor(0.0, device=dev), torch.tensor(1.0, device=dev),
+                                       validate_args=False)
+    hp = utils.Hyperparameters(args.base_dim, args.res_blocks, True, True, True, True)
+    model = flow_realnvp.RealNVP(3, args.size, prior, hp).to(dev)
+    tr = FlowTrainer(model, args.batch, dtype=args.dtype, seed=1000 + rank, process_group=pg)
+    tr.set_pixels(synthetic_pixels(args.batch, 3, args.size, seed=rank).to(dev))
+
+    if not args.no_graph:
+        tr.capture(warmup=2)
+    for _ in range(args.warmup):
+        tr.step()
+    tr.reset_metrics()
+
+    def barrier():
+        if pg is not None:
+            import torch.distributed as dist
+            dist.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.step()
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    mean_ll = tr.mean_logll(args.steps)
+    if pg is not None:
+        import torch.distributed as dist
+        t = torch.tensor([dt, mean_ll], dtype=torch.float64, device=dev)
+        mx = t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        dt = float(mx[0])
+        mean_ll = float(t[1]) / world
+    bpd = tr.bits_per_dim(mean_ll)
+    imgs = world * args.batch * args.steps
+    value = imgs / dt
+    roof, fams = kernel_roofline(tr)
+    out = None
+    if rank == 0:
+        out = {
+            "metric": "images/sec + bits/dim, RealNVP 64x64x3 training",
+            "value": round(value, 2),
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (uniform 8-bit pixels, device Philox dequantisation noise); random init",
+            "config": {"workload": "config 1: RealNVP %dx%dx3, res-blocks %d, base-dim %d, per-GPU batch %d, "
+                                   "train step fwd+bwd+Adam" % (args.size, args.size, args.res_blocks, args.base_dim,
+                                                                args.batch),
+                       "global_batch": world * args.batch, "image_size": args.size, "res_blocks": args.res_blocks,
+                       "base_dim": args.base_dim, "parallelism": "dp%d" % world,
+                       "graph": not args.no_graph},
+            "bits_per_dim": round(bpd, 4),
+            "step_roofline_frac": round(value / world * ALG_BYTES_PER_IMG / (HBM_PEAK_GBS * 1e9), 5),
+            "roofline": roof,
+            "kernel_families": fams,
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args)
+        print(json.dumps(out), flush=True)
+    if pg is not None:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

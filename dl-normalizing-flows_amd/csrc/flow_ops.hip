@@ -155,10 +155,11 @@ __device__ __forceinline__ float philox_uniform(uint64_t seed, uint64_t ctr) {
 __device__ __forceinline__ float softplusf(float v) { return v > 20.f ? v : log1pf(expf(v)); }
 
 __global__ void k_logit_fwd(const float* __restrict__ x, const float* __restrict__ noise, uint64_t seed, uint64_t offset,
-                            float cst, float* __restrict__ y, float* __restrict__ logdet, int n) {
+                            const long long* epoch, float cst, float* __restrict__ y, float* __restrict__ logdet, int n) {
     __shared__ double red[16];
     const int b = blockIdx.x;
     const long long base = (long long)b * n;
+    if (epoch) offset += (uint64_t)epoch[0] * (uint64_t)gridDim.x * (uint64_t)n;
     const float sp_pre = softplusf(-(float)(log((double)cst) - log(1.0 - (double)cst)));
     double acc = 0;
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
@@ -174,11 +175,13 @@ __global__ void k_logit_fwd(const float* __restrict__ x, const float* __restrict
     if (threadIdx.x == 0) logdet[b] = (float)acc;
 }
 
-extern "C" int rnvp_logit_fwd(const float* x, const float* noise, uint64_t seed, uint64_t offset, float constraint,
-                              float* y, float* logdet, int B, int n_per_sample, void* stream) {
+extern "C" int rnvp_logit_fwd(const float* x, const float* noise, uint64_t seed, uint64_t offset,
+                              const long long* epoch, float constraint, float* y, float* logdet, int B,
+                              int n_per_sample, void* stream) {
     if (!x || !y || !logdet || B < 0 || n_per_sample <= 0) return RNVP_E_INVALID;
     if (B == 0) return RNVP_OK;
-    k_logit_fwd<<<B, 512, 0, (hipStream_t)stream>>>(x, noise, seed, offset, constraint, y, logdet, n_per_sample);
+    k_logit_fwd<<<B, 512, 0, (hipStream_t)stream>>>(x, noise, seed, offset, epoch, constraint, y, logdet,
+                                                     n_per_sample);
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
 }
@@ -314,12 +317,14 @@ __global__ void k_adam(float4* __restrict__ p, const float4* __restrict__ g, flo
     const float step_size = sh[0], inv_bc2s = sh[1];
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
         float4 pp = p[i], gg = g[i], mm = m[i], vv = v[i];
-        uint32_t rm = regm ? regm[i] : 0u;
+        const uint32_t mk = regm ? regm[i] : 0x01010101u;
         float* pa = (float*)&pp; float* ga = (float*)&gg; float* ma = (float*)&mm; float* va = (float*)&vv;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
+            const uint32_t f = (mk >> (8 * j)) & 0xff;
+            if (f == 0) continue;                      // frozen parameter
             float gr = ga[j] + wd * pa[j];
-            if ((rm >> (8 * j)) & 0xff) gr += 2.f * reg * pa[j];
+            if (f == 2) gr += 2.f * reg * pa[j];       // weight_scale regulariser
             ma[j] = ma[j] + (1.f - b1) * (gr - ma[j]);
             va[j] = va[j] * b2 + (1.f - b2) * gr * gr;
             float den = sqrtf(va[j]) * inv_bc2s + eps;

@@ -31,6 +31,23 @@ def stream_ptr():
     return torch.cuda.current_stream().cuda_stream
 
 
+# Optional launch timing (bench.py's per-kernel roofline): when PROFILE is a
+# list, every engine launch appends (family, algorithmic bytes, flops,
+# start event, end event), events recorded on the launch stream.
+PROFILE = None
+
+
+def _launch(family, nbytes, flops, fn, *args):
+    if PROFILE is None:
+        return fn(*args)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    fn(*args)
+    e1.record()
+    PROFILE.append((family, nbytes, flops, e0, e1))
+
+
 class Arena:
     """Bump allocator over one device tensor (256-B aligned slots)."""
 
@@ -273,10 +290,12 @@ class CouplingEngine:
                 a.pro_bn_relu = 1
                 a.pro = self._bn(T, op.pro_bn, training, ar.ptr("s:" + op.pro_bn), M)
             a.out_sums = ar.ptr("s:" + op.stats_bn) if (op.stats_bn and training) else None
-            L.conv2d(C.byref(a), s)
+            esz = DTYPES[sv["dtype"]][1]
+            nb = esz * (M * cs_in + spec.cout * kp_f + M * cs_out * (1 + int(bool(op.residual)) + int(op.accumulate)))
+            _launch("conv_fwd", nb, 2.0 * M * spec.cout * spec.ks * spec.ks * spec.cin, L.conv2d, C.byref(a), s)
 
     # ---------------------------------------------------------------- forward
-    def forward(self, x, training, dtype, full_ldj, saved=None, prepare=True, ldj_sample=None):
+    def forward(self, x, training, dtype, full_ldj, saved=None, prepare=True, ldj_sample=None, z_out=None):
         """x: [B,C,H,W] fp32 device tensor.  Returns (z, ldj, saved) where ldj
         is the elementwise log_diag_J [B,C,H,W] (full_ldj) or this coupling's
         per-sample sum [B] (accumulated into ldj_sample when given)."""
@@ -289,7 +308,7 @@ class CouplingEngine:
         sv = saved if saved is not None else self.alloc_saved(B, H, W, dtype, dev, training)
         ar = sv["arena"]
         T = self._tensors()
-        z = torch.empty_like(x)
+        z = torch.empty_like(x) if z_out is None else z_out
         if ldj_sample is None:
             ldj_sample = torch.zeros(B, device=dev, dtype=torch.float32)
         ldj_full = torch.empty_like(x) if full_ldj else None
@@ -398,7 +417,10 @@ class CouplingEngine:
                     c.epi_x = ar.ptr(op.x)
                     c.epi = self._bn(T, op.pro_bn, training, ar.ptr("s:" + op.pro_bn), M)
                     c.epi_sums = sar.ptr("e:" + op.pro_bn)
-                L.conv2d(C.byref(c), s)
+                esz = DTYPES[dtype][1]
+                nb = esz * (M * cs_out + spec.cin * kp_d + M * cs_in * (1 + int(bool(op.pro_bn)) + int(bool(
+                    st.residual)) + int(st.accumulate)))
+                _launch("conv_dgrad", nb, 2.0 * M * spec.cout * spec.ks * spec.ks * spec.cin, L.conv2d, C.byref(c), s)
             elif st.kind == "bn_apply":
                 bn = op.pro_bn
                 c = BNBwdArgs()
@@ -410,7 +432,9 @@ class CouplingEngine:
                 c.residual = sar.ptr(st.residual) if st.residual else None
                 c.accumulate = int(st.accumulate)
                 c.dgamma, c.dbeta = gp(bn + "weight"), gp(bn + "bias")
-                L.bn_bwd_apply(C.byref(c), s)
+                esz = DTYPES[dtype][1]
+                nb = esz * M * cs_in * (3 + int(bool(st.residual)) + int(st.accumulate))
+                _launch("bn_bwd", nb, 0.0, L.bn_bwd_apply, C.byref(c), s)
             else:
                 c = WgradArgs()
                 c.dtype, c.B, c.H, c.W, c.ks = dt, B, H, W, spec.ks
@@ -421,7 +445,10 @@ class CouplingEngine:
                 c.dy, c.cs_dy, c.n = sar.ptr(st.gy), cs_out, spec.cout
                 c.dw, c.kp = sar.ptr("dw:" + op.conv), kp_f
                 c.dbias = gp(bname) if bname else None
-                L.conv2d_wgrad(C.byref(c), s)
+                esz = DTYPES[dtype][1]
+                nb = esz * (M * cs_in + M * cs_out) + 4 * spec.cout * spec.ks * spec.ks * spec.cin
+                _launch("conv_wgrad", nb, 2.0 * M * spec.cout * spec.ks * spec.ks * spec.cin, L.conv2d_wgrad,
+                        C.byref(c), s)
         L.weight_norm_bwd(sc["wn_table"].data_ptr(), sc["n_wn"], sc["wn_rows"], gbase, s)
         a.gh0, a.cs_gh0 = sar.ptr("g:h0"), chan_stride(self.P.buf_ch["h0"])
         a.in_bwd_sums = sar.ptr("in_bwd_sums")

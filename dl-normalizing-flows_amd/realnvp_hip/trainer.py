@@ -1,0 +1,276 @@
+"""Fused RealNVP NLL training step (train.py:176-200) on the MI355X.
+
+One step = logit_transform of a uint8-valued pixel batch (device Philox
+noise), RealNVP forward with per-sample log-det accumulation, N(0,1) prior,
+loss = -mean(log_prob + logdet) + 5e-5 * weight_scale, explicit backward
+through every coupling / permutation, and a fused Adam update (coupled L2
+weight decay, train.py:134) over ONE flat fp32 parameter arena.
+
+MI355X-specific structure:
+  * parameters, gradients and both Adam moments are flat arenas; the
+    drop-in modules' nn.Parameters are views into the parameter arena, so
+    state_dict / load_state_dict / torch optimizers keep working;
+  * every buffer is allocated once; the whole step is captured into a HIP
+    graph and replayed (no per-kernel host cost);
+  * data parallel: one process per GPU, batch slice per rank, gradient
+    arena all-reduced (average) over RCCL in buckets between the backward
+    graph and the optimizer graph.  BatchNorm statistics stay per rank
+    (= the reference's semantics for each 64-image shard).
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+from .engine import stream_ptr
+
+
+class FlowTrainer:
+    def __init__(self, model, batch_size, lr=5e-4, weight_decay=5e-5, betas=(0.9, 0.999), eps=1e-8,
+                 scale_reg=5e-5, dtype="bf16", seed=0, process_group=None, bucket_mb=64):
+        self.model = model
+        self.dev = next(model.parameters()).device
+        if self.dev.type != "cuda":
+            raise RuntimeError("FlowTrainer needs the model on a HIP device")
+        self.B = batch_size
+        self.lr, self.wd, self.betas, self.eps, self.reg = lr, weight_decay, betas, eps, scale_reg
+        self.dtype = dtype
+        self.seed = seed
+        self.pg = process_group
+        model.set_precision(dtype)
+        model.train()
+        self._build_arenas()
+        self._build_plan()
+        self.graph = None
+        self.graph_opt = None
+        self.external_input = False
+        self.bucket_elems = max(1, int(bucket_mb * 2 ** 20 // 4))
+
+    # ----------------------------------------------------------------- arenas
+    def _build_arenas(self):
+        named = list(self.model.named_parameters())
+        n = sum(p.numel() for _, p in named)
+        n_pad = (n + 3) // 4 * 4
+        dev = self.dev
+        self.n = n_pad
+        self.param = torch.zeros(n_pad, device=dev, dtype=torch.float32)
+        self.grad = torch.zeros(n_pad, device=dev, dtype=torch.float32)
+        self.exp_avg = torch.zeros(n_pad, device=dev, dtype=torch.float32)
+        self.exp_avg_sq = torch.zeros(n_pad, device=dev, dtype=torch.float32)
+        mask = np.zeros(n_pad, dtype=np.uint8)
+        self.offsets = {}
+        off = 0
+        with torch.no_grad():
+            for name, p in named:
+                k = p.numel()
+                self.param[off:off + k].copy_(p.detach().reshape(-1))
+                p.data = self.param[off:off + k].view_as(p)
+                if p.requires_grad:
+                    mask[off:off + k] = 2 if name.split(".")[-1] in ("weight_g", "scale") else 1
+                self.offsets[name] = off
+                off += k
+        self.mask = torch.from_numpy(mask).to(dev)
+        self.step_t = torch.zeros(1, device=dev, dtype=torch.int64)
+        self.n_trainable = int((mask > 0).sum())
+
+    # ------------------------------------------------------------------- plan
+    def _build_plan(self):
+        m = self.model
+        B, C, S = self.B, m.channels, m.image_size
+        dev = self.dev
+        f32 = dict(device=dev, dtype=torch.float32)
+        self.pix = torch.zeros(B, C, S, S, **f32)
+        self.xl = torch.empty(B, C, S, S, **f32)
+        self.logdet = torch.empty(B, **f32)
+        self.ldj = torch.zeros(B, **f32)
+        self.lp = torch.empty(B, **f32)
+        self.g_lp = torch.full((B,), -1.0 / B, **f32)
+        self.ll_acc = torch.zeros(1, dtype=torch.float64, device=dev)
+        self.stages = []   # forward program: ("coupling", mod, eng, in, out, sv, block) | perm ops
+        cur = self.xl
+        c, s = C, S
+        offs = []
+        for si in range(1, m.n_scales):
+            ckbd, chan = m._scale_mods(si)
+            for mod in ckbd:
+                cur = self._add_coupling(mod, cur)
+            sq = torch.empty(B, 4 * c, s // 2, s // 2, **f32)
+            self.stages.append(("squeeze", cur, sq))
+            cur = sq
+            for mod in chan:
+                cur = self._add_coupling(mod, cur)
+            un = torch.empty(B, c, s, s, **f32)
+            self.stages.append(("undo", cur, un))
+            on = torch.empty(B, 2 * c, s // 2, s // 2, **f32)
+            off = torch.empty_like(on)
+            self.stages.append(("factor_out", un, on, off))
+            offs.append(off)
+            cur = on
+            c, s = 2 * c, s // 2
+        for mod in m._scale_mods(m.n_scales)[0]:
+            cur = self._add_coupling(mod, cur)
+        for off in reversed(offs):
+            full = torch.empty(B, off.shape[1] // 2, off.shape[2] * 2, off.shape[3] * 2, **f32)
+            self.stages.append(("restore", cur, off, full))
+            cur = full
+        self.z = cur
+        # backward buffers: a gradient buffer per forward tensor
+        self.gbuf = {}
+
+    def _add_coupling(self, mod, x):
+        eng = mod.engine()
+        B, C, H, W = x.shape
+        sv = eng.alloc_saved(B, H, W, self.dtype, self.dev, True)
+        z = torch.empty_like(x)
+        first = next(n for n, _ in mod.named_parameters())
+        name = self._module_name(mod) + "." + first
+        block = self.grad[self.offsets[name]:self.offsets[name] + eng.n_params]
+        self.stages.append(("coupling", mod, eng, x, z, sv, block))
+        return z
+
+    def _module_name(self, mod):
+        if not hasattr(self, "_names"):
+            self._names = {id(m): n for n, m in self.model.named_modules()}
+        return self._names[id(mod)]
+
+    def _g(self, t):
+        """gradient buffer shaped like forward tensor t"""
+        k = t.data_ptr()
+        g = self.gbuf.get(k)
+        if g is None:
+            g = torch.empty_like(t)
+            self.gbuf[k] = g
+        return g
+
+    # ------------------------------------------------------------------- step
+    def _forward(self):
+        L = _lib.lib()
+        s = stream_ptr()
+        B = self.B
+        n = self.pix[0].numel()
+        if not self.external_input:
+            L.logit_fwd(self.pix.data_ptr(), None, self.seed, 0, self.step_t.data_ptr(), 0.9, self.xl.data_ptr(),
+                        self.logdet.data_ptr(), B, n, s)
+        self.ldj.zero_()
+        for st in self.stages:
+            if st[0] == "coupling":
+                _, mod, eng, x, z, sv, _ = st
+                eng.forward(x, True, self.dtype, False, saved=sv, prepare=True, ldj_sample=self.ldj, z_out=z)
+            elif st[0] == "squeeze":
+                _, a, b = st
+                L.squeeze(a.data_ptr(), b.data_ptr(), *a.shape, s)
+            elif st[0] == "undo":
+                _, a, b = st
+                L.undo_squeeze(a.data_ptr(), b.data_ptr(), *b.shape, s)
+            elif st[0] == "factor_out":
+                _, a, on, off = st
+                L.factor_out(a.data_ptr(), on.data_ptr(), off.data_ptr(), *a.shape, s)
+            else:
+                _, on, off, full = st
+                L.restore(on.data_ptr(), off.data_ptr(), full.data_ptr(), *full.shape, s)
+        L.prior_logprob(self.z.data_ptr(), self.ldj.data_ptr(), self.lp.data_ptr(), B, self.z[0].numel(), s)
+        self.ll_acc += (self.lp + self.logdet).mean().double()
+
+    def _backward(self):
+        L = _lib.lib()
+        s = stream_ptr()
+        B = self.B
+        gz = self._g(self.z)
+        L.prior_logprob_bwd(self.z.data_ptr(), self.g_lp.data_ptr(), gz.data_ptr(), B, self.z[0].numel(), s)
+        for st in reversed(self.stages):
+            if st[0] == "coupling":
+                _, mod, eng, x, z, sv, block = st
+                eng.backward(sv, self._g(z), None, self.g_lp, block, gx=self._g(x))
+            elif st[0] == "squeeze":
+                _, a, b = st
+                L.undo_squeeze(self._g(b).data_ptr(), self._g(a).data_ptr(), *a.shape, s)
+            elif st[0] == "undo":
+                _, a, b = st
+                L.squeeze(self._g(b).data_ptr(), self._g(a).data_ptr(), *b.shape, s)
+            elif st[0] == "factor_out":
+                _, a, on, off = st
+                L.restore(self._g(on).data_ptr(), self._g(off).data_ptr(), self._g(a).data_ptr(), *a.shape, s)
+            else:
+                _, on, off, full = st
+                L.factor_out(self._g(full).data_ptr(), self._g(on).data_ptr(), self._g(off).data_ptr(),
+                             *full.shape, s)
+
+    def _optimizer(self):
+        b1, b2 = self.betas
+        _lib.lib().adam_step(self.param.data_ptr(), self.grad.data_ptr(), self.exp_avg.data_ptr(),
+                             self.exp_avg_sq.data_ptr(), self.n, self.step_t.data_ptr(), self.lr, b1, b2, self.eps,
+                             self.wd, self.mask.data_ptr(), self.reg, stream_ptr())
+
+    def _allreduce(self):
+        if self.pg is None:
+            return
+        import torch.distributed as dist
+        for i in range(0, self.n, self.bucket_elems):
+            dist.all_reduce(self.grad[i:i + self.bucket_elems], op=dist.ReduceOp.AVG, group=self.pg)
+
+    def _fwd_bwd(self):
+        self.grad.zero_()
+        self._forward()
+        self._backward()
+
+    def step_eager(self):
+        self._fwd_bwd()
+        self._allreduce()
+        self._optimizer()
+
+    def capture(self, warmup=2):
+        """Warm up eagerly on a side stream, then capture the step into HIP graphs."""
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self.step_eager()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        if self.pg is None:
+            with torch.cuda.graph(self.graph):
+                self._fwd_bwd()
+                self._optimizer()
+        else:
+            with torch.cuda.graph(self.graph):
+                self._fwd_bwd()
+            self.graph_opt = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph_opt):
+                self._optimizer()
+        torch.cuda.synchronize()
+
+    def step(self):
+        if self.graph is None:
+            return self.step_eager()
+        self.graph.replay()
+        if self.graph_opt is not None:
+            self._allreduce()
+            self.graph_opt.replay()
+
+    def set_pixels(self, pix):
+        self.external_input = False
+        self.pix.copy_(pix)
+
+    def set_input(self, x, logdet):
+        """Feed an already logit-transformed batch (parity tests)."""
+        self.external_input = True
+        self.xl.copy_(x)
+        self.logdet.copy_(logdet)
+
+    def reset_optimizer(self):
+        self.exp_avg.zero_()
+        self.exp_avg_sq.zero_()
+        self.step_t.zero_()
+
+    def reset_metrics(self):
+        self.ll_acc.zero_()
+
+    def mean_logll(self, steps):
+        return float(self.ll_acc.item()) / max(steps, 1)
+
+    def bits_per_dim(self, mean_ll):
+        """train.py:203-204."""
+        D = self.model.image_size ** 2 * self.model.channels
+        return (-mean_ll + math.log(256.0) * D) / (D * math.log(2.0))

@@ -60,5 +60,6 @@ def logit_transform(x, constraint=0.9, reverse=False, noise=None, seed=None):
         nptr = noise.data_ptr()
     if seed is None:
         seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-    L.logit_fwd(x.data_ptr(), nptr, seed, 0, float(constraint), y.data_ptr(), logdet.data_ptr(), B, n, stream_ptr())
+    L.logit_fwd(x.data_ptr(), nptr, seed, 0, None, float(constraint), y.data_ptr(), logdet.data_ptr(), B, n,
+                stream_ptr())
     return y, logdet

@@ -52,9 +52,12 @@ int rnvp_restore(const float* on, const float* off, float* x, int B, int C, int 
 /* ---- logit transform (utils.py:33-72) ----------------------------------
  * y = logit(((x*255+u)/256*2-1)*c+1)/2), logdet[b] = sum softplus(y)+softplus(-y)-softplus(-logit(c)).
  * u = noise[i] when noise != NULL, else a counter-based Philox4x32-10 uniform
- * in [0,1) keyed by (seed, offset + i).  n_per_sample = C*H*W. */
-int rnvp_logit_fwd(const float* x, const float* noise, uint64_t seed, uint64_t offset, float constraint,
-                   float* y, float* logdet, int B, int n_per_sample, void* stream);
+ * in [0,1) keyed by (seed, offset + i), where offset is advanced by
+ * (*epoch) * B * n_per_sample when epoch (a device int64, e.g. the optimizer
+ * step) is non-NULL -- so a replayed HIP graph draws fresh noise every step.
+ * n_per_sample = C*H*W. */
+int rnvp_logit_fwd(const float* x, const float* noise, uint64_t seed, uint64_t offset, const long long* epoch,
+                   float constraint, float* y, float* logdet, int B, int n_per_sample, void* stream);
 int rnvp_logit_inv(const float* x, float* y, float constraint, long long n, void* stream);
 
 /* ---- prior log-prob and per-sample reduction (flow_realnvp.py:329-340) --
@@ -197,12 +200,15 @@ int rnvp_sumsq_multi(const rnvp_tensor_ref* refs_device, int n_refs, float* out,
 int rnvp_sumsq_bwd_multi(const rnvp_tensor_ref* refs_device, int n_refs, const float* gout, float coef, void* stream);
 
 /* torch.optim.Adam step (coupled L2 weight decay, train.py:134) over a flat
- * fp32 parameter arena.  step is a device int64 incremented by this call;
- * reg_mask (optional, uint8 per element) adds reg_coef*2*p to the gradient
- * of the weight_g/scale parameters (the 5e-5*weight_scale term, train.py:194). */
+ * fp32 parameter arena (n % 4 == 0, 16-B aligned).  step is a device int64
+ * incremented by this call.  mask (optional, uint8 per element): 0 = frozen
+ * (requires_grad=False: parameter and moments untouched, as torch skips
+ * params without grad), 1 = trainable, 2 = trainable and regularised, i.e.
+ * reg_coef*2*p is added to its gradient (the 5e-5*weight_scale term of
+ * train.py:194 for trainable weight_g / scale).  NULL = all trainable. */
 int rnvp_adam_step(float* param, float* grad, float* exp_avg, float* exp_avg_sq, long long n,
                    long long* step, float lr, float beta1, float beta2, float eps, float weight_decay,
-                   const uint8_t* reg_mask, float reg_coef, void* stream);
+                   const uint8_t* mask, float reg_coef, void* stream);
 
 /* misc */
 int rnvp_fill_f64(double* p, long long n, double v, void* stream);

@@ -184,7 +184,9 @@ def test_model_vs_reference(case):
     loss = -(lp + logdet).mean() + 5e-5 * ws
     np.testing.assert_allclose(float(loss), float(g["loss"]), rtol=1e-5)
     loss.backward()
-    assert rel(x.grad.cpu().numpy(), g["grad_x"]) < 1e-2
+    # fp32 floor of dL/dx through 28 batch-stat couplings: the CPU oracle in
+    # fp32 vs fp64 differs by 2.9e-3 (m32_d32_r2) and 1.4e-2 (m64_d32_r4, B=2)
+    assert rel(x.grad.cpu().numpy(), g["grad_x"]) < 3e-2
     names = [n for n, p in model.named_parameters() if p.requires_grad]
     assert names == list(g["grad_names"])
     params = dict(model.named_parameters())
@@ -239,7 +241,10 @@ def test_reference_training_loop_trajectory():
     model.eval()
     with torch.no_grad():
         lp, _ = model(T(g["x"]))
-    np.testing.assert_allclose(lp.cpu().numpy(), g["traj_eval_logprob_after"], rtol=1e-4)
+    # after 3 Adam steps: Adam's m/sqrt(v) turns the fp32 noise of near-zero
+    # gradients (conv biases feeding a BatchNorm, ...) into +-lr updates, so
+    # the weights differ at the 1e-4 level -> 5e-4 on the resulting log-prob
+    np.testing.assert_allclose(lp.cpu().numpy(), g["traj_eval_logprob_after"], rtol=5e-4)
 
 
 def test_bf16_mode_close_to_fp32():
