@@ -84,8 +84,14 @@ __device__ __forceinline__ void bn_affine(const rnvp_bn_src& s, int C, int c, fl
                                           float* mean_out = nullptr, float* rstd_out = nullptr) {
     double mean, var;
     if (s.sums) {
-        mean = s.sums[c] / s.count;
-        var = s.sums[C + c] / s.count - mean * mean;
+        double s1 = 0, s2 = 0;
+        const int ns = s.shards > 0 ? s.shards : 1;
+        for (int h = 0; h < ns; ++h) {
+            s1 += s.sums[(long long)h * 2 * C + c];
+            s2 += s.sums[(long long)h * 2 * C + C + c];
+        }
+        mean = s1 / s.count;
+        var = s2 / s.count - mean * mean;
         if (var < 0) var = 0;
     } else {
         mean = s.mean[c];
@@ -98,6 +104,66 @@ __device__ __forceinline__ void bn_affine(const rnvp_bn_src& s, int C, int c, fl
     shift = b - (float)mean * g * rstd;
     if (mean_out) *mean_out = (float)mean;
     if (rstd_out) *rstd_out = rstd;
+}
+
+// Whole-block reduction of sharded BN sums ([shards][2*C] fp64) for channels
+// [c0, c0+nc) into LDS s1[nc], s2[nc].  Every (channel, shard) pair is a
+// separate, independent load spread over the block (no per-thread serial
+// chain of dependent loads), accumulated with LDS fp64 atomics (ds_add_f64).
+// Must be reached by every thread of the block.
+__device__ __forceinline__ void block_shard_sums(const double* sums, int C, int shards, int c0, int nc, double* s1,
+                                                 double* s2) {
+    if (shards < 1) shards = 1;
+    for (int i = threadIdx.x; i < nc; i += blockDim.x) {
+        s1[i] = 0.0;
+        s2[i] = 0.0;
+    }
+    __syncthreads();
+    const int total = nc * shards;
+    for (int t = threadIdx.x; t < total; t += blockDim.x) {
+        const int c = t % nc, h = t / nc;
+        const double* p = sums + (long long)h * 2 * C + c0 + c;
+        atomicAdd(&s1[c], p[0]);
+        atomicAdd(&s2[c], p[C]);
+    }
+    __syncthreads();
+}
+
+// Whole-block BN table for channels [c0, c0+nc): scale/shift such that
+// bn(x) = x*scale + shift, plus mean / rstd when requested.  Channels >= C
+// (padding) get scale = shift = 0, mean = 0, rstd = 1.  tmp: 2*nc doubles of
+// LDS.  Must be reached by every thread of the block.
+__device__ __forceinline__ void block_bn_table(const rnvp_bn_src& s, int C, int c0, int nc, float* scale, float* shift,
+                                               float* mean_out, float* rstd_out, double* tmp) {
+    const int nv = max(0, min(nc, C - c0));
+    if (s.sums) block_shard_sums(s.sums, C, s.shards, c0, nv, tmp, tmp + nc);
+    for (int i = threadIdx.x; i < nc; i += blockDim.x) {
+        const int c = c0 + i;
+        float sc = 0.f, sf = 0.f, mo = 0.f, ro = 1.f;
+        if (i < nv) {
+            double mean, var;
+            if (s.sums) {
+                mean = tmp[i] / s.count;
+                var = tmp[nc + i] / s.count - mean * mean;
+                if (var < 0) var = 0;
+            } else {
+                mean = s.mean[c];
+                var = s.var[c];
+            }
+            const float rstd = (float)(1.0 / sqrt(var + (double)s.eps));
+            const float g = s.gamma ? s.gamma[c] : 1.f;
+            const float b = s.beta ? s.beta[c] : 0.f;
+            sc = g * rstd;
+            sf = b - (float)mean * g * rstd;
+            mo = (float)mean;
+            ro = rstd;
+        }
+        scale[i] = sc;
+        shift[i] = sf;
+        if (mean_out) mean_out[i] = mo;
+        if (rstd_out) rstd_out[i] = ro;
+    }
+    __syncthreads();
 }
 
 static inline int rnvp_grid(long long n, int block, int cap = 4096) {

@@ -2,19 +2,33 @@
 //
 // Implicit GEMM over NHWC activations: M = B*H*W pixels, N = output channels,
 // K = ks*ks*cs_in (tap-major, channel-minor).  BatchNorm+ReLU of the operand is
-// applied while staging the A tile (global -> registers -> LDS), bias /
+// applied while staging the A tile (global -> registers -> LDS); bias /
 // residual / skip accumulation and the next BatchNorm's batch statistics are
 // fused into the epilogue.  The data gradient is the same kernel on the
 // flipped/transposed weight image with a ReLU+BN-backward epilogue; the
 // weight gradient reduces over pixels with both operands transposed through
 // LDS by ds_read_b64_tr_b16.
 //
+// Pipeline: a stage is 128 B of K per tile row (64 bf16 / 32 f32), double
+// buffered in LDS; the global loads of stage k+1 are issued before the MFMAs
+// of stage k and land in registers, the BN/ReLU transform and the LDS store
+// happen after the MFMAs -> one barrier per stage, load latency under compute.
+// Small grids (deep scales: M = 1024..4096 pixels, K up to 4608) split K over
+// workgroups into an fp32 workspace reduced by a second, epilogue kernel.
+// BN statistics go to rnvp_stat_shards(M) shards (bounded atomic contention).
+//
 // MFMA: bf16 -> v_mfma_f32_16x16x32_bf16 (fp32 accumulate);
 //       f32  -> v_mfma_f32_16x16x4_f32 (exact fp32, parity mode).
-// A 16-byte chunk holds 8 bf16 / 4 f32; one LDS tile row is 4 chunks = 64 B.
 #include <math.h>
 
 #include "common.h"
+
+extern "C" int rnvp_stat_shards(long long M) {
+    long long s = M / 8192;
+    int r = 1;
+    while (r < 32 && r * 2 <= s) r *= 2;
+    return r;
+}
 
 namespace {
 
@@ -36,25 +50,52 @@ template <> struct Mf<float> {
     }
 };
 
-__device__ __forceinline__ int swz(int row, int c4) { return row * 4 + (c4 ^ ((row >> 2) & 3)); }
+// [row][8 chunks of 16 B]; XOR swizzle spreads the 16 rows one ds_read_b128
+// lane group reads over all 64 banks (rows r, r+1 differ in bank half, r>>1
+// picks the chunk).
+__device__ __forceinline__ int sw8(int row, int c) { return row * 8 + (c ^ ((row >> 1) & 7)); }
+
+__device__ __forceinline__ double* shard_ptr(double* sums, int shards, int N) {
+    return sums ? sums + (long long)(blockIdx.x % shards) * 2 * N : nullptr;
+}
+
+// per-element epilogue shared by the direct and the split-K path
+template <typename T>
+__device__ __forceinline__ float epi_value(const rnvp_conv_args& a, long long o, float acc, float bias, float e_sc,
+                                           float e_sf, float e_mean, float e_rstd, float& s1, float& s2) {
+    float v = acc + bias;
+    if (a.residual) v += ldv((const T*)a.residual + o);
+    if (a.accumulate) v += ldv((const T*)a.y + o);
+    if (a.epi_relu_bn_bwd) {
+        const float xv = ldv((const T*)a.epi_x + o);
+        if (xv * e_sc + e_sf <= 0.f) v = 0.f;
+        s1 += v;
+        s2 += v * (xv - e_mean) * e_rstd;
+    } else {
+        s1 += v;
+        s2 += v * v;
+    }
+    return v;
+}
 
 // ---------------------------------------------------------------------------
 // forward / data-gradient conv
 // ---------------------------------------------------------------------------
-template <typename T, int BM, int BN, int WM, int WN>
-__global__ __launch_bounds__(256) void k_conv(rnvp_conv_args a) {
+template <typename T, int BM, int BN, int WM, int WN, bool PARTIAL>
+__global__ __launch_bounds__(256) void k_conv(rnvp_conv_args a, int kt_per_split, int shards) {
     constexpr int CH = Mf<T>::CH;
-    constexpr int BK = 4 * CH;
+    constexpr int BKS = 8 * CH;                        // K elements per stage
     constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
-    constexpr int A_PER = (BM * 4) / 256;
-    constexpr int B_CHUNKS = BN * 4;
+    constexpr int A_PER = (BM * 8) / 256;
+    constexpr int B_CH = BN * 8;
+    constexpr int B_PER = (B_CH + 255) / 256;
     static_assert(WM * WN == 4, "4 waves");
-    static_assert(A_PER >= 1, "BM >= 64");
+    static_assert(A_PER >= 1, "BM >= 32");
 
-    __shared__ u32x4 As[BM * 4];
-    __shared__ u32x4 Bs[BN * 4];
+    __shared__ u32x4 As[2][BM * 8];
+    __shared__ u32x4 Bs[2][BN * 8];
     __shared__ float red[WM * BN * 2];
-    extern __shared__ float bnp[];   // [2 * cs_in] prologue scale / shift
+    extern __shared__ double dsm[];   // tmp [2*max(cs,BN)] fp64 | bnp [2*cs] | etab [4*BN]
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid / WN, wn = wid % WN;
@@ -65,23 +106,22 @@ __global__ __launch_bounds__(256) void k_conv(rnvp_conv_args a) {
     const int n0 = blockIdx.y * BN;
     const T* __restrict__ X = (const T*)a.x;
     const T* __restrict__ Wt = (const T*)a.w;
+    const bool pro = a.pro_bn_relu != 0;
+    const bool epi_bn = !PARTIAL && a.epi_relu_bn_bwd;
 
-    if (a.pro_bn_relu) {
-        for (int c = tid; c < cs; c += 256) {
-            float sc = 0.f, sf = 0.f;
-            if (c < a.cin) bn_affine(a.pro, a.cin, c, sc, sf);
-            bnp[c] = sc;
-            bnp[cs + c] = sf;
-        }
-    }
+    double* tmp = dsm;
+    float* bnp = (float*)(dsm + 2 * max(cs, BN));   // prologue scale [cs] | shift [cs]
+    float* etab = bnp + 2 * cs;                      // epilogue scale | shift | mean | rstd [BN each]
+    if (pro) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + cs, nullptr, nullptr, tmp);
+    if (epi_bn) block_bn_table(a.epi, N, n0, BN, etab, etab + BN, etab + 2 * BN, etab + 3 * BN, tmp);
 
-    // per-thread A rows (fixed over the K loop)
-    const int c4 = tid & 3;
+    // per-thread A rows (fixed over K) and chunk column
+    const int cA = tid & 7;
     long long arow_m[A_PER];
     int arow_y[A_PER], arow_x[A_PER];
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
-        const int r = (tid + i * 256) >> 2;
+        const int r = (tid + i * 256) >> 3;
         const long long m = m0 + r;
         arow_m[i] = m < M ? m : -1;
         const long long mm = m < M ? m : 0;
@@ -95,124 +135,406 @@ __global__ __launch_bounds__(256) void k_conv(rnvp_conv_args a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-    __syncthreads();
-    const int nk = (K + BK - 1) / BK;
-    for (int kt = 0; kt < nk; ++kt) {
-        // ---- stage A (implicit im2col + BN/ReLU prologue) ----
-        const int k = kt * BK + c4 * CH;
+    const int nk = (K + BKS - 1) / BKS;
+    const int kt0 = blockIdx.z * kt_per_split;
+    const int kt1 = min(nk, kt0 + kt_per_split);
+
+    u32x4 ra[A_PER], rb[B_PER];
+    unsigned amask = 0;
+    int aci = 0;
+
+    auto gload = [&](int kt) {
+        const int k = kt * BKS + cA * CH;
         const int tap = k / cs, ci = k - tap * cs;
         const int dy = tap / ks - pad, dx = tap % ks - pad;
+        aci = ci;
+        amask = 0;
 #pragma unroll
         for (int i = 0; i < A_PER; ++i) {
-            const int r = (tid + i * 256) >> 2;
-            u32x4 v = u32x4{0u, 0u, 0u, 0u};
             const int yy = arow_y[i] + dy, xx = arow_x[i] + dx;
+            ra[i] = u32x4{0u, 0u, 0u, 0u};
             if (arow_m[i] >= 0 && k < K && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) {
-                const long long off = (arow_m[i] + (long long)dy * a.W + dx) * cs + ci;
-                v = *(const u32x4*)(X + off);
-                if (a.pro_bn_relu) {
+                ra[i] = *(const u32x4*)(X + (arow_m[i] + (long long)dy * a.W + dx) * cs + ci);
+                amask |= 1u << i;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < B_PER; ++i) {
+            const int q = tid + i * 256;
+            rb[i] = u32x4{0u, 0u, 0u, 0u};
+            if (q < B_CH) {
+                const int nr = q >> 3, cc = q & 7;
+                if (n0 + nr < N) rb[i] = *(const u32x4*)(Wt + (long long)(n0 + nr) * a.kp + kt * BKS + cc * CH);
+            }
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < A_PER; ++i) {
+            const int r = (tid + i * 256) >> 3;
+            u32x4 v = ra[i];
+            if (pro) {
+                if (amask & (1u << i)) {
                     float f[CH];
                     unpack(v, f, T());
 #pragma unroll
-                    for (int j = 0; j < CH; ++j) f[j] = fmaxf(f[j] * bnp[ci + j] + bnp[cs + ci + j], 0.f);
+                    for (int j = 0; j < CH; ++j) f[j] = fmaxf(f[j] * bnp[aci + j] + bnp[cs + aci + j], 0.f);
                     v = pack(f, T());
+                } else {
+                    v = u32x4{0u, 0u, 0u, 0u};
                 }
             }
-            As[swz(r, c4)] = v;
+            As[buf][sw8(r, cA)] = v;
         }
-        // ---- stage B (packed weights [n][kp]) ----
-        for (int q = tid; q < B_CHUNKS; q += 256) {
-            const int nr = q >> 2, cc = q & 3;
-            u32x4 v = u32x4{0u, 0u, 0u, 0u};
-            if (n0 + nr < N) v = *(const u32x4*)(Wt + (long long)(n0 + nr) * a.kp + kt * BK + cc * CH);
-            Bs[swz(nr, cc)] = v;
+#pragma unroll
+        for (int i = 0; i < B_PER; ++i) {
+            const int q = tid + i * 256;
+            if (q < B_CH) Bs[buf][sw8(q >> 3, q & 7)] = rb[i];
         }
-        __syncthreads();
-        // ---- MFMA ----
-        const int g = lane >> 4, li = lane & 15;
-        u32x4 af[TM], bfr[TN];
+    };
+
+    __syncthreads();   // bnp ready
+    if (kt0 < kt1) {
+        gload(kt0);
+        lstore(0);
+    }
+    __syncthreads();
+    const int g = lane >> 4, li = lane & 15;
+    for (int kt = kt0; kt < kt1; ++kt) {
+        const int cur = (kt - kt0) & 1;
+        const bool more = kt + 1 < kt1;
+        if (more) gload(kt + 1);
 #pragma unroll
-        for (int i = 0; i < TM; ++i) af[i] = As[swz(wm * WTM + i * 16 + li, g)];
+        for (int s = 0; s < 2; ++s) {
+            u32x4 af[TM], bfr[TN];
 #pragma unroll
-        for (int j = 0; j < TN; ++j) bfr[j] = Bs[swz(wn * WTN + j * 16 + li, g)];
+            for (int i = 0; i < TM; ++i) af[i] = As[cur][sw8(wm * WTM + i * 16 + li, s * 4 + g)];
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+            for (int j = 0; j < TN; ++j) bfr[j] = Bs[cur][sw8(wn * WTN + j * 16 + li, s * 4 + g)];
 #pragma unroll
-            for (int j = 0; j < TN; ++j) Mf<T>::step(af[i], bfr[j], acc[i][j]);
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) Mf<T>::step(af[i], bfr[j], acc[i][j]);
+        }
+        if (more) lstore(cur ^ 1);
         __syncthreads();
     }
 
-    // ---- epilogue ----
-    T* __restrict__ Y = (T*)a.y;
-    const T* __restrict__ R = (const T*)a.residual;
-    const T* __restrict__ EX = (const T*)a.epi_x;
     const int cso = a.cs_out;
-    const bool want_sums = a.out_sums || (a.epi_relu_bn_bwd && a.epi_sums);
-    float s1[TN], s2[TN];
-    float e_sc[TN], e_sf[TN], e_mean[TN], e_rstd[TN], bias[TN];
+    if constexpr (PARTIAL) {
+        float* ws = a.ws + (long long)blockIdx.z * M * N;
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        const int n = n0 + wn * WTN + j * 16 + (lane & 15);
-        s1[j] = 0.f;
-        s2[j] = 0.f;
-        bias[j] = (a.bias && n < N) ? a.bias[n] : 0.f;
-        e_sc[j] = e_sf[j] = e_mean[j] = 0.f;
-        e_rstd[j] = 1.f;
-        if (a.epi_relu_bn_bwd && n < N) bn_affine(a.epi, N, n, e_sc[j], e_sf[j], &e_mean[j], &e_rstd[j]);
-    }
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
+            for (int r = 0; r < 4; ++r) {
+                const long long m = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+                if (m >= M) continue;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const long long m = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
-            if (m >= M) continue;
+                for (int j = 0; j < TN; ++j) {
+                    const int n = n0 + wn * WTN + j * 16 + (lane & 15);
+                    if (n < N) ws[m * N + n] = acc[i][j][r];
+                }
+            }
+        return;
+    } else {
+        // ---- fused epilogue ----
+        T* __restrict__ Y = (T*)a.y;
+        const bool want_sums = a.out_sums || (a.epi_relu_bn_bwd && a.epi_sums);
+        float s1[TN], s2[TN];
+        float e_sc[TN], e_sf[TN], e_mean[TN], e_rstd[TN], bias[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int col = wn * WTN + j * 16 + (lane & 15);
+            const int n = n0 + col;
+            s1[j] = 0.f;
+            s2[j] = 0.f;
+            bias[j] = (a.bias && n < N) ? a.bias[n] : 0.f;
+            e_sc[j] = e_sf[j] = e_mean[j] = 0.f;
+            e_rstd[j] = 1.f;
+            if (epi_bn) {
+                e_sc[j] = etab[col];
+                e_sf[j] = etab[BN + col];
+                e_mean[j] = etab[2 * BN + col];
+                e_rstd[j] = etab[3 * BN + col];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const long long m = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+                if (m >= M) continue;
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int n = n0 + wn * WTN + j * 16 + (lane & 15);
+                    if (n >= cso) continue;
+                    const long long o = m * cso + n;
+                    float v = 0.f;
+                    if (n < N) v = epi_value<T>(a, o, acc[i][j][r], bias[j], e_sc[j], e_sf[j], e_mean[j], e_rstd[j],
+                                                s1[j], s2[j]);
+                    stv(&Y[o], v);
+                }
+            }
+        }
+        if (want_sums) {
+            double* sums = shard_ptr(a.epi_relu_bn_bwd ? a.epi_sums : a.out_sums, shards, N);
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
-                const int n = n0 + wn * WTN + j * 16 + (lane & 15);
-                if (n >= cso) continue;
-                const long long o = m * cso + n;
-                float v = 0.f;
-                if (n < N) {
-                    v = acc[i][j][r] + bias[j];
-                    if (R) v += ldv(&R[o]);
-                    if (a.accumulate) v += ldv(&Y[o]);
-                    if (a.epi_relu_bn_bwd) {
-                        const float xv = ldv(&EX[o]);
-                        if (xv * e_sc[j] + e_sf[j] <= 0.f) v = 0.f;
-                        s1[j] += v;
-                        s2[j] += v * (xv - e_mean[j]) * e_rstd[j];
-                    } else {
-                        s1[j] += v;
-                        s2[j] += v * v;
-                    }
+                s1[j] += __shfl_xor(s1[j], 16, 64);
+                s1[j] += __shfl_xor(s1[j], 32, 64);
+                s2[j] += __shfl_xor(s2[j], 16, 64);
+                s2[j] += __shfl_xor(s2[j], 32, 64);
+                if (lane < 16) {
+                    const int col = wn * WTN + j * 16 + lane;
+                    red[(wm * BN + col) * 2] = s1[j];
+                    red[(wm * BN + col) * 2 + 1] = s2[j];
                 }
-                stv(&Y[o], v);
+            }
+            __syncthreads();
+            for (int col = tid; col < BN; col += 256) {
+                const int n = n0 + col;
+                if (n >= N) continue;
+                float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+                for (int w = 0; w < WM; ++w) {
+                    t1 += red[(w * BN + col) * 2];
+                    t2 += red[(w * BN + col) * 2 + 1];
+                }
+                atomicAdd(&sums[n], (double)t1);
+                atomicAdd(&sums[N + n], (double)t2);
             }
         }
     }
-    if (want_sums) {
-        double* sums = a.epi_relu_bn_bwd ? a.epi_sums : a.out_sums;
+}
+
+// split-K reduction + epilogue: block = [16 rows][64 cols], thread = (col, 4
+// rows); the <= 8 x 4 partial loads of a thread are independent.
+constexpr int MAX_SPLITS = 8;
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_splitk_epi(rnvp_conv_args a, int splits, int shards) {
+    __shared__ float red[4][64][2];
+    __shared__ double tmp[128];
+    __shared__ float etab[4 * 64];
+    const int tid = threadIdx.x, col = tid & 63, rg = tid >> 6;
+    const long long M = (long long)a.B * a.H * a.W;
+    const int N = a.n, cso = a.cs_out;
+    const int n0 = blockIdx.y * 64;
+    const long long m0 = (long long)blockIdx.x * 16 + rg * 4;
+    const int n = n0 + col;
+    if (a.epi_relu_bn_bwd) block_bn_table(a.epi, N, n0, 64, etab, etab + 64, etab + 128, etab + 192, tmp);
+    float bias = 0.f, e_sc = 0.f, e_sf = 0.f, e_mean = 0.f, e_rstd = 1.f;
+    if (n < N) {
+        if (a.bias) bias = a.bias[n];
+        if (a.epi_relu_bn_bwd) {
+            e_sc = etab[col]; e_sf = etab[64 + col]; e_mean = etab[128 + col]; e_rstd = etab[192 + col];
+        }
+    }
+    float accv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (n < N) {
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
+        for (int z = 0; z < MAX_SPLITS; ++z) {
+            if (z < splits) {
+                const float* wz = a.ws + (long long)z * M * N;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (m0 + r < M) accv[r] += wz[(m0 + r) * N + n];
+            }
+        }
+    }
+    float s1 = 0.f, s2 = 0.f;
+    T* Y = (T*)a.y;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const long long m = m0 + r;
+        if (m >= M || n >= cso) continue;
+        const long long o = m * cso + n;
+        float v = 0.f;
+        if (n < N) v = epi_value<T>(a, o, accv[r], bias, e_sc, e_sf, e_mean, e_rstd, s1, s2);
+        stv(&Y[o], v);
+    }
+    const bool want_sums = a.out_sums || (a.epi_relu_bn_bwd && a.epi_sums);
+    if (want_sums) {
+        red[rg][col][0] = s1;
+        red[rg][col][1] = s2;
+        __syncthreads();
+        if (rg == 0 && n < N) {
+            double* sums = shard_ptr(a.epi_relu_bn_bwd ? a.epi_sums : a.out_sums, shards, N);
+            float t1 = red[0][col][0] + red[1][col][0] + red[2][col][0] + red[3][col][0];
+            float t2 = red[0][col][1] + red[1][col][1] + red[2][col][1] + red[3][col][1];
+            atomicAdd(&sums[n], (double)t1);
+            atomicAdd(&sums[N + n], (double)t2);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// register-streaming conv for small channel counts (scales 1-2)
+// ---------------------------------------------------------------------------
+// For K <= ~600 and N <= 64 the whole packed weight matrix fits in LDS, and an
+// MFMA A-fragment row (lane&15) x k-group (lane>>4) is exactly one pixel's
+// 16-byte channel chunk: waves stream A fragments from global/L2 straight into
+// registers (BN+ReLU applied there), no LDS round trip and no barrier in the
+// main loop.  Each wave owns 64-pixel tiles (4 MFMA row tiles) and the next
+// k-step's fragments are loaded before the current MFMAs.
+template <typename T, int NT>
+__global__ __launch_bounds__(256) void k_conv_stream(rnvp_conv_args a, int shards) {
+    constexpr int CH = Mf<T>::CH;
+    constexpr int KS = 4 * CH;             // K per step call (bf16: one 16x16x32, f32: four 16x16x4)
+    constexpr int NC = 16 * NT;            // columns held by a wave
+    extern __shared__ double dsm[];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, li = lane & 15;
+    const long long M = (long long)a.B * a.H * a.W;
+    const int N = a.n, cs = a.cs_in, ks = a.ks, pad = ks >> 1;
+    const int K = ks * ks * cs;
+    const int nsteps = (K + KS - 1) / KS;
+    const int kpl = nsteps * KS + CH;      // LDS row pitch (+16 B: conflict-free column reads)
+    const bool pro = a.pro_bn_relu != 0;
+    const bool epi_bn = a.epi_relu_bn_bwd != 0;
+    const int ntmp = cs > NC ? cs : NC;
+
+    double* tmp = dsm;
+    float* bnp = (float*)(dsm + 2 * ntmp);
+    float* etab = bnp + 2 * cs;
+    float* red = etab + 4 * NC;            // [4 waves][NC][2]
+    T* Wl = (T*)(red + 4 * NC * 2);
+
+    if (pro) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + cs, nullptr, nullptr, tmp);
+    if (epi_bn) block_bn_table(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp);
+    // weights -> LDS (rows >= N and k >= K zero)
+    {
+        const T* Wg = (const T*)a.w;
+        const int cpr = kpl / CH;
+        for (int q = tid; q < NC * cpr; q += 256) {
+            const int r = q / cpr, c = q - r * cpr;
+            u32x4 v = u32x4{0u, 0u, 0u, 0u};
+            if (r < N && c * CH < nsteps * KS) v = *(const u32x4*)(Wg + (long long)r * a.kp + c * CH);
+            *(u32x4*)(Wl + r * kpl + c * CH) = v;
+        }
+    }
+    __syncthreads();
+
+    const T* __restrict__ X = (const T*)a.x;
+    T* __restrict__ Y = (T*)a.y;
+    const int cso = a.cs_out;
+    float bias[NT], e_sc[NT], e_sf[NT], e_mean[NT], e_rstd[NT], s1[NT], s2[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int n = j * 16 + li;
+        bias[j] = (a.bias && n < N) ? a.bias[n] : 0.f;
+        e_sc[j] = epi_bn ? etab[n] : 0.f;
+        e_sf[j] = epi_bn ? etab[NC + n] : 0.f;
+        e_mean[j] = epi_bn ? etab[2 * NC + n] : 0.f;
+        e_rstd[j] = epi_bn ? etab[3 * NC + n] : 1.f;
+        s1[j] = 0.f;
+        s2[j] = 0.f;
+    }
+
+    const long long ntiles = (M + 63) / 64;
+    for (long long t = (long long)blockIdx.x * 4 + wid; t < ntiles; t += (long long)gridDim.x * 4) {
+        long long mrow[4];
+        int yr[4], xr[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const long long m = t * 64 + i * 16 + li;
+            mrow[i] = m < M ? m : -1;
+            const long long mm = m < M ? m : 0;
+            xr[i] = (int)(mm % a.W);
+            yr[i] = (int)((mm / a.W) % a.H);
+        }
+        floatx4 acc[4][NT];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+        u32x4 ra[4];
+        unsigned msk = 0;
+        int cur_ci = 0;
+        auto load = [&](int s) {
+            const int k = s * KS + g * CH;
+            const int tap = k / cs, ci = k - tap * cs;
+            const int dy = tap / ks - pad, dx = tap % ks - pad;
+            cur_ci = ci;
+            msk = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                ra[i] = u32x4{0u, 0u, 0u, 0u};
+                const int yy = yr[i] + dy, xx = xr[i] + dx;
+                if (mrow[i] >= 0 && k < K && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) {
+                    ra[i] = *(const u32x4*)(X + (mrow[i] + (long long)dy * a.W + dx) * cs + ci);
+                    msk |= 1u << i;
+                }
+            }
+        };
+        load(0);
+        for (int s = 0; s < nsteps; ++s) {
+            u32x4 av[4];
+            const int ci = cur_ci;
+            const unsigned mk = msk;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) av[i] = ra[i];
+            if (s + 1 < nsteps) load(s + 1);
+            if (pro) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    if (mk & (1u << i)) {
+                        float f[CH];
+                        unpack(av[i], f, T());
+#pragma unroll
+                        for (int j = 0; j < CH; ++j) f[j] = fmaxf(f[j] * bnp[ci + j] + bnp[cs + ci + j], 0.f);
+                        av[i] = pack(f, T());
+                    }
+                }
+            }
+            u32x4 bv[NT];
+#pragma unroll
+            for (int j = 0; j < NT; ++j) bv[j] = *(const u32x4*)(Wl + (j * 16 + li) * kpl + s * KS + g * CH);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j) Mf<T>::step(av[i], bv[j], acc[i][j]);
+        }
+        // epilogue for this tile
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const long long m = t * 64 + i * 16 + g * 4 + r;
+                if (m >= M) continue;
+#pragma unroll
+                for (int j = 0; j < NT; ++j) {
+                    const int n = j * 16 + li;
+                    if (n >= cso) continue;
+                    const long long o = m * cso + n;
+                    float v = 0.f;
+                    if (n < N) v = epi_value<T>(a, o, acc[i][j][r], bias[j], e_sc[j], e_sf[j], e_mean[j], e_rstd[j],
+                                                s1[j], s2[j]);
+                    stv(&Y[o], v);
+                }
+            }
+    }
+    const bool want_sums = a.out_sums || (epi_bn && a.epi_sums);
+    if (want_sums) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
             s1[j] += __shfl_xor(s1[j], 16, 64);
             s1[j] += __shfl_xor(s1[j], 32, 64);
             s2[j] += __shfl_xor(s2[j], 16, 64);
             s2[j] += __shfl_xor(s2[j], 32, 64);
             if (lane < 16) {
-                const int col = wn * WTN + j * 16 + lane;
-                red[(wm * BN + col) * 2] = s1[j];
-                red[(wm * BN + col) * 2 + 1] = s2[j];
+                red[(wid * NC + j * 16 + lane) * 2] = s1[j];
+                red[(wid * NC + j * 16 + lane) * 2 + 1] = s2[j];
             }
         }
         __syncthreads();
-        for (int col = tid; col < BN; col += 256) {
-            const int n = n0 + col;
-            if (n >= N) continue;
+        double* sums = shard_ptr(epi_bn ? a.epi_sums : a.out_sums, shards, N);
+        for (int n = tid; n < N; n += 256) {
             float t1 = 0.f, t2 = 0.f;
 #pragma unroll
-            for (int w = 0; w < WM; ++w) {
-                t1 += red[(w * BN + col) * 2];
-                t2 += red[(w * BN + col) * 2 + 1];
+            for (int w = 0; w < 4; ++w) {
+                t1 += red[(w * NC + n) * 2];
+                t2 += red[(w * NC + n) * 2 + 1];
             }
             atomicAdd(&sums[n], (double)t1);
             atomicAdd(&sums[N + n], (double)t2);
@@ -220,12 +542,73 @@ __global__ __launch_bounds__(256) void k_conv(rnvp_conv_args a) {
     }
 }
 
+template <typename T>
+size_t stream_lds_bytes(const rnvp_conv_args* a, int nt) {
+    constexpr int CH = Mf<T>::CH, KS = 4 * CH;
+    const int K = a->ks * a->ks * a->cs_in;
+    const int kpl = ((K + KS - 1) / KS) * KS + CH;
+    const int nc = 16 * nt, ntmp = a->cs_in > nc ? a->cs_in : nc;
+    return 16 * (size_t)ntmp + 8 * (size_t)a->cs_in + 16 * (size_t)nc + 32 * (size_t)nc +
+           (size_t)nc * kpl * sizeof(T);
+}
+
+template <typename T, int NT>
+int launch_stream(const rnvp_conv_args* a, hipStream_t s) {
+    const long long M = (long long)a->B * a->H * a->W;
+    const long long ntiles = (M + 63) / 64;
+    long long grid = (ntiles + 3) / 4;
+    if (grid > 1024) grid = 1024;
+    k_conv_stream<T, NT><<<(unsigned)grid, 256, stream_lds_bytes<T>(a, NT), s>>>(*a, rnvp_stat_shards(M));
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+// true when the streaming kernel handles this conv (N <= 64, weights fit LDS)
+template <typename T>
+bool stream_ok(const rnvp_conv_args* a) {
+    if (a->n > 64 || a->cs_in > 64) return false;
+    const int nt = a->n <= 16 ? 1 : (a->n <= 32 ? 2 : 4);
+    return stream_lds_bytes<T>(a, nt) <= 48 * 1024;
+}
+
+template <typename T>
+int dispatch_stream(const rnvp_conv_args* a, hipStream_t s) {
+    if (a->n <= 16) return launch_stream<T, 1>(a, s);
+    if (a->n <= 32) return launch_stream<T, 2>(a, s);
+    return launch_stream<T, 4>(a, s);
+}
+
 template <typename T, int BM, int BN, int WM, int WN>
 int launch_conv(const rnvp_conv_args* a, hipStream_t s) {
+    constexpr int BKS = 8 * Mf<T>::CH;
     const long long M = (long long)a->B * a->H * a->W;
-    dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)((a->n + BN - 1) / BN));
-    size_t shm = a->pro_bn_relu ? 2 * (size_t)a->cs_in * sizeof(float) : 0;
-    k_conv<T, BM, BN, WM, WN><<<grid, 256, shm, s>>>(*a);
+    const int K = a->ks * a->ks * a->cs_in;
+    const int nk = (K + BKS - 1) / BKS;
+    const long long gm = (M + BM - 1) / BM, gn = (a->n + BN - 1) / BN;
+    const long long grid = gm * gn;
+    const int shards = rnvp_stat_shards(M);
+    const int cs = a->cs_in;
+    const size_t shm = 16 * (size_t)(cs > BN ? cs : BN) + 8 * (size_t)cs + 16 * (size_t)BN;
+    int splits = 1;
+    if (a->ws && grid < 384 && nk >= 8) {
+        splits = (int)((512 + grid - 1) / grid);
+        if (splits > MAX_SPLITS) splits = MAX_SPLITS;
+        if (splits > nk / 4) splits = nk / 4;
+        while (splits > 1 && (long long)splits * M * a->n > a->ws_elems) --splits;
+    }
+    if (splits > 1) {
+        const int kps = (nk + splits - 1) / splits;
+        splits = (nk + kps - 1) / kps;
+        dim3 g1((unsigned)gm, (unsigned)gn, (unsigned)splits);
+        k_conv<T, BM, BN, WM, WN, true><<<g1, 256, shm, s>>>(*a, kps, shards);
+        RNVP_LAUNCH_CHECK();
+        dim3 g2((unsigned)((M + 15) / 16), (unsigned)((a->cs_out + 63) / 64));
+        k_splitk_epi<T><<<g2, 256, 0, s>>>(*a, splits, shards);
+        RNVP_LAUNCH_CHECK();
+        return RNVP_OK;
+    }
+    dim3 g1((unsigned)gm, (unsigned)gn, 1);
+    k_conv<T, BM, BN, WM, WN, false><<<g1, 256, shm, s>>>(*a, nk, shards);
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
 }
@@ -233,29 +616,35 @@ int launch_conv(const rnvp_conv_args* a, hipStream_t s) {
 template <typename T>
 int dispatch_conv(const rnvp_conv_args* a, hipStream_t s) {
     const long long M = (long long)a->B * a->H * a->W;
+    if (stream_ok<T>(a)) return dispatch_stream<T>(a, s);
+    // largest tile that still gives >= 512 workgroups (2 per CU); small grids
+    // fall through to 64x64 tiles and split K
     if (a->n <= 16) return launch_conv<T, 128, 16, 4, 1>(a, s);
-    if (a->n <= 32) return launch_conv<T, 128, 32, 4, 1>(a, s);
-    if (a->n <= 64) return launch_conv<T, 128, 64, 2, 2>(a, s);
-    if (M >= 16384) return launch_conv<T, 128, 128, 2, 2>(a, s);
-    return launch_conv<T, 64, 128, 1, 4>(a, s);
+    if (a->n <= 32) return M >= 512 * 128 ? launch_conv<T, 128, 32, 4, 1>(a, s) : launch_conv<T, 64, 32, 4, 1>(a, s);
+    if (a->n <= 64) return M >= 512 * 128 ? launch_conv<T, 128, 64, 2, 2>(a, s) : launch_conv<T, 64, 64, 2, 2>(a, s);
+    const long long g128 = ((M + 127) / 128) * ((a->n + 127) / 128);
+    if (g128 >= 512) return launch_conv<T, 128, 128, 2, 2>(a, s);
+    return launch_conv<T, 64, 64, 2, 2>(a, s);
 }
 
 // ---------------------------------------------------------------------------
 // weight gradient
 // ---------------------------------------------------------------------------
-// Output tile [64 co][64 k]; 4 waves as 2x2 of 32x32.  Per stage BKM pixels
-// (32 bf16 / 16 f32) of dy (P) and act(x) (Q) are staged row-major [m][col];
-// MFMA operands are columns, read transposed.
+// Output tile [64 co][64 k]; 4 waves as 2x2 of 32x32.  A stage is STG pixels
+// (64 bf16 / 32 f32) of dy (P) and act(x) (Q), staged row-major [m][col] in
+// double-buffered LDS; MFMA operands are columns, read transposed
+// (ds_read_b64_tr_b16 for bf16).
 template <typename T>
 __global__ __launch_bounds__(256) void k_wgrad(rnvp_wgrad_args a, long long m_per_block) {
     constexpr int CH = Mf<T>::CH;
-    constexpr int BKM = (sizeof(T) == 2) ? 32 : 16;
-    constexpr int CPR = 64 / CH;           // chunks per 64-element row
-    constexpr int ROWB = 64 * sizeof(T) + 16;   // padded row bytes
-    __shared__ __attribute__((aligned(16))) char Ps[BKM * ROWB];
-    __shared__ __attribute__((aligned(16))) char Qs[BKM * ROWB];
+    constexpr int STG = (sizeof(T) == 2) ? 64 : 32;   // pixels per stage (two MFMA K-steps)
+    constexpr int CPR = 64 / CH;                      // chunks per 64-column row
+    constexpr int ROWB = 64 * sizeof(T) + 16;         // padded row bytes
+    constexpr int PER = STG * CPR / 256;              // chunks per thread per operand (2)
+    __shared__ __attribute__((aligned(16))) char Ps[2][STG * ROWB];
+    __shared__ __attribute__((aligned(16))) char Qs[2][STG * ROWB];
     __shared__ float dbs[64];
-    extern __shared__ float bnp[];
+    extern __shared__ double dsm[];   // tmp [2*cs] fp64 | bnp scale [cs] | shift [cs]
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wc = wid >> 1, wk = wid & 1;
@@ -268,114 +657,143 @@ __global__ __launch_bounds__(256) void k_wgrad(rnvp_wgrad_args a, long long m_pe
     const T* __restrict__ X = (const T*)a.x;
     const T* __restrict__ DY = (const T*)a.dy;
     const bool do_bias = a.dbias && blockIdx.y == 0;
+    const bool pro = a.pro_bn_relu != 0;
 
-    if (a.pro_bn_relu) {
-        for (int c = tid; c < cs; c += 256) {
-            float sc = 0.f, sf = 0.f;
-            if (c < a.cin) bn_affine(a.pro, a.cin, c, sc, sf);
-            bnp[c] = sc;
-            bnp[cs + c] = sf;
-        }
-    }
+    float* bnp = (float*)(dsm + 2 * cs);
+    if (pro) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + cs, nullptr, nullptr, dsm);
     if (tid < 64) dbs[tid] = 0.f;
-    // staging coordinates: row r (pixel), chunk c (column group)
-    const int sr = tid / CPR, sc = tid % CPR;
-    const int pk = k0 + sc * CH;                 // Q column
+    const int sc_ = tid % CPR;
+    const int pk = k0 + sc_ * CH;                // Q column
     const int ptap = pk / cs, pci = pk - ptap * cs;
     const int pdy = ptap / ks - pad, pdx = ptap % ks - pad;
-    const int pco = co0 + sc * CH;               // P column
+    const int pco = co0 + sc_ * CH;              // P column
 
     floatx4 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    __syncthreads();
 
-    for (long long mt = mb; mt < me; mt += BKM) {
-        const long long m = mt + sr;
-        // P: dy[m][co]
-        {
-            u32x4 v = u32x4{0u, 0u, 0u, 0u};
-            if (m < me && pco < N) v = *(const u32x4*)(DY + m * a.cs_dy + pco);
-            *(u32x4*)(Ps + sr * ROWB + sc * 16) = v;
-        }
-        // Q: act(x)[m + tap][ci]
-        {
-            u32x4 v = u32x4{0u, 0u, 0u, 0u};
-            if (m < me && pk < K) {
-                const int xx = (int)(m % a.W), yy = (int)((m / a.W) % a.H);
-                const int y2 = yy + pdy, x2 = xx + pdx;
-                if (y2 >= 0 && y2 < a.H && x2 >= 0 && x2 < a.W) {
-                    v = *(const u32x4*)(X + (m + (long long)pdy * a.W + pdx) * cs + pci);
-                    if (a.pro_bn_relu) {
-                        float f[CH];
-                        unpack(v, f, T());
+    u32x4 rp[PER], rq[PER];
+    unsigned qmask = 0;
+    auto gload = [&](long long mt) {
+        qmask = 0;
 #pragma unroll
-                        for (int j = 0; j < CH; ++j) f[j] = fmaxf(f[j] * bnp[pci + j] + bnp[cs + pci + j], 0.f);
-                        v = pack(f, T());
+        for (int i = 0; i < PER; ++i) {
+            const int r = (tid + i * 256) / CPR;
+            const long long m = mt + r;
+            rp[i] = u32x4{0u, 0u, 0u, 0u};
+            rq[i] = u32x4{0u, 0u, 0u, 0u};
+            if (m < me) {
+                if (pco < N) rp[i] = *(const u32x4*)(DY + m * a.cs_dy + pco);
+                if (pk < K) {
+                    const int xx = (int)(m % a.W), yy = (int)((m / a.W) % a.H);
+                    const int y2 = yy + pdy, x2 = xx + pdx;
+                    if (y2 >= 0 && y2 < a.H && x2 >= 0 && x2 < a.W) {
+                        rq[i] = *(const u32x4*)(X + (m + (long long)pdy * a.W + pdx) * cs + pci);
+                        qmask |= 1u << i;
                     }
                 }
             }
-            *(u32x4*)(Qs + sr * ROWB + sc * 16) = v;
         }
-        __syncthreads();
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int r = (tid + i * 256) / CPR;
+            u32x4 v = rq[i];
+            if (pro) {
+                if (qmask & (1u << i)) {
+                    float f[CH];
+                    unpack(v, f, T());
+#pragma unroll
+                    for (int j = 0; j < CH; ++j) f[j] = fmaxf(f[j] * bnp[pci + j] + bnp[cs + pci + j], 0.f);
+                    v = pack(f, T());
+                } else {
+                    v = u32x4{0u, 0u, 0u, 0u};
+                }
+            }
+            *(u32x4*)(Ps[buf] + r * ROWB + sc_ * 16) = rp[i];
+            *(u32x4*)(Qs[buf] + r * ROWB + sc_ * 16) = v;
+        }
+    };
+
+    __syncthreads();
+    if (mb < me) {
+        gload(mb);
+        lstore(0);
+    }
+    __syncthreads();
+    const int g = lane >> 4, li = lane & 15;
+    int it = 0;
+    for (long long mt = mb; mt < me; mt += STG, ++it) {
+        const int cur = it & 1;
+        const bool more = mt + STG < me;
+        if (more) gload(mt + STG);
         if (do_bias && tid < 64) {
             float t = 0.f;
-            for (int r = 0; r < BKM; ++r) t += ldv((const T*)(Ps + r * ROWB) + tid);
+            for (int r = 0; r < STG; ++r) t += ldv((const T*)(Ps[cur] + r * ROWB) + tid);
             dbs[tid] += t;
         }
-        const int g = lane >> 4, li = lane & 15;
         if constexpr (sizeof(T) == 2) {
             const int q = li >> 2, p = li & 3;
-            u32x4 af[2], bfr[2];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int c0 = wc * 32 + i * 16 + 4 * p;
-                i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)(Ps + (8 * g + q) * ROWB + c0 * 2));
-                i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)(Ps + (8 * g + 4 + q) * ROWB + c0 * 2));
-                af[i].x = (uint32_t)(uint16_t)lo.x | ((uint32_t)(uint16_t)lo.y << 16);
-                af[i].y = (uint32_t)(uint16_t)lo.z | ((uint32_t)(uint16_t)lo.w << 16);
-                af[i].z = (uint32_t)(uint16_t)hi.x | ((uint32_t)(uint16_t)hi.y << 16);
-                af[i].w = (uint32_t)(uint16_t)hi.z | ((uint32_t)(uint16_t)hi.w << 16);
+            for (int s = 0; s < 2; ++s) {
+                u32x4 af[2], bfr[2];
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const int c0 = wc * 32 + i * 16 + 4 * p;
+                    const char* base = Ps[cur] + (32 * s + 8 * g + q) * ROWB + c0 * 2;
+                    i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)base);
+                    i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)(base + 4 * ROWB));
+                    af[i].x = (uint32_t)(uint16_t)lo.x | ((uint32_t)(uint16_t)lo.y << 16);
+                    af[i].y = (uint32_t)(uint16_t)lo.z | ((uint32_t)(uint16_t)lo.w << 16);
+                    af[i].z = (uint32_t)(uint16_t)hi.x | ((uint32_t)(uint16_t)hi.y << 16);
+                    af[i].w = (uint32_t)(uint16_t)hi.z | ((uint32_t)(uint16_t)hi.w << 16);
+                }
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int c0 = wk * 32 + j * 16 + 4 * p;
+                    const char* base = Qs[cur] + (32 * s + 8 * g + q) * ROWB + c0 * 2;
+                    i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)base);
+                    i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)(base + 4 * ROWB));
+                    bfr[j].x = (uint32_t)(uint16_t)lo.x | ((uint32_t)(uint16_t)lo.y << 16);
+                    bfr[j].y = (uint32_t)(uint16_t)lo.z | ((uint32_t)(uint16_t)lo.w << 16);
+                    bfr[j].z = (uint32_t)(uint16_t)hi.x | ((uint32_t)(uint16_t)hi.y << 16);
+                    bfr[j].w = (uint32_t)(uint16_t)hi.z | ((uint32_t)(uint16_t)hi.w << 16);
+                }
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) Mf<bf16_t>::step(af[i], bfr[j], acc[i][j]);
             }
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int c0 = wk * 32 + j * 16 + 4 * p;
-                i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)(Qs + (8 * g + q) * ROWB + c0 * 2));
-                i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)(Qs + (8 * g + 4 + q) * ROWB + c0 * 2));
-                bfr[j].x = (uint32_t)(uint16_t)lo.x | ((uint32_t)(uint16_t)lo.y << 16);
-                bfr[j].y = (uint32_t)(uint16_t)lo.z | ((uint32_t)(uint16_t)lo.w << 16);
-                bfr[j].z = (uint32_t)(uint16_t)hi.x | ((uint32_t)(uint16_t)hi.y << 16);
-                bfr[j].w = (uint32_t)(uint16_t)hi.z | ((uint32_t)(uint16_t)hi.w << 16);
-            }
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j) Mf<bf16_t>::step(af[i], bfr[j], acc[i][j]);
         } else {
-            u32x4 af[2], bfr[2];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const float* pcol = (const float*)Ps + wc * 32 + i * 16 + li;
-                af[i].x = __float_as_uint(*(const float*)((const char*)pcol + (4 * g + 0) * ROWB));
-                af[i].y = __float_as_uint(*(const float*)((const char*)pcol + (4 * g + 1) * ROWB));
-                af[i].z = __float_as_uint(*(const float*)((const char*)pcol + (4 * g + 2) * ROWB));
-                af[i].w = __float_as_uint(*(const float*)((const char*)pcol + (4 * g + 3) * ROWB));
+            for (int s = 0; s < 2; ++s) {
+                u32x4 af[2], bfr[2];
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const char* pcol = Ps[cur] + (16 * s + 4 * g) * ROWB + (wc * 32 + i * 16 + li) * 4;
+                    af[i].x = *(const uint32_t*)(pcol);
+                    af[i].y = *(const uint32_t*)(pcol + ROWB);
+                    af[i].z = *(const uint32_t*)(pcol + 2 * ROWB);
+                    af[i].w = *(const uint32_t*)(pcol + 3 * ROWB);
+                }
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const char* qcol = Qs[cur] + (16 * s + 4 * g) * ROWB + (wk * 32 + j * 16 + li) * 4;
+                    bfr[j].x = *(const uint32_t*)(qcol);
+                    bfr[j].y = *(const uint32_t*)(qcol + ROWB);
+                    bfr[j].z = *(const uint32_t*)(qcol + 2 * ROWB);
+                    bfr[j].w = *(const uint32_t*)(qcol + 3 * ROWB);
+                }
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) Mf<float>::step(af[i], bfr[j], acc[i][j]);
             }
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const float* qcol = (const float*)Qs + wk * 32 + j * 16 + li;
-                bfr[j].x = __float_as_uint(*(const float*)((const char*)qcol + (4 * g + 0) * ROWB));
-                bfr[j].y = __float_as_uint(*(const float*)((const char*)qcol + (4 * g + 1) * ROWB));
-                bfr[j].z = __float_as_uint(*(const float*)((const char*)qcol + (4 * g + 2) * ROWB));
-                bfr[j].w = __float_as_uint(*(const float*)((const char*)qcol + (4 * g + 3) * ROWB));
-            }
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j) Mf<float>::step(af[i], bfr[j], acc[i][j]);
         }
+        if (more) lstore(cur ^ 1);
         __syncthreads();
     }
     // D rows = co, cols = k
@@ -394,18 +812,20 @@ __global__ __launch_bounds__(256) void k_wgrad(rnvp_wgrad_args a, long long m_pe
 
 template <typename T>
 int launch_wgrad(const rnvp_wgrad_args* a, hipStream_t s) {
-    constexpr int BKM = (sizeof(T) == 2) ? 32 : 16;
+    constexpr int STG = (sizeof(T) == 2) ? 64 : 32;
     const long long M = (long long)a->B * a->H * a->W;
     const int K = a->ks * a->ks * a->cs_in;
     const int tco = (a->n + 63) / 64, tk = (K + 63) / 64;
-    long long steps = (M + BKM - 1) / BKM;
-    long long z = 1024 / (tco * tk);
+    long long steps = (M + STG - 1) / STG;
+    // enough blocks to fill the chip, but at most 128 fp32 adders per dw word
+    long long z = (1024 + tco * tk - 1) / (tco * tk);
+    if (z > 128) z = 128;
     if (z < 1) z = 1;
     if (z > steps) z = steps;
-    long long mpb = ((steps + z - 1) / z) * BKM;
+    long long mpb = ((steps + z - 1) / z) * STG;
     z = (M + mpb - 1) / mpb;
     dim3 grid((unsigned)tco, (unsigned)tk, (unsigned)z);
-    size_t shm = a->pro_bn_relu ? 2 * (size_t)a->cs_in * sizeof(float) : 0;
+    size_t shm = 24 * (size_t)a->cs_in;
     k_wgrad<T><<<grid, 256, shm, s>>>(*a, mpb);
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
@@ -417,23 +837,29 @@ int launch_wgrad(const rnvp_wgrad_args* a, hipStream_t s) {
 template <typename T>
 __global__ void k_bn_bwd(rnvp_bn_bwd_args a) {
     constexpr int CH = Mf<T>::CH;
-    extern __shared__ float p[];   // per channel: coef, k1, k2, mean, rstd
+    extern __shared__ double dsm[];   // tmp [2*cs] | gsum [2*cs] fp64 | p [5*cs] f32
     const int cs = a.cs, C = a.C;
     const double cnt = (double)a.M;
+    double* gs = dsm + 2 * cs;
+    float* p = (float*)(dsm + 4 * cs);   // per channel: coef, k1, k2, mean, rstd
+    float* t_sc = p + 5 * cs;            // scratch: scale, shift, mean, rstd [cs each]
+    block_bn_table(a.bn, C, 0, cs, t_sc, t_sc + cs, t_sc + 2 * cs, t_sc + 3 * cs, dsm);
+    block_shard_sums(a.sums, C, a.sum_shards, 0, C, gs, gs + cs);
     for (int c = threadIdx.x; c < cs; c += blockDim.x) {
         float coef = 0.f, k1 = 0.f, k2 = 0.f, mean = 0.f, rstd = 1.f;
         if (c < C) {
-            float sc, sf;
-            bn_affine(a.bn, C, c, sc, sf, &mean, &rstd);
+            mean = t_sc[2 * cs + c];
+            rstd = t_sc[3 * cs + c];
             const float gam = a.bn.gamma ? a.bn.gamma[c] : 1.f;
             coef = gam * rstd;
+            const double g1 = gs[c], g2 = gs[cs + c];
             if (a.bn.sums) {   // train mode: batch statistics carry gradient
-                k1 = (float)(a.sums[c] / cnt);
-                k2 = (float)(a.sums[C + c] / cnt);
+                k1 = (float)(g1 / cnt);
+                k2 = (float)(g2 / cnt);
             }
             if (blockIdx.x == 0) {
-                if (a.dbeta) a.dbeta[c] = (float)a.sums[c];
-                if (a.dgamma) a.dgamma[c] = (float)a.sums[C + c];
+                if (a.dbeta) a.dbeta[c] = (float)g1;
+                if (a.dgamma) a.dgamma[c] = (float)g2;
             }
         }
         p[5 * c] = coef; p[5 * c + 1] = k1; p[5 * c + 2] = k2; p[5 * c + 3] = mean; p[5 * c + 4] = rstd;
@@ -557,7 +983,7 @@ extern "C" int rnvp_conv2d(const rnvp_conv_args* a, void* stream) {
     if (a->ks != 1 && a->ks != 3) return RNVP_E_UNSUPPORTED;
     if (a->B < 0 || a->H <= 0 || a->W <= 0 || a->n <= 0 || a->cin <= 0) return RNVP_E_INVALID;
     if ((a->cs_in & 7) || (a->cs_out & 7) || a->cs_in < a->cin || a->cs_out < a->n) return RNVP_E_INVALID;
-    if ((a->kp & 31) || a->kp < a->ks * a->ks * a->cs_in) return RNVP_E_INVALID;
+    if ((a->kp & 63) || a->kp < a->ks * a->ks * a->cs_in) return RNVP_E_INVALID;
     if (!al16(a->x) || !al16(a->w)) return RNVP_E_INVALID;
     if (a->epi_relu_bn_bwd && !a->epi_x) return RNVP_E_INVALID;
     if (a->B == 0) return RNVP_OK;
@@ -581,13 +1007,14 @@ extern "C" int rnvp_conv2d_wgrad(const rnvp_wgrad_args* a, void* stream) {
 extern "C" int rnvp_bn_bwd_apply(const rnvp_bn_bwd_args* a, void* stream) {
     if (!a || !a->g || !a->x || !a->dx || !a->sums || a->M < 0 || a->C <= 0 || (a->cs & 7) || a->cs < a->C)
         return RNVP_E_INVALID;
+    if (a->sum_shards < 1) return RNVP_E_INVALID;
     if (a->dtype != RNVP_F32 && a->dtype != RNVP_BF16) return RNVP_E_INVALID;
     if (!al16(a->g) || !al16(a->x) || !al16(a->dx) || (a->residual && !al16(a->residual))) return RNVP_E_INVALID;
     if (a->M == 0) return RNVP_OK;
     hipStream_t s = (hipStream_t)stream;
     const int CH = a->dtype == RNVP_F32 ? 4 : 8;
     const long long nch = a->M * (a->cs / CH);
-    size_t shm = 5 * (size_t)a->cs * sizeof(float);
+    size_t shm = 68 * (size_t)a->cs;   // 4*cs fp64 + 9*cs f32 (see k_bn_bwd)
     if (a->dtype == RNVP_F32) k_bn_bwd<float><<<rnvp_grid(nch, 256, 2048), 256, shm, s>>>(*a);
     else k_bn_bwd<bf16_t><<<rnvp_grid(nch, 256, 2048), 256, shm, s>>>(*a);
     RNVP_LAUNCH_CHECK();

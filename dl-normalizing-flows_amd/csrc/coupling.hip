@@ -82,6 +82,7 @@ __global__ void k_in_apply(rnvp_coupling_args a) {
     const double cnt = (double)g.B * g.HW;
     for (int c = threadIdx.x; c < g.Cb; c += blockDim.x) {
         rnvp_bn_src s;
+        s.shards = 1;
         s.sums = a.training ? a.in_sums : nullptr;
         s.count = cnt;
         s.mean = a.in_rmean; s.var = a.in_rvar;
@@ -424,6 +425,7 @@ __device__ __forceinline__ void in_bwd_vals(const rnvp_coupling_args& a, const G
 __device__ __forceinline__ void in_bn_params(const rnvp_coupling_args& a, const Geo& g, int cb, float& sc, float& sf,
                                              float& mean, float& rstd) {
     rnvp_bn_src s;
+    s.shards = 1;
     s.sums = a.training ? a.in_sums : nullptr;
     s.count = (double)g.B * g.HW;
     s.mean = a.in_rmean; s.var = a.in_rvar;

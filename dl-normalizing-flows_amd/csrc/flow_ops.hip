@@ -244,10 +244,12 @@ extern "C" int rnvp_prior_logprob_bwd(const float* z, const float* gout, float* 
 // BatchNorm running statistics (torch BatchNorm2d train-mode semantics)
 // ---------------------------------------------------------------------------
 __global__ void k_bn_running(const rnvp_bn_running* __restrict__ d, float mom) {
+    extern __shared__ double tmp[];   // [2*C]
     const rnvp_bn_running r = d[blockIdx.x];
+    block_shard_sums(r.sums, r.C, r.shards, 0, r.C, tmp, tmp + r.C);
     for (int c = threadIdx.x; c < r.C; c += blockDim.x) {
-        double mean = r.sums[c] / r.count;
-        double var = r.sums[r.C + c] / r.count - mean * mean;
+        double mean = tmp[c] / r.count;
+        double var = tmp[r.C + c] / r.count - mean * mean;
         if (var < 0) var = 0;
         double unb = r.count > 1 ? var * r.count / (r.count - 1) : var;
         r.rmean[c] = (1.f - mom) * r.rmean[c] + mom * (float)mean;
@@ -256,10 +258,10 @@ __global__ void k_bn_running(const rnvp_bn_running* __restrict__ d, float mom) {
     if (threadIdx.x == 0 && r.nbt) r.nbt[0] += 1;
 }
 
-extern "C" int rnvp_bn_running_update(const rnvp_bn_running* d, int n, float momentum, void* stream) {
-    if (n < 0 || (n > 0 && !d)) return RNVP_E_INVALID;
+extern "C" int rnvp_bn_running_update(const rnvp_bn_running* d, int n, int max_c, float momentum, void* stream) {
+    if (n < 0 || (n > 0 && !d) || max_c <= 0) return RNVP_E_INVALID;
     if (n == 0) return RNVP_OK;
-    k_bn_running<<<n, 256, 0, (hipStream_t)stream>>>(d, momentum);
+    k_bn_running<<<n, 256, 16 * (size_t)max_c, (hipStream_t)stream>>>(d, momentum);
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
 }

@@ -20,11 +20,12 @@ f64 = C.c_double
 
 
 class BNSrc(C.Structure):
-    _fields_ = [("sums", vp), ("count", f64), ("mean", vp), ("var", vp), ("gamma", vp), ("beta", vp), ("eps", f32)]
+    _fields_ = [("sums", vp), ("count", f64), ("mean", vp), ("var", vp), ("gamma", vp), ("beta", vp), ("eps", f32),
+                ("shards", i32)]
 
 
 class BNRunning(C.Structure):
-    _fields_ = [("sums", vp), ("count", f64), ("C", i32), ("pad", i32), ("rmean", vp), ("rvar", vp), ("nbt", vp)]
+    _fields_ = [("sums", vp), ("count", f64), ("C", i32), ("shards", i32), ("rmean", vp), ("rvar", vp), ("nbt", vp)]
 
 
 class ConvArgs(C.Structure):
@@ -35,7 +36,8 @@ class ConvArgs(C.Structure):
                 ("bias", vp), ("residual", vp), ("accumulate", i32),
                 ("pro_bn_relu", i32), ("pro", BNSrc),
                 ("out_sums", vp),
-                ("epi_relu_bn_bwd", i32), ("epi_x", vp), ("epi", BNSrc), ("epi_sums", vp)]
+                ("epi_relu_bn_bwd", i32), ("epi_x", vp), ("epi", BNSrc), ("epi_sums", vp),
+                ("ws", vp), ("ws_elems", i64)]
 
 
 class WgradArgs(C.Structure):
@@ -48,7 +50,7 @@ class WgradArgs(C.Structure):
 
 class BNBwdArgs(C.Structure):
     _fields_ = [("dtype", i32), ("M", i64), ("C", i32), ("cs", i32),
-                ("g", vp), ("x", vp), ("bn", BNSrc), ("sums", vp),
+                ("g", vp), ("x", vp), ("bn", BNSrc), ("sums", vp), ("sum_shards", i32),
                 ("dx", vp), ("residual", vp), ("accumulate", i32),
                 ("dgamma", vp), ("dbeta", vp)]
 
@@ -96,7 +98,8 @@ _SIGS = {
     "rnvp_logit_inv": (i32, [vp, vp, f32, i64, vp]),
     "rnvp_prior_logprob": (i32, [vp, vp, vp, i32, i32, vp]),
     "rnvp_prior_logprob_bwd": (i32, [vp, vp, vp, i32, i32, vp]),
-    "rnvp_bn_running_update": (i32, [vp, i32, f32, vp]),
+    "rnvp_bn_running_update": (i32, [vp, i32, i32, f32, vp]),
+    "rnvp_stat_shards": (i32, [i64]),
     "rnvp_conv2d": (i32, [C.POINTER(ConvArgs), vp]),
     "rnvp_conv2d_wgrad": (i32, [C.POINTER(WgradArgs), vp]),
     "rnvp_bn_bwd_apply": (i32, [C.POINTER(BNBwdArgs), vp]),
@@ -125,7 +128,8 @@ class _Lib:
             fn = getattr(self.dll, name)
             fn.restype = res
             fn.argtypes = args
-            setattr(self, name[len("rnvp_"):], self._wrap(name, fn) if res is i32 and name != "rnvp_version" else fn)
+            raw = name in ("rnvp_version", "rnvp_stat_shards") or res is not i32
+            setattr(self, name[len("rnvp_"):], fn if raw else self._wrap(name, fn))
 
     def _wrap(self, name, fn):
         dll = self.dll

@@ -85,8 +85,31 @@ class Arena:
         return s, o + nb
 
 
-def _bn_src(sums, count, mean, var, gamma, beta):
-    return BNSrc(sums or None, float(count), mean or None, var or None, gamma or None, beta or None, BN_EPS)
+def _bn_src(sums, count, mean, var, gamma, beta, shards=1):
+    return BNSrc(sums or None, float(count), mean or None, var or None, gamma or None, beta or None, BN_EPS,
+                 int(shards))
+
+
+def stat_shards(M):
+    return int(_lib.lib().stat_shards(int(M)))
+
+
+_SPLITK_WS = {}
+
+
+def splitk_workspace(device, elems):
+    """Per-device fp32 split-K workspace shared by every conv launch (all
+    engine launches are ordered on the caller's stream)."""
+    key = str(device)
+    t = _SPLITK_WS.get(key)
+    if t is None or t.numel() < elems:
+        t = torch.empty(max(elems, 1 << 16), dtype=torch.float32, device=device)
+        _SPLITK_WS[key] = t
+    return t
+
+
+def splitk_elems(M, nmax):
+    return 8 * M * nmax if M <= 16384 else 0
 
 
 class CouplingEngine:
@@ -140,8 +163,8 @@ class CouplingEngine:
         geo = OrderedDict()
         for name, spec in self.P.convs.items():
             cs_in, cs_out = chan_stride(spec.cin), chan_stride(spec.cout)
-            kp_f = round_up(spec.ks * spec.ks * cs_in, 32)
-            kp_d = round_up(spec.ks * spec.ks * cs_out, 32)
+            kp_f = round_up(spec.ks * spec.ks * cs_in, 64)
+            kp_d = round_up(spec.ks * spec.ks * cs_out, 64)
             geo[name] = (cs_in, cs_out, kp_f, kp_d)
             ar.add("wf:" + name, spec.cout * kp_f * esz)
             ar.add("wd:" + name, spec.cin * kp_d * esz)
@@ -187,21 +210,23 @@ class CouplingEngine:
         ar.add("u", B * self.C * H * W * 4)
         ar.add("in_sums", 2 * self.Cb * 8)
         ar.add("out_sums", 2 * self.Cb * 8)
+        sh = stat_shards(M)
         for bn, spec in self.P.bns.items():
-            ar.add("s:" + bn, 2 * spec.c * 8)
+            ar.add("s:" + bn, sh * 2 * spec.c * 8)
         ar.alloc(device)
-        sv = dict(arena=ar, B=B, H=H, W=W, dtype=dtype, training=training)
+        sv = dict(arena=ar, B=B, H=H, W=W, dtype=dtype, training=training, shards=sh)
         # running-stat update table for the net BNs
         if training and self.P.bns:
             T = self._tensors()
             rows = []
             for bn, spec in self.P.bns.items():
-                r = BNRunning(ar.ptr("s:" + bn), float(M), spec.c, 0, T[bn + "running_mean"].data_ptr(),
+                r = BNRunning(ar.ptr("s:" + bn), float(M), spec.c, sh, T[bn + "running_mean"].data_ptr(),
                               T[bn + "running_var"].data_ptr(), T[bn + "num_batches_tracked"].data_ptr())
                 rows.append(r)
             tab = (BNRunning * len(rows))(*rows)
             sv["bn_table"] = torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(device)
             sv["bn_n"] = len(rows)
+            sv["bn_cmax"] = max(spec.c for spec in self.P.bns.values())
         return sv
 
     def scratch(self, B, H, W, dtype, device):
@@ -223,8 +248,9 @@ class CouplingEngine:
         ar.add("bwd_sums", 3 * self.Cb * 8)
         ar.add("in_bwd_sums", 2 * self.Cb * 8)
         last = "in_bwd_sums"
+        sh = stat_shards(M)
         for bn, spec in self.P.bns.items():
-            ar.add("e:" + bn, 2 * spec.c * 8)
+            ar.add("e:" + bn, sh * 2 * spec.c * 8)
             last = "e:" + bn
         zr = ar.range_bytes(first, last)
         for b, ch in self.P.buf_ch.items():
@@ -240,8 +266,11 @@ class CouplingEngine:
             e.dw = ar.ptr("dw:" + name)
             descs.append(e)
         tab = (WNDesc * len(descs))(*descs)
+        nmax = max(max(s.cin, s.cout) for s in self.P.convs.values())
+        wse = splitk_elems(M, nmax)
         sc = dict(arena=ar, zero=zr, wn_table=torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(device),
-                  wn_key=wsz["key"], wn_rows=wsz["rows"], n_wn=len(descs))
+                  wn_key=wsz["key"], wn_rows=wsz["rows"], n_wn=len(descs), shards=sh,
+                  ws=splitk_workspace(device, wse) if wse else None, ws_elems=wse)
         self._scratch[key] = sc
         return sc
 
@@ -265,7 +294,8 @@ class CouplingEngine:
 
     def _bn(self, T, bn, training, sums_ptr, M):
         return _bn_src(sums_ptr if training else None, M, T[bn + "running_mean"].data_ptr(),
-                       T[bn + "running_var"].data_ptr(), T[bn + "weight"].data_ptr(), T[bn + "bias"].data_ptr())
+                       T[bn + "running_var"].data_ptr(), T[bn + "weight"].data_ptr(), T[bn + "bias"].data_ptr(),
+                       stat_shards(M))
 
     def _net_forward(self, T, sv, ws, training, s):
         L = _lib.lib()
@@ -274,6 +304,7 @@ class CouplingEngine:
         M = B * H * W
         dt = DTYPES[sv["dtype"]][0]
         war = ws["arena"]
+        sc = self.scratch(B, H, W, sv["dtype"], ar.buf.device)
         for op in self.P.ops:
             spec = self.P.convs[op.conv]
             cs_in, cs_out, kp_f, _ = ws["geo"][op.conv]
@@ -290,6 +321,8 @@ class CouplingEngine:
                 a.pro_bn_relu = 1
                 a.pro = self._bn(T, op.pro_bn, training, ar.ptr("s:" + op.pro_bn), M)
             a.out_sums = ar.ptr("s:" + op.stats_bn) if (op.stats_bn and training) else None
+            if sc["ws"] is not None:
+                a.ws, a.ws_elems = sc["ws"].data_ptr(), sc["ws_elems"]
             esz = DTYPES[sv["dtype"]][1]
             nb = esz * (M * cs_in + spec.cout * kp_f + M * cs_out * (1 + int(bool(op.residual)) + int(op.accumulate)))
             _launch("conv_fwd", nb, 2.0 * M * spec.cout * spec.ks * spec.ks * spec.cin, L.conv2d, C.byref(a), s)
@@ -321,7 +354,7 @@ class CouplingEngine:
         L.coupling_in_fwd(C.byref(a), s)
         self._net_forward(T, sv, ws, training, s)
         if training and "bn_table" in sv:
-            L.bn_running_update(sv["bn_table"].data_ptr(), sv["bn_n"], BN_MOMENTUM, s)
+            L.bn_running_update(sv["bn_table"].data_ptr(), sv["bn_n"], sv["bn_cmax"], BN_MOMENTUM, s)
         a.st = ar.ptr("st")
         a.u, a.z = ar.ptr("u"), z.data_ptr()
         a.out_sums = ar.ptr("out_sums")
@@ -349,7 +382,7 @@ class CouplingEngine:
         L.coupling_in_fwd(C.byref(a), s)
         self._net_forward(T, sv, ws, training, s)
         if training and "bn_table" in sv:
-            L.bn_running_update(sv["bn_table"].data_ptr(), sv["bn_n"], BN_MOMENTUM, s)
+            L.bn_running_update(sv["bn_table"].data_ptr(), sv["bn_n"], sv["bn_cmax"], BN_MOMENTUM, s)
         out = torch.empty_like(x)
         ldj = torch.empty_like(x)
         a.st = ar.ptr("st")
@@ -417,6 +450,8 @@ class CouplingEngine:
                     c.epi_x = ar.ptr(op.x)
                     c.epi = self._bn(T, op.pro_bn, training, ar.ptr("s:" + op.pro_bn), M)
                     c.epi_sums = sar.ptr("e:" + op.pro_bn)
+                if sc["ws"] is not None:
+                    c.ws, c.ws_elems = sc["ws"].data_ptr(), sc["ws_elems"]
                 esz = DTYPES[dtype][1]
                 nb = esz * (M * cs_out + spec.cin * kp_d + M * cs_in * (1 + int(bool(op.pro_bn)) + int(bool(
                     st.residual)) + int(st.accumulate)))
@@ -428,6 +463,7 @@ class CouplingEngine:
                 c.g, c.x = sar.ptr(st.tmp), ar.ptr(op.x)
                 c.bn = self._bn(T, bn, training, ar.ptr("s:" + bn), M)
                 c.sums = sar.ptr("e:" + bn)
+                c.sum_shards = sc["shards"]
                 c.dx = sar.ptr(st.gx)
                 c.residual = sar.ptr(st.residual) if st.residual else None
                 c.accumulate = int(st.accumulate)

@@ -66,24 +66,30 @@ int rnvp_logit_inv(const float* x, float* y, float constraint, long long n, void
 int rnvp_prior_logprob(const float* z, const float* ldj, float* out, int B, int n_per_sample, void* stream);
 int rnvp_prior_logprob_bwd(const float* z, const float* gout, float* gz, int B, int n_per_sample, void* stream);
 
-/* ---- batch-norm statistic sources -------------------------------------- */
+/* ---- batch-norm statistic sources --------------------------------------
+ * Batch sums written by many workgroups are SHARDED to keep fp64 atomic
+ * contention bounded: layout [shards][2][C]; a reader adds the shards.
+ * rnvp_stat_shards(M) is the shard count the conv kernels use for an M-pixel
+ * output (callers size their sum buffers with it). */
 typedef struct rnvp_bn_src {
-    const double* sums;   /* [2*C] {sum, sum of squares} of the batch, or NULL */
+    const double* sums;   /* [shards][2*C] {sum, sum of squares} of the batch, or NULL */
     double count;         /* elements per channel behind sums */
     const float* mean;    /* running mean (used when sums == NULL) */
     const float* var;     /* running var */
     const float* gamma;   /* affine weight, NULL = 1 */
     const float* beta;    /* affine bias, NULL = 0 */
     float eps;
+    int shards;           /* >= 1 */
 } rnvp_bn_src;
+int rnvp_stat_shards(long long M);
 
 /* running-stat update of nn.BatchNorm2d in train mode, for n BN sites at once.
  * rm = (1-mom) rm + mom mean; rv = (1-mom) rv + mom var*count/(count-1); nbt += 1 */
 typedef struct rnvp_bn_running {
-    const double* sums; double count; int C; int pad;
+    const double* sums; double count; int C; int shards;
     float* rmean; float* rvar; long long* nbt;
 } rnvp_bn_running;
-int rnvp_bn_running_update(const rnvp_bn_running* descs_device, int n, float momentum, void* stream);
+int rnvp_bn_running_update(const rnvp_bn_running* descs_device, int n, int max_c, float momentum, void* stream);
 
 /* ---- s/t ResNet convolution (MFMA implicit GEMM) -----------------------
  * replaces WeightNormConv2d.forward (modules_realnvp.py:64-71) inside
@@ -95,12 +101,16 @@ int rnvp_bn_running_update(const rnvp_bn_running* descs_device, int n, float mom
  * applied AFTER act (as nn.Conv2d pads its input).  k = (ky*ks+kx)*cs_in + ci.
  * epi_relu_bn_bwd (used for the data gradient): the result g is multiplied
  * by [relu(bn(epi_x)) > 0] before being stored, and epi_sums accumulates
- * {sum g, sum g*xhat} per output channel. */
+ * {sum g, sum g*xhat} per output channel.  out_sums / epi_sums are sharded
+ * with rnvp_stat_shards(B*H*W) shards and must be zeroed by the caller.
+ * Small grids split K over workgroups when a workspace is given
+ * (ws: fp32, >= splits * M * n elements; the epilogue then runs in a second
+ * kernel that reduces the splits). */
 typedef struct rnvp_conv_args {
     int dtype;
     int B, H, W, ks;
     const void* x; int cs_in; int cin;
-    const void* w; int kp;              /* packed weights [n][kp], kp % 32 == 0 */
+    const void* w; int kp;              /* packed weights [n][kp], kp % 64 == 0 */
     void* y; int cs_out; int n;
     const float* bias;
     const void* residual;
@@ -108,6 +118,7 @@ typedef struct rnvp_conv_args {
     int pro_bn_relu; rnvp_bn_src pro;
     double* out_sums;
     int epi_relu_bn_bwd; const void* epi_x; rnvp_bn_src epi; double* epi_sums;
+    float* ws; long long ws_elems;      /* split-K workspace (optional) */
 } rnvp_conv_args;
 int rnvp_conv2d(const rnvp_conv_args* a, void* stream);
 
@@ -129,7 +140,8 @@ int rnvp_conv2d_wgrad(const rnvp_wgrad_args* a, void* stream);
  * also writes dgamma = sum_gxhat, dbeta = sum_g (when non-NULL) */
 typedef struct rnvp_bn_bwd_args {
     int dtype; long long M; int C; int cs;
-    const void* g; const void* x; rnvp_bn_src bn; const double* sums;
+    const void* g; const void* x; rnvp_bn_src bn;
+    const double* sums; int sum_shards;  /* the dgrad epilogue's epi_sums */
     void* dx; const void* residual; int accumulate;
     float* dgamma; float* dbeta;
 } rnvp_bn_bwd_args;

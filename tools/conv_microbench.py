@@ -1,0 +1,135 @@
+"""Microbenchmark of the MFMA conv kernels in isolation (GPU box).
+
+    python tools/conv_microbench.py [--quick]
+
+For each config: median time of repeated launches (HIP events on the launch
+stream), algorithmic bytes (x read once, w, y written, + residual/accumulate
+and the dgrad epilogue's x read) and FLOPs, achieved GB/s and TFLOP/s.
+"""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "dl-normalizing-flows_amd"))
+
+import torch  # noqa: E402
+
+from realnvp_hip import _lib  # noqa: E402
+from realnvp_hip._lib import BNSrc, ConvArgs, WgradArgs  # noqa: E402
+from realnvp_hip.engine import splitk_workspace, stat_shards  # noqa: E402
+from realnvp_hip.net import chan_stride, round_up  # noqa: E402
+
+
+def bench(fn, iters=20):
+    s = torch.cuda.current_stream()
+    for _ in range(3):
+        fn()
+    ts = []
+    for _ in range(iters):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        fn()
+        e1.record(s)
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    ts.sort()
+    return ts[len(ts) // 2] * 1e3   # us
+
+
+def conv_case(B, H, W, cin, cout, ks, pro=False, stats=False, residual=False, acc=False, dgrad_epi=False,
+              dtype="bf16", wgrad=False):
+    dev = "cuda"
+    tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+    esz = 2 if dtype == "bf16" else 4
+    M = B * H * W
+    csi, cso = chan_stride(cin), chan_stride(cout)
+    kp = round_up(ks * ks * csi, 64)
+    x = torch.randn(M, csi, device=dev).to(tdt)
+    w = (torch.randn(cout, kp, device=dev) * 0.05).to(tdt)
+    y = torch.zeros(M, cso, device=dev).to(tdt)
+    r = torch.randn(M, cso, device=dev).to(tdt)
+    sh = stat_shards(M)
+    sums_in = torch.rand(sh, 2, cin, device=dev, dtype=torch.float64) * M / sh
+    sums_in[:, 1] += 2 * M / sh
+    sums_out = torch.zeros(sh, 2, cout, device=dev, dtype=torch.float64)
+    gam = torch.ones(max(cin, cout), device=dev)
+    bet = torch.zeros(max(cin, cout), device=dev)
+    ws = splitk_workspace(dev, 8 * M * cout if M <= 16384 else 1)
+    L = _lib.lib()
+    s = torch.cuda.current_stream().cuda_stream
+    if wgrad:
+        dw = torch.zeros(cout, kp, device=dev)
+        a = WgradArgs()
+        a.dtype = 1 if dtype == "bf16" else 0
+        a.B, a.H, a.W, a.ks = B, H, W, ks
+        a.x, a.cs_in, a.cin = x.data_ptr(), csi, cin
+        if pro:
+            a.pro_bn_relu = 1
+            a.pro = BNSrc(sums_in.data_ptr(), float(M), None, None, gam.data_ptr(), bet.data_ptr(), 1e-5, sh)
+        a.dy, a.cs_dy, a.n = y.data_ptr(), cso, cout
+        a.dw, a.kp = dw.data_ptr(), kp
+        fn = lambda: L.conv2d_wgrad(C.byref(a), s)  # noqa: E731
+        nbytes = esz * M * (csi + cso) + 4 * cout * ks * ks * cin
+    else:
+        a = ConvArgs()
+        a.dtype = 1 if dtype == "bf16" else 0
+        a.B, a.H, a.W, a.ks = B, H, W, ks
+        a.x, a.cs_in, a.cin = x.data_ptr(), csi, cin
+        a.w, a.kp = w.data_ptr(), kp
+        a.y, a.cs_out, a.n = y.data_ptr(), cso, cout
+        a.residual = r.data_ptr() if residual else None
+        a.accumulate = int(acc)
+        if pro:
+            a.pro_bn_relu = 1
+            a.pro = BNSrc(sums_in.data_ptr(), float(M), None, None, gam.data_ptr(), bet.data_ptr(), 1e-5, sh)
+        if stats:
+            a.out_sums = sums_out.data_ptr()
+        if dgrad_epi:
+            a.epi_relu_bn_bwd = 1
+            a.epi_x = r.data_ptr()
+            a.epi = BNSrc(sums_in.data_ptr(), float(M), None, None, gam.data_ptr(), bet.data_ptr(), 1e-5, sh)
+            a.epi_sums = sums_out.data_ptr()
+        a.ws, a.ws_elems = ws.data_ptr(), ws.numel()
+        fn = lambda: L.conv2d(C.byref(a), s)  # noqa: E731
+        nbytes = esz * (M * csi + cout * kp + M * cso * (1 + int(residual) + int(acc) + int(dgrad_epi)))
+    us = bench(fn)
+    flops = 2.0 * M * cout * ks * ks * cin
+    return us, nbytes / us / 1e3, flops / us / 1e6
+
+
+def main():
+    torch.manual_seed(0)
+    cases = [
+        # name, B, H, W, cin, cout, ks, flags
+        ("s1 1x1 32->32 plain", 64, 64, 64, 32, 32, 1, {}),
+        ("s1 1x1 32->32 pro", 64, 64, 64, 32, 32, 1, dict(pro=True)),
+        ("s1 1x1 32->32 pro+stats", 64, 64, 64, 32, 32, 1, dict(pro=True, stats=True)),
+        ("s1 1x1 32->32 pro+stats+res", 64, 64, 64, 32, 32, 1, dict(pro=True, stats=True, residual=True)),
+        ("s1 1x1 32->32 skip acc", 64, 64, 64, 32, 32, 1, dict(acc=True)),
+        ("s1 3x3 32->32 pro+stats", 64, 64, 64, 32, 32, 3, dict(pro=True, stats=True)),
+        ("s1 3x3 32->32 dgrad", 64, 64, 64, 32, 32, 3, dict(dgrad_epi=True)),
+        ("s1 3x3 7->32 in", 64, 64, 64, 7, 32, 3, dict(stats=True)),
+        ("s1 1x1 32->6 out", 64, 64, 64, 32, 6, 1, dict(pro=True)),
+        ("s2 1x1 64->64 pro+stats", 64, 32, 32, 64, 64, 1, dict(pro=True, stats=True)),
+        ("s2 3x3 64->64 pro+stats", 64, 32, 32, 64, 64, 3, dict(pro=True, stats=True)),
+        ("s3 3x3 128->128 pro+stats", 64, 16, 16, 128, 128, 3, dict(pro=True, stats=True)),
+        ("s4 3x3 256->256 pro+stats", 64, 8, 8, 256, 256, 3, dict(pro=True, stats=True)),
+        ("s5 3x3 512->512 pro+stats", 64, 4, 4, 512, 512, 3, dict(pro=True, stats=True)),
+        ("s5 1x1 512->512 pro+stats", 64, 4, 4, 512, 512, 1, dict(pro=True, stats=True)),
+        ("wgrad s1 1x1 32", 64, 64, 64, 32, 32, 1, dict(pro=True, wgrad=True)),
+        ("wgrad s1 3x3 32", 64, 64, 64, 32, 32, 3, dict(pro=True, wgrad=True)),
+        ("wgrad s2 3x3 64", 64, 32, 32, 64, 64, 3, dict(pro=True, wgrad=True)),
+        ("wgrad s3 3x3 128", 64, 16, 16, 128, 128, 3, dict(pro=True, wgrad=True)),
+        ("wgrad s5 3x3 512", 64, 4, 4, 512, 512, 3, dict(pro=True, wgrad=True)),
+        ("wgrad s5 1x1 512", 64, 4, 4, 512, 512, 1, dict(pro=True, wgrad=True)),
+    ]
+    print("%-32s %9s %9s %9s" % ("case", "us", "GB/s", "TFLOP/s"))
+    for name, B, H, W, ci, co, ks, fl in cases:
+        us, gbs, tfs = conv_case(B, H, W, ci, co, ks, **fl)
+        print("%-32s %9.1f %9.1f %9.1f" % (name, us, gbs, tfs), flush=True)
+
+
+if __name__ == "__main__":
+    main()
