@@ -166,8 +166,9 @@ def main():
                                        validate_args=False)
     hp = utils.Hyperparameters(args.base_dim, args.res_blocks, True, True, True, True)
     model = flow_realnvp.RealNVP(3, args.size, prior, hp).to(dev)
-    tr = FlowTrainer(model, args.batch, dtype=args.dtype, seed=1000 + rank, process_group=pg)
-    tr.set_pixels(synthetic_pixels(args.batch, 3, args.size, seed=rank).to(dev))
+    from realnvp_hip.dist import max_over_ranks, mean_over_ranks, rank_seed
+    tr = FlowTrainer(model, args.batch, dtype=args.dtype, seed=rank_seed(1000, rank), process_group=pg)
+    tr.set_pixels(synthetic_pixels(args.batch, 3, args.size, seed=rank_seed(0, rank)).to(dev))
 
     if not args.no_graph:
         tr.capture(warmup=2)
@@ -190,13 +191,8 @@ def main():
     dt = time.perf_counter() - t0
     mean_ll = tr.mean_logll(args.steps)
     if pg is not None:
-        import torch.distributed as dist
-        t = torch.tensor([dt, mean_ll], dtype=torch.float64, device=dev)
-        mx = t.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        dt = float(mx[0])
-        mean_ll = float(t[1]) / world
+        dt = max_over_ranks(dt, dev, pg)
+        mean_ll = mean_over_ranks(mean_ll, dev, pg)
     bpd = tr.bits_per_dim(mean_ll)
     imgs = world * args.batch * args.steps
     value = imgs / dt

@@ -1,0 +1,53 @@
+"""Data parallelism for the RealNVP step: one process per GPU, sample sharding,
+one exchange (gradient average) per optimizer step.
+
+The path shards by sample: rank r trains on its own batch slice, BatchNorm
+statistics stay local (= the reference's batch-64 semantics per shard), and
+the flat gradient arena is averaged with all-reduce in fixed-size buckets
+(RCCL over xGMI on MI355X; gloo on CPU for tests).
+"""
+import torch
+import torch.distributed as dist
+
+
+def bucket_ranges(n, bucket_elems):
+    """[start, end) ranges covering [0, n) in buckets of bucket_elems."""
+    b = max(1, int(bucket_elems))
+    return [(i, min(n, i + b)) for i in range(0, n, b)]
+
+
+def allreduce_average(flat, group=None, bucket_elems=16 << 20):
+    """In-place average of a flat tensor across the group, bucket by bucket."""
+    world = dist.get_world_size(group)
+    if world == 1:
+        return flat
+    avg = getattr(dist.ReduceOp, "AVG", None)
+    use_avg = avg is not None and dist.get_backend(group) == "nccl"
+    for s, e in bucket_ranges(flat.numel(), bucket_elems):
+        if use_avg:
+            dist.all_reduce(flat[s:e], op=avg, group=group)
+        else:
+            dist.all_reduce(flat[s:e], op=dist.ReduceOp.SUM, group=group)
+            flat[s:e].div_(world)
+    return flat
+
+
+def max_over_ranks(value, device, group=None):
+    """max of a python float over ranks (the bench's timing rule)."""
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
+
+
+def mean_over_ranks(value, device, group=None):
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        t /= dist.get_world_size(group)
+    return float(t.item())
+
+
+def rank_seed(base, rank):
+    """Per-rank data seed: every rank draws a different batch (weak scaling)."""
+    return int(base) * 1000003 + int(rank)

@@ -205,9 +205,8 @@ class FlowTrainer:
     def _allreduce(self):
         if self.pg is None:
             return
-        import torch.distributed as dist
-        for i in range(0, self.n, self.bucket_elems):
-            dist.all_reduce(self.grad[i:i + self.bucket_elems], op=dist.ReduceOp.AVG, group=self.pg)
+        from .dist import allreduce_average
+        allreduce_average(self.grad, self.pg, self.bucket_elems)
 
     def _fwd_bwd(self):
         self.grad.zero_()
