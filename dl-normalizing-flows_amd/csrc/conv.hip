@@ -634,8 +634,17 @@ int dispatch_conv(const rnvp_conv_args* a, hipStream_t s) {
 // (64 bf16 / 32 f32) of dy (P) and act(x) (Q), staged row-major [m][col] in
 // double-buffered LDS; MFMA operands are columns, read transposed
 // (ds_read_b64_tr_b16 for bf16).
+struct WgView {
+    const void* x; const void* dy; rnvp_bn_src pro;
+    int H, W, ks, cs_in, cin, cs_dy, n, kp, pro_bn_relu;
+};
+
+// one [64 co] x [64 k] tile over pixels [mb, me): result to out[co*kp + k]
+// (fp32 atomics or plain stores) and, when bias_out, the bias sums of the
+// tile's co columns to bias_out[co] (atomic or plain).
 template <typename T>
-__global__ __launch_bounds__(256) void k_wgrad(rnvp_wgrad_args a, long long m_per_block) {
+__device__ __forceinline__ void wgrad_tile(const WgView& a, int co0, int k0, long long mb, long long me,
+                                           long long M, float* out, bool atomic, float* bias_out, bool bias_atomic) {
     constexpr int CH = Mf<T>::CH;
     constexpr int STG = (sizeof(T) == 2) ? 64 : 32;   // pixels per stage (two MFMA K-steps)
     constexpr int CPR = 64 / CH;                      // chunks per 64-column row
@@ -648,19 +657,14 @@ __global__ __launch_bounds__(256) void k_wgrad(rnvp_wgrad_args a, long long m_pe
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wc = wid >> 1, wk = wid & 1;
-    const long long M = (long long)a.B * a.H * a.W;
     const int N = a.n, cs = a.cs_in, ks = a.ks, pad = ks >> 1;
     const int K = ks * ks * cs;
-    const int co0 = blockIdx.x * 64, k0 = blockIdx.y * 64;
-    const long long mb = (long long)blockIdx.z * m_per_block;
-    const long long me = (mb + m_per_block < M) ? mb + m_per_block : M;
     const T* __restrict__ X = (const T*)a.x;
     const T* __restrict__ DY = (const T*)a.dy;
-    const bool do_bias = a.dbias && blockIdx.y == 0;
+    const bool do_bias = bias_out != nullptr;
     const bool pro = a.pro_bn_relu != 0;
 
     float* bnp = (float*)(dsm + 2 * cs);
-    if (pro) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + cs, nullptr, nullptr, dsm);
     if (tid < 64) dbs[tid] = 0.f;
     const int sc_ = tid % CPR;
     const int pk = k0 + sc_ * CH;                // Q column
@@ -718,11 +722,10 @@ __global__ __launch_bounds__(256) void k_wgrad(rnvp_wgrad_args a, long long m_pe
         }
     };
 
+    if (mb < me) gload(mb);          // first stage in flight while the BN table settles
+    if (pro) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + cs, nullptr, nullptr, dsm);
     __syncthreads();
-    if (mb < me) {
-        gload(mb);
-        lstore(0);
-    }
+    if (mb < me) lstore(0);
     __syncthreads();
     const int g = lane >> 4, li = lane & 15;
     int it = 0;
@@ -805,9 +808,26 @@ __global__ __launch_bounds__(256) void k_wgrad(rnvp_wgrad_args a, long long m_pe
             for (int r = 0; r < 4; ++r) {
                 const int co = co0 + wc * 32 + i * 16 + (lane >> 4) * 4 + r;
                 const int k = k0 + wk * 32 + j * 16 + (lane & 15);
-                if (co < N && k < K) atomicAdd(&a.dw[(long long)co * a.kp + k], acc[i][j][r]);
+                if (co < N && k < K) {
+                    float* o = out + (long long)co * a.kp + k;
+                    if (atomic) atomicAdd(o, acc[i][j][r]);
+                    else *o = acc[i][j][r];
+                }
             }
-    if (do_bias && tid < 64 && co0 + tid < N) atomicAdd(&a.dbias[co0 + tid], dbs[tid]);
+    if (do_bias && tid < 64 && co0 + tid < N) {
+        if (bias_atomic) atomicAdd(&bias_out[co0 + tid], dbs[tid]);
+        else bias_out[co0 + tid] = dbs[tid];
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_wgrad(rnvp_wgrad_args a, long long m_per_block) {
+    const long long M = (long long)a.B * a.H * a.W;
+    const long long mb = (long long)blockIdx.z * m_per_block;
+    const long long me = (mb + m_per_block < M) ? mb + m_per_block : M;
+    const WgView v{a.x, a.dy, a.pro, a.H, a.W, a.ks, a.cs_in, a.cin, a.cs_dy, a.n, a.kp, a.pro_bn_relu};
+    wgrad_tile<T>(v, blockIdx.x * 64, blockIdx.y * 64, mb, me, M, a.dw, true,
+                  (a.dbias && blockIdx.y == 0) ? a.dbias : nullptr, true);
 }
 
 template <typename T>
@@ -829,6 +849,30 @@ int launch_wgrad(const rnvp_wgrad_args* a, hipStream_t s) {
     k_wgrad<T><<<grid, 256, shm, s>>>(*a, mpb);
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
+}
+
+// grouped: block -> (conv, slab z, co tile, k tile).  Consecutive tasks (the
+// tiles of one slab, which re-read the same pixels through L2) are placed on
+// one XCD: dispatch hands block b to XCD b % 8, so task = bijective remap.
+template <typename T>
+__global__ __launch_bounds__(256) void k_wgrad_grouped(rnvp_wgrad_group g) {
+    const int nb = gridDim.x, b = blockIdx.x;
+    const int q = nb / 8, r = nb % 8, xcd = b % 8;
+    const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
+    int c = 0;
+    while (c + 1 < g.n_conv && g.conv[c + 1].task0 <= t) ++c;
+    const rnvp_wgrad_conv& cv = g.conv[c];
+    const int tco = (cv.n + 63) / 64;
+    const int local = t - cv.task0;
+    const int per = tco * cv.tk;
+    const int z = local / per, rr = local - z * per;
+    const int cot = rr / cv.tk, kt = rr - cot * cv.tk;
+    const long long M = (long long)g.B * g.H * g.W;
+    const long long mb = (long long)z * cv.m_per_slab;
+    const long long me = (mb + cv.m_per_slab < M) ? mb + cv.m_per_slab : M;
+    const WgView v{cv.x, cv.dy, cv.pro, g.H, g.W, cv.ks, cv.cs_in, cv.cin, cv.cs_dy, cv.n, cv.kp, cv.pro_bn_relu};
+    wgrad_tile<T>(v, cot * 64, kt * 64, mb, me, M, cv.ws + (long long)z * cv.n * cv.kp, false,
+                  (cv.wsb && kt == 0) ? cv.wsb + (long long)z * cv.n : nullptr, false);
 }
 
 // ---------------------------------------------------------------------------
@@ -941,35 +985,59 @@ __global__ void k_wn_fwd(const rnvp_wn_desc* __restrict__ descs, int n_desc) {
     }
 }
 
+// one block per output row co: dW row = sum of the nz partial slabs, gathered
+// into LDS in v's [ci][tap] order (coalesced over the packed k), then the
+// weight-norm backward and the bias partial sum.
+constexpr int WN_ROW_LDS = 4608;
+
 __global__ void k_wn_bwd(const rnvp_wn_desc* __restrict__ descs, int n_desc, float* gbase) {
     __shared__ double red[16];
+    __shared__ float rowbuf[WN_ROW_LDS];
     const int row = blockIdx.x;
     const rnvp_wn_desc d = descs[find_desc(descs, n_desc, row)];
     const int co = row - d.row0;
     const int kk = d.ks * d.ks, kr = d.cin * kk;
+    const int nz = d.nz > 0 ? d.nz : 1;
+    const long long zs = (long long)d.cout * d.kp_f;
     const float* v = d.v + (long long)co * kr;
     const float* dw = d.dw + (long long)co * d.kp_f;
-    double dot = 0;
-    for (int i = threadIdx.x; i < kr; i += blockDim.x) {
-        const int ci = i / kk, tap = i - ci * kk;
-        dot += (double)dw[tap * d.cs_in + ci] * v[i];
+    const bool in_lds = kr <= WN_ROW_LDS;
+    auto dw_at = [&](int k) {
+        float t = 0.f;
+        for (int z = 0; z < nz; ++z) t += dw[z * zs + k];
+        return t;
+    };
+    if (in_lds) {
+        const int K = kk * d.cs_in;
+        for (int k = threadIdx.x; k < K; k += blockDim.x) {
+            const int tap = k / d.cs_in, ci = k - tap * d.cs_in;
+            if (ci < d.cin) rowbuf[ci * kk + tap] = dw_at(k);
+        }
+        __syncthreads();
     }
+    auto dwv = [&](int i) {
+        if (in_lds) return rowbuf[i];
+        const int ci = i / kk, tap = i - ci * kk;
+        return dw_at(tap * d.cs_in + ci);
+    };
+    double dot = 0;
+    for (int i = threadIdx.x; i < kr; i += blockDim.x) dot += (double)dwv(i) * v[i];
     dot = block_sum(dot, red);
     float* dv = gbase + d.dv_off + (long long)co * kr;
     if (d.g) {
         const float nrm = d.norm[co];
         const float gs = d.g[co] / nrm;
         const float proj = (float)(dot / ((double)nrm * nrm));
-        for (int i = threadIdx.x; i < kr; i += blockDim.x) {
-            const int ci = i / kk, tap = i - ci * kk;
-            dv[i] = gs * (dw[tap * d.cs_in + ci] - proj * v[i]);
-        }
+        for (int i = threadIdx.x; i < kr; i += blockDim.x) dv[i] = gs * (dwv(i) - proj * v[i]);
         if (threadIdx.x == 0 && d.dg_off >= 0) gbase[d.dg_off + co] = (float)(dot / nrm);
     } else {
-        for (int i = threadIdx.x; i < kr; i += blockDim.x) {
-            const int ci = i / kk, tap = i - ci * kk;
-            dv[i] = dw[tap * d.cs_in + ci];
-        }
+        for (int i = threadIdx.x; i < kr; i += blockDim.x) dv[i] = dwv(i);
+    }
+    if (d.dbp) {
+        float bs = 0.f;
+        for (int z = threadIdx.x; z < nz; z += blockDim.x) bs += d.dbp[(long long)z * d.cout + co];
+        bs = block_sum(bs, (float*)red);
+        if (threadIdx.x == 0) gbase[d.db_off + co] = bs;
     }
 }
 
@@ -1002,6 +1070,49 @@ extern "C" int rnvp_conv2d_wgrad(const rnvp_wgrad_args* a, void* stream) {
     if (a->B == 0) return RNVP_OK;
     hipStream_t s = (hipStream_t)stream;
     return a->dtype == RNVP_F32 ? launch_wgrad<float>(a, s) : launch_wgrad<bf16_t>(a, s);
+}
+
+extern "C" int rnvp_wgrad_slabs(long long M) {
+    // ~2048 pixels per slab (32 stages of 64), at most 128 slabs
+    long long z = M / 2048;
+    if (z > 128) z = 128;
+    if (z < 1) z = 1;
+    return (int)z;
+}
+
+extern "C" int rnvp_conv2d_wgrad_grouped(const rnvp_wgrad_group* gin, void* stream) {
+    if (!gin || gin->n_conv <= 0 || gin->n_conv > RNVP_WGRAD_GROUP_MAX) return RNVP_E_INVALID;
+    if (gin->dtype != RNVP_F32 && gin->dtype != RNVP_BF16) return RNVP_E_INVALID;
+    if (gin->B < 0 || gin->H <= 0 || gin->W <= 0) return RNVP_E_INVALID;
+    if (gin->B == 0) return RNVP_OK;
+    rnvp_wgrad_group g = *gin;
+    const long long M = (long long)g.B * g.H * g.W;
+    const int STG = g.dtype == RNVP_BF16 ? 64 : 32;
+    long long tasks = 0;
+    int max_cs = 8;
+    for (int c = 0; c < g.n_conv; ++c) {
+        rnvp_wgrad_conv& v = g.conv[c];
+        if (!v.x || !v.dy || !v.ws) return RNVP_E_INVALID;
+        if (v.ks != 1 && v.ks != 3) return RNVP_E_UNSUPPORTED;
+        if (v.n <= 0 || v.cin <= 0 || v.nz <= 0) return RNVP_E_INVALID;
+        if ((v.cs_in & 7) || (v.cs_dy & 7) || v.cs_in < v.cin || v.cs_dy < v.n) return RNVP_E_INVALID;
+        if (v.kp < v.ks * v.ks * v.cs_in) return RNVP_E_INVALID;
+        if (!al16(v.x) || !al16(v.dy)) return RNVP_E_INVALID;
+        const long long steps = (M + STG - 1) / STG;
+        v.m_per_slab = ((steps + v.nz - 1) / v.nz) * STG;
+        if ((M + v.m_per_slab - 1) / v.m_per_slab > v.nz) return RNVP_E_INVALID;
+        v.tk = (v.ks * v.ks * v.cs_in + 63) / 64;
+        v.task0 = (int)tasks;
+        tasks += (long long)v.nz * ((v.n + 63) / 64) * v.tk;
+        if (v.cs_in > max_cs) max_cs = v.cs_in;
+    }
+    if (tasks <= 0 || tasks > (1ll << 30)) return RNVP_E_INVALID;
+    hipStream_t s = (hipStream_t)stream;
+    const size_t shm = 24 * (size_t)max_cs;
+    if (g.dtype == RNVP_F32) k_wgrad_grouped<float><<<(unsigned)tasks, 256, shm, s>>>(g);
+    else k_wgrad_grouped<bf16_t><<<(unsigned)tasks, 256, shm, s>>>(g);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
 }
 
 extern "C" int rnvp_bn_bwd_apply(const rnvp_bn_bwd_args* a, void* stream) {

@@ -59,7 +59,22 @@ class WNDesc(C.Structure):
     _fields_ = [("v", vp), ("g", vp), ("wf", vp), ("wd", vp), ("norm", vp),
                 ("dw", vp), ("dv_off", i64), ("dg_off", i64),
                 ("cout", i32), ("cin", i32), ("ks", i32), ("cs_in", i32), ("kp_f", i32),
-                ("cs_out", i32), ("kp_d", i32), ("row0", i32)]
+                ("cs_out", i32), ("kp_d", i32), ("row0", i32),
+                ("nz", i32), ("dbp", vp), ("db_off", i64)]
+
+
+WGRAD_GROUP_MAX = 24
+
+
+class WgradConv(C.Structure):
+    _fields_ = [("x", vp), ("dy", vp), ("ws", vp), ("wsb", vp), ("pro", BNSrc),
+                ("cs_in", i32), ("cin", i32), ("ks", i32), ("cs_dy", i32), ("n", i32), ("kp", i32),
+                ("pro_bn_relu", i32), ("nz", i32), ("m_per_slab", i64), ("task0", i32), ("tk", i32)]
+
+
+class WgradGroup(C.Structure):
+    _fields_ = [("dtype", i32), ("B", i32), ("H", i32), ("W", i32), ("n_conv", i32),
+                ("conv", WgradConv * WGRAD_GROUP_MAX)]
 
 
 class CouplingArgs(C.Structure):
@@ -102,6 +117,8 @@ _SIGS = {
     "rnvp_stat_shards": (i32, [i64]),
     "rnvp_conv2d": (i32, [C.POINTER(ConvArgs), vp]),
     "rnvp_conv2d_wgrad": (i32, [C.POINTER(WgradArgs), vp]),
+    "rnvp_wgrad_slabs": (i32, [i64]),
+    "rnvp_conv2d_wgrad_grouped": (i32, [C.POINTER(WgradGroup), vp]),
     "rnvp_bn_bwd_apply": (i32, [C.POINTER(BNBwdArgs), vp]),
     "rnvp_weight_norm_fwd": (i32, [vp, i32, i32, i32, vp]),
     "rnvp_weight_norm_bwd": (i32, [vp, i32, i32, vp, vp]),
@@ -128,7 +145,7 @@ class _Lib:
             fn = getattr(self.dll, name)
             fn.restype = res
             fn.argtypes = args
-            raw = name in ("rnvp_version", "rnvp_stat_shards") or res is not i32
+            raw = name in ("rnvp_version", "rnvp_stat_shards", "rnvp_wgrad_slabs") or res is not i32
             setattr(self, name[len("rnvp_"):], fn if raw else self._wrap(name, fn))
 
     def _wrap(self, name, fn):

@@ -18,7 +18,8 @@ from collections import OrderedDict
 import torch
 
 from . import _lib
-from ._lib import (BNBwdArgs, BNRunning, BNSrc, ConvArgs, CouplingArgs, WgradArgs, WNDesc, RNVP_BF16, RNVP_F32)
+from ._lib import (BNBwdArgs, BNRunning, BNSrc, ConvArgs, CouplingArgs, WgradConv, WgradGroup, WNDesc, RNVP_BF16,
+                   RNVP_F32, WGRAD_GROUP_MAX)
 from .net import backward_program, build_program, chan_stride, round_up
 
 BN_EPS = 1e-5
@@ -112,6 +113,20 @@ def splitk_elems(M, nmax):
     return 8 * M * nmax if M <= 16384 else 0
 
 
+_WGRAD_WS = {}
+
+
+def wgrad_workspace(device, elems):
+    """Per-device fp32 workspace for the grouped weight-gradient partial slabs
+    (one coupling's backward at a time, all on the caller's stream)."""
+    key = str(device)
+    t = _WGRAD_WS.get(key)
+    if t is None or t.numel() < elems:
+        t = torch.empty(max(elems, 1 << 16), dtype=torch.float32, device=device)
+        _WGRAD_WS[key] = t
+    return t
+
+
 class CouplingEngine:
     """Executor for one Checkerboard/Channelwise affine coupling module."""
 
@@ -184,6 +199,7 @@ class CouplingEngine:
             d.dg_off = self.layout[gn][0] if (gn and spec.scale) else -1
             d.cout, d.cin, d.ks, d.cs_in, d.kp_f, d.cs_out, d.kp_d, d.row0 = (
                 spec.cout, spec.cin, spec.ks, cs_in, kp_f, cs_out, kp_d, row0)
+            d.nz = 1
             row0 += spec.cout
             descs.append(d)
         table = (WNDesc * len(descs))(*descs)
@@ -237,17 +253,11 @@ class CouplingEngine:
         esz = DTYPES[dtype][1]
         M = B * H * W
         ar = Arena()
-        # zeroed every backward: dW images and the reductions (kept contiguous)
+        # zeroed every backward: the reductions (kept contiguous)
         wsz = self.weights(dtype)
-        first = last = None
-        for name, spec in self.P.convs.items():
-            kp_f = wsz["geo"][name][2]
-            ar.add("dw:" + name, spec.cout * kp_f * 4)
-            first = first or "dw:" + name
-            last = "dw:" + name
         ar.add("bwd_sums", 3 * self.Cb * 8)
         ar.add("in_bwd_sums", 2 * self.Cb * 8)
-        last = "in_bwd_sums"
+        first, last = "bwd_sums", "in_bwd_sums"
         sh = stat_shards(M)
         for bn, spec in self.P.bns.items():
             ar.add("e:" + bn, sh * 2 * spec.c * 8)
@@ -258,19 +268,41 @@ class CouplingEngine:
         cmax = max([chan_stride(s.cin) for s in self.P.convs.values()])
         ar.add("gtmp", M * cmax * esz)
         ar.alloc(device)
-        # weight-norm backward table (dw pointers into this scratch)
+        # grouped weight-gradient partial slabs: [nz][cout][kp_f] (+ bias [nz][cout])
+        nz = int(_lib.lib().wgrad_slabs(M))
+        wg = {}
+        off = 0
+        for name, spec in self.P.convs.items():
+            kp_f = wsz["geo"][name][2]
+            ow = off
+            off += nz * spec.cout * kp_f
+            ob = None
+            if spec.bias:
+                ob = off
+                off += nz * spec.cout
+            wg[name] = (ow, ob)
+            off = round_up(off, 64)
+        wgws = wgrad_workspace(device, off)
+        wbase = wgws.data_ptr()
+        # weight-norm backward table (sums the slabs, writes dv / dg / dbias)
         descs = []
         for d, (name, spec) in zip(wsz["descs"], self.P.convs.items()):
             e = WNDesc()
             C.memmove(C.addressof(e), C.addressof(d), C.sizeof(WNDesc))
-            e.dw = ar.ptr("dw:" + name)
+            ow, ob = wg[name]
+            e.dw = wbase + 4 * ow
+            e.nz = nz
+            _, _, bname = self._conv_names(spec)
+            e.dbp = wbase + 4 * ob if ob is not None else None
+            e.db_off = self.layout[bname][0] if ob is not None else 0
             descs.append(e)
         tab = (WNDesc * len(descs))(*descs)
         nmax = max(max(s.cin, s.cout) for s in self.P.convs.values())
         wse = splitk_elems(M, nmax)
         sc = dict(arena=ar, zero=zr, wn_table=torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(device),
                   wn_key=wsz["key"], wn_rows=wsz["rows"], n_wn=len(descs), shards=sh,
-                  ws=splitk_workspace(device, wse) if wse else None, ws_elems=wse)
+                  ws=splitk_workspace(device, wse) if wse else None, ws_elems=wse,
+                  wg=wg, wg_nz=nz, wg_ws=wgws)
         self._scratch[key] = sc
         return sc
 
@@ -394,7 +426,13 @@ class CouplingEngine:
     # --------------------------------------------------------------- backward
     def backward(self, sv, gz, gl_full, gl_sample, grad_block, gx=None):
         """Returns dL/dx; parameter gradients are written into grad_block
-        (flat fp32, zeroed by the caller; scale/bias grads accumulate)."""
+        (flat fp32, zeroed by the caller; scale/shift grads accumulate).
+
+        The data-gradient chain (dgrad -> BN apply per conv) runs first; the
+        weight gradients of all the net's convs only need their (complete,
+        never rewritten) output gradients and saved inputs, so they run as
+        ONE grouped launch afterwards (partial slabs, no atomics), followed by
+        the weight-norm backward that sums the slabs."""
         L = _lib.lib()
         x = sv["x"]
         B, H, W, dtype, training = sv["B"], sv["H"], sv["W"], sv["dtype"], sv["training"]
@@ -431,6 +469,10 @@ class CouplingEngine:
         a.g_scale, a.g_scale_shift = gp("scale"), gp("scale_shift")
         L.coupling_out_bwd(C.byref(a), s)
 
+        grp = WgradGroup()
+        grp.dtype, grp.B, grp.H, grp.W = dt, B, H, W
+        wg_bytes = wg_flops = 0.0
+        wbase = sc["wg_ws"].data_ptr()
         for st in self.steps:
             op = st.op
             spec = self.P.convs[op.conv]
@@ -472,19 +514,23 @@ class CouplingEngine:
                 nb = esz * M * cs_in * (3 + int(bool(st.residual)) + int(st.accumulate))
                 _launch("bn_bwd", nb, 0.0, L.bn_bwd_apply, C.byref(c), s)
             else:
-                c = WgradArgs()
-                c.dtype, c.B, c.H, c.W, c.ks = dt, B, H, W, spec.ks
-                c.x, c.cs_in, c.cin = ar.ptr(op.x), cs_in, spec.cin
+                if grp.n_conv >= WGRAD_GROUP_MAX:
+                    raise RuntimeError("grouped wgrad: more than %d convs" % WGRAD_GROUP_MAX)
+                c = grp.conv[grp.n_conv]
+                grp.n_conv += 1
+                ow, ob = sc["wg"][op.conv]
+                c.x, c.cs_in, c.cin, c.ks = ar.ptr(op.x), cs_in, spec.cin, spec.ks
                 if op.pro_bn:
                     c.pro_bn_relu = 1
                     c.pro = self._bn(T, op.pro_bn, training, ar.ptr("s:" + op.pro_bn), M)
                 c.dy, c.cs_dy, c.n = sar.ptr(st.gy), cs_out, spec.cout
-                c.dw, c.kp = sar.ptr("dw:" + op.conv), kp_f
-                c.dbias = gp(bname) if bname else None
+                c.ws, c.kp, c.nz = wbase + 4 * ow, kp_f, sc["wg_nz"]
+                c.wsb = wbase + 4 * ob if ob is not None else None
                 esz = DTYPES[dtype][1]
-                nb = esz * (M * cs_in + M * cs_out) + 4 * spec.cout * spec.ks * spec.ks * spec.cin
-                _launch("conv_wgrad", nb, 2.0 * M * spec.cout * spec.ks * spec.ks * spec.cin, L.conv2d_wgrad,
-                        C.byref(c), s)
+                wg_bytes += esz * (M * cs_in + M * cs_out) + 4 * sc["wg_nz"] * spec.cout * kp_f
+                wg_flops += 2.0 * M * spec.cout * spec.ks * spec.ks * spec.cin
+        if grp.n_conv:
+            _launch("conv_wgrad", wg_bytes, wg_flops, L.conv2d_wgrad_grouped, C.byref(grp), s)
         L.weight_norm_bwd(sc["wn_table"].data_ptr(), sc["n_wn"], sc["wn_rows"], gbase, s)
         a.gh0, a.cs_gh0 = sar.ptr("g:h0"), chan_stride(self.P.buf_ch["h0"])
         a.in_bwd_sums = sar.ptr("in_bwd_sums")

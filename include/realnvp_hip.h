@@ -135,6 +135,33 @@ typedef struct rnvp_wgrad_args {
 } rnvp_wgrad_args;
 int rnvp_conv2d_wgrad(const rnvp_wgrad_args* a, void* stream);
 
+/* grouped weight gradient: the wgrads of every conv of one coupling's s/t
+ * network in ONE launch (they are independent of each other once the
+ * coupling's data-gradient chain has run).  Conv c's pixel range is cut into
+ * nz slabs; a workgroup owns one [64 n] x [64 k] tile of one slab and stores
+ * its fp32 partial to ws[z][n][kp] (plain stores, no atomics, deterministic);
+ * the bias partial of k tile 0 goes to wsb[z][n].  The weight-norm backward
+ * (rnvp_weight_norm_bwd with nz slabs) sums the partials.  The library fills
+ * m_per_slab / task0 / tk.  Replaces the per-conv backward of
+ * WeightNormConv2d (modules_realnvp.py:53-59) for the whole ResidualModule. */
+#define RNVP_WGRAD_GROUP_MAX 24
+typedef struct rnvp_wgrad_conv {
+    const void* x; const void* dy;
+    float* ws;                          /* [nz][n][kp] fp32 partials */
+    float* wsb;                         /* [nz][n] bias partials or NULL */
+    rnvp_bn_src pro;
+    int cs_in, cin, ks, cs_dy, n, kp, pro_bn_relu, nz;
+    long long m_per_slab;               /* filled by the library */
+    int task0, tk;                      /* filled by the library */
+} rnvp_wgrad_conv;
+typedef struct rnvp_wgrad_group {
+    int dtype, B, H, W, n_conv;
+    rnvp_wgrad_conv conv[RNVP_WGRAD_GROUP_MAX];
+} rnvp_wgrad_group;
+/* slab count the grouped wgrad uses for a conv over M pixels (size ws with it) */
+int rnvp_wgrad_slabs(long long M);
+int rnvp_conv2d_wgrad_grouped(const rnvp_wgrad_group* g, void* stream);
+
 /* batch-norm backward apply (train mode), the second half of BN backward:
  * dx = gamma*rstd*(g - sum_g/M - xhat * sum_gxhat/M) (+ residual) (+= dx if accumulate)
  * also writes dgamma = sum_gxhat, dbeta = sum_g (when non-NULL) */
@@ -151,15 +178,19 @@ int rnvp_bn_bwd_apply(const rnvp_bn_bwd_args* a, void* stream);
  * w = g * v / ||v||, packed into the forward layout wf[co][(ky*ks+kx)*cs_in+ci]
  * and the flipped, transposed data-gradient layout wd[ci][(ky'*ks+kx')*cs_out+co]
  * (w[co][ci][ks-1-ky'][ks-1-kx']).  g == NULL means a plain conv (w = v).
- * bwd: dv = (g/|v|)(dw - (v.dw/|v|^2) v), dg = v.dw/|v| from the packed dw,
- * written at grad_base + dv_off / dg_off (elements; dg_off < 0 = frozen g). */
+ * bwd: dv = (g/|v|)(dw - (v.dw/|v|^2) v), dg = v.dw/|v| from the packed dw
+ * (sum of nz slabs), written at grad_base + dv_off / dg_off (elements;
+ * dg_off < 0 = frozen g); dbias = sum of the nz bias partials at db_off. */
 typedef struct rnvp_wn_desc {
     const float* v; const float* g;
     void* wf; void* wd; float* norm;
-    const float* dw;                   /* packed [cout][kp_f] fp32 (bwd) */
+    const float* dw;                   /* packed [nz][cout][kp_f] fp32 (bwd), summed over nz */
     long long dv_off; long long dg_off;
     int cout, cin, ks, cs_in, kp_f, cs_out, kp_d;
     int row0;                          /* first global row (prefix sum of cout) */
+    int nz;                            /* dw partial slabs (>= 1) */
+    const float* dbp;                  /* bias partials [nz][cout] or NULL */
+    long long db_off;                  /* bias gradient offset (elements) */
 } rnvp_wn_desc;
 int rnvp_weight_norm_fwd(const rnvp_wn_desc* descs_device, int n_desc, int total_rows, int dtype, void* stream);
 int rnvp_weight_norm_bwd(const rnvp_wn_desc* descs_device, int n_desc, int total_rows, float* grad_base, void* stream);
