@@ -55,6 +55,24 @@ __device__ __forceinline__ u32x4 pack(const float* v, bf16_t) {
     return c;
 }
 
+// 4 consecutive elements (8 B of bf16 / 16 B of f32) <-> float[4]
+__device__ __forceinline__ void ld4(const float* p, float* v) {
+    const floatx4 t = *(const floatx4*)p;
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+}
+__device__ __forceinline__ void ld4(const bf16_t* p, float* v) {
+    const uint2 t = *(const uint2*)p;
+    v[0] = __uint_as_float(t.x << 16); v[1] = __uint_as_float(t.x & 0xffff0000u);
+    v[2] = __uint_as_float(t.y << 16); v[3] = __uint_as_float(t.y & 0xffff0000u);
+}
+__device__ __forceinline__ void st4(float* p, const float* v) { *(floatx4*)p = floatx4{v[0], v[1], v[2], v[3]}; }
+__device__ __forceinline__ void st4(bf16_t* p, const float* v) {
+    uint2 t;
+    t.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+    t.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    *(uint2*)p = t;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -59,23 +59,47 @@ __device__ __forceinline__ double* shard_ptr(double* sums, int shards, int N) {
     return sums ? sums + (long long)(blockIdx.x % shards) * 2 * N : nullptr;
 }
 
-// per-element epilogue shared by the direct and the split-K path
+// 4-channel epilogue in the transposed layout: y = acc + bias (+ residual)
+// (+ y), or the dgrad ReLU/BN-backward form; BN statistics into s1/s2.
+// et: LDS epilogue table at channel n0 (scale | shift | mean | rstd, pitch).
 template <typename T>
-__device__ __forceinline__ float epi_value(const rnvp_conv_args& a, long long o, float acc, float bias, float e_sc,
-                                           float e_sf, float e_mean, float e_rstd, float& s1, float& s2) {
-    float v = acc + bias;
-    if (a.residual) v += ldv((const T*)a.residual + o);
-    if (a.accumulate) v += ldv((const T*)a.y + o);
-    if (a.epi_relu_bn_bwd) {
-        const float xv = ldv((const T*)a.epi_x + o);
-        if (xv * e_sc + e_sf <= 0.f) v = 0.f;
-        s1 += v;
-        s2 += v * (xv - e_mean) * e_rstd;
-    } else {
-        s1 += v;
-        s2 += v * v;
+__device__ __forceinline__ void epi4(const rnvp_conv_args& a, long long o, const floatx4& acc, const float* bias,
+                                     bool epi_bn, const float* et, int pitch, float* s1, float* s2, int nvalid) {
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = acc[r] + bias[r];
+    if (a.residual) {
+        float t[4];
+        ld4((const T*)a.residual + o, t);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += t[r];
     }
-    return v;
+    if (a.accumulate) {
+        float t[4];
+        ld4((const T*)a.y + o, t);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += t[r];
+    }
+    if (epi_bn) {
+        float xv[4];
+        ld4((const T*)a.epi_x + o, xv);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            if (xv[r] * et[r] + et[pitch + r] <= 0.f) v[r] = 0.f;
+            s1[r] += v[r];
+            s2[r] += v[r] * (xv[r] - et[2 * pitch + r]) * et[3 * pitch + r];
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            s1[r] += v[r];
+            s2[r] += v[r] * v[r];
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        if (r >= nvalid) v[r] = 0.f;
+    st4((T*)a.y + o, v);
 }
 
 // ---------------------------------------------------------------------------
@@ -112,8 +136,7 @@ __global__ __launch_bounds__(256) void k_conv(rnvp_conv_args a, int kt_per_split
     double* tmp = dsm;
     float* bnp = (float*)(dsm + 2 * max(cs, BN));   // prologue scale [cs] | shift [cs]
     float* etab = bnp + 2 * cs;                      // epilogue scale | shift | mean | rstd [BN each]
-    if (pro) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + cs, nullptr, nullptr, tmp);
-    if (epi_bn) block_bn_table(a.epi, N, n0, BN, etab, etab + BN, etab + 2 * BN, etab + 3 * BN, tmp);
+    float* btab = etab + 4 * BN;                     // bias [BN]
 
     // per-thread A rows (fixed over K) and chunk column
     const int cA = tid & 7;
@@ -193,11 +216,14 @@ __global__ __launch_bounds__(256) void k_conv(rnvp_conv_args a, int kt_per_split
         }
     };
 
-    __syncthreads();   // bnp ready
-    if (kt0 < kt1) {
-        gload(kt0);
-        lstore(0);
-    }
+    // the first stage's loads are in flight while the BN tables are built
+    if (kt0 < kt1) gload(kt0);
+    if (pro) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + cs, nullptr, nullptr, tmp);
+    if (epi_bn) block_bn_table(a.epi, N, n0, BN, etab, etab + BN, etab + 2 * BN, etab + 3 * BN, tmp);
+    if (!PARTIAL)
+        for (int c = tid; c < BN; c += 256) btab[c] = (a.bias && n0 + c < N) ? a.bias[n0 + c] : 0.f;
+    __syncthreads();   // bnp / etab / btab ready
+    if (kt0 < kt1) lstore(0);
     __syncthreads();
     const int g = lane >> 4, li = lane & 15;
     for (int kt = kt0; kt < kt1; ++kt) {
@@ -211,10 +237,11 @@ __global__ __launch_bounds__(256) void k_conv(rnvp_conv_args a, int kt_per_split
             for (int i = 0; i < TM; ++i) af[i] = As[cur][sw8(wm * WTM + i * 16 + li, s * 4 + g)];
 #pragma unroll
             for (int j = 0; j < TN; ++j) bfr[j] = Bs[cur][sw8(wn * WTN + j * 16 + li, s * 4 + g)];
+            // transposed product: acc[i][j] = D[n][m], a lane owns 4 channels of one pixel
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
-                for (int j = 0; j < TN; ++j) Mf<T>::step(af[i], bfr[j], acc[i][j]);
+                for (int j = 0; j < TN; ++j) Mf<T>::step(bfr[j], af[i], acc[i][j]);
         }
         if (more) lstore(cur ^ 1);
         __syncthreads();
@@ -222,74 +249,56 @@ __global__ __launch_bounds__(256) void k_conv(rnvp_conv_args a, int kt_per_split
 
     const int cso = a.cs_out;
     if constexpr (PARTIAL) {
-        float* ws = a.ws + (long long)blockIdx.z * M * N;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const long long m = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
-                if (m >= M) continue;
-#pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    const int n = n0 + wn * WTN + j * 16 + (lane & 15);
-                    if (n < N) ws[m * N + n] = acc[i][j][r];
-                }
-            }
-        return;
-    } else {
-        // ---- fused epilogue ----
-        T* __restrict__ Y = (T*)a.y;
-        const bool want_sums = a.out_sums || (a.epi_relu_bn_bwd && a.epi_sums);
-        float s1[TN], s2[TN];
-        float e_sc[TN], e_sf[TN], e_mean[TN], e_rstd[TN], bias[TN];
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int col = wn * WTN + j * 16 + (lane & 15);
-            const int n = n0 + col;
-            s1[j] = 0.f;
-            s2[j] = 0.f;
-            bias[j] = (a.bias && n < N) ? a.bias[n] : 0.f;
-            e_sc[j] = e_sf[j] = e_mean[j] = 0.f;
-            e_rstd[j] = 1.f;
-            if (epi_bn) {
-                e_sc[j] = etab[col];
-                e_sf[j] = etab[BN + col];
-                e_mean[j] = etab[2 * BN + col];
-                e_rstd[j] = etab[3 * BN + col];
-            }
-        }
+        float* ws = a.ws + (long long)blockIdx.z * M * cso;
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
+            const long long m = m0 + wm * WTM + i * 16 + li;
+            if (m >= M) continue;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const long long m = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
-                if (m >= M) continue;
+            for (int j = 0; j < TN; ++j) {
+                const int n = n0 + wn * WTN + j * 16 + 4 * g;
+                if (n < cso) *(floatx4*)(ws + m * cso + n) = acc[i][j];
+            }
+        }
+        return;
+    } else {
+        // ---- fused epilogue (4 channels of one pixel per lane) ----
+        const bool want_sums = a.out_sums || (a.epi_relu_bn_bwd && a.epi_sums);
+        float s1[TN][4], s2[TN][4];
 #pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    const int n = n0 + wn * WTN + j * 16 + (lane & 15);
-                    if (n >= cso) continue;
-                    const long long o = m * cso + n;
-                    float v = 0.f;
-                    if (n < N) v = epi_value<T>(a, o, acc[i][j][r], bias[j], e_sc[j], e_sf[j], e_mean[j], e_rstd[j],
-                                                s1[j], s2[j]);
-                    stv(&Y[o], v);
-                }
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const long long m = m0 + wm * WTM + i * 16 + li;
+            if (m >= M) continue;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int col = wn * WTN + j * 16 + 4 * g;
+                const int n = n0 + col;
+                if (n >= cso) continue;
+                epi4<T>(a, m * cso + n, acc[i][j], btab + col, epi_bn, etab + col, BN, s1[j], s2[j], N - n);
             }
         }
         if (want_sums) {
             double* sums = shard_ptr(a.epi_relu_bn_bwd ? a.epi_sums : a.out_sums, shards, N);
 #pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                s1[j] += __shfl_xor(s1[j], 16, 64);
-                s1[j] += __shfl_xor(s1[j], 32, 64);
-                s2[j] += __shfl_xor(s2[j], 16, 64);
-                s2[j] += __shfl_xor(s2[j], 32, 64);
-                if (lane < 16) {
-                    const int col = wn * WTN + j * 16 + lane;
-                    red[(wm * BN + col) * 2] = s1[j];
-                    red[(wm * BN + col) * 2 + 1] = s2[j];
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float u1 = s1[j][r], u2 = s2[j][r];
+#pragma unroll
+                    for (int o = 1; o < 16; o <<= 1) {
+                        u1 += __shfl_xor(u1, o, 64);
+                        u2 += __shfl_xor(u2, o, 64);
+                    }
+                    if (li == 0) {
+                        const int col = wn * WTN + j * 16 + 4 * g + r;
+                        red[(wm * BN + col) * 2] = u1;
+                        red[(wm * BN + col) * 2 + 1] = u2;
+                    }
                 }
-            }
             __syncthreads();
             for (int col = tid; col < BN; col += 256) {
                 const int n = n0 + col;
@@ -307,63 +316,55 @@ __global__ __launch_bounds__(256) void k_conv(rnvp_conv_args a, int kt_per_split
     }
 }
 
-// split-K reduction + epilogue: block = [16 rows][64 cols], thread = (col, 4
-// rows); the <= 8 x 4 partial loads of a thread are independent.
+// split-K reduction + epilogue: block = [16 pixels][64 channels], thread =
+// 4 channels of one pixel; partials ws[z][m][cs_out] (fp32).
 constexpr int MAX_SPLITS = 8;
 
 template <typename T>
 __global__ __launch_bounds__(256) void k_splitk_epi(rnvp_conv_args a, int splits, int shards) {
-    __shared__ float red[4][64][2];
+    __shared__ float red[16][64][2];
     __shared__ double tmp[128];
     __shared__ float etab[4 * 64];
-    const int tid = threadIdx.x, col = tid & 63, rg = tid >> 6;
+    __shared__ float btab[64];
+    const int tid = threadIdx.x, c4 = tid & 15, row = tid >> 4;
     const long long M = (long long)a.B * a.H * a.W;
     const int N = a.n, cso = a.cs_out;
     const int n0 = blockIdx.y * 64;
-    const long long m0 = (long long)blockIdx.x * 16 + rg * 4;
-    const int n = n0 + col;
-    if (a.epi_relu_bn_bwd) block_bn_table(a.epi, N, n0, 64, etab, etab + 64, etab + 128, etab + 192, tmp);
-    float bias = 0.f, e_sc = 0.f, e_sf = 0.f, e_mean = 0.f, e_rstd = 1.f;
-    if (n < N) {
-        if (a.bias) bias = a.bias[n];
-        if (a.epi_relu_bn_bwd) {
-            e_sc = etab[col]; e_sf = etab[64 + col]; e_mean = etab[128 + col]; e_rstd = etab[192 + col];
-        }
-    }
-    float accv[4] = {0.f, 0.f, 0.f, 0.f};
-    if (n < N) {
+    const long long m = (long long)blockIdx.x * 16 + row;
+    const int col = 4 * c4, n = n0 + col;
+    const bool epi_bn = a.epi_relu_bn_bwd != 0;
+    // partial loads first (independent of the tables)
+    floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+    const bool live = m < M && n < cso;
+    if (live) {
+        const float* wz = a.ws + m * cso + n;
 #pragma unroll
-        for (int z = 0; z < MAX_SPLITS; ++z) {
-            if (z < splits) {
-                const float* wz = a.ws + (long long)z * M * N;
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    if (m0 + r < M) accv[r] += wz[(m0 + r) * N + n];
-            }
-        }
+        for (int z = 0; z < MAX_SPLITS; ++z)
+            if (z < splits) acc += *(const floatx4*)(wz + (long long)z * M * cso);
     }
-    float s1 = 0.f, s2 = 0.f;
-    T* Y = (T*)a.y;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const long long m = m0 + r;
-        if (m >= M || n >= cso) continue;
-        const long long o = m * cso + n;
-        float v = 0.f;
-        if (n < N) v = epi_value<T>(a, o, accv[r], bias, e_sc, e_sf, e_mean, e_rstd, s1, s2);
-        stv(&Y[o], v);
-    }
-    const bool want_sums = a.out_sums || (a.epi_relu_bn_bwd && a.epi_sums);
+    if (epi_bn) block_bn_table(a.epi, N, n0, 64, etab, etab + 64, etab + 128, etab + 192, tmp);
+    if (tid < 64) btab[tid] = (a.bias && n0 + tid < N) ? a.bias[n0 + tid] : 0.f;
+    __syncthreads();
+    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+    if (live) epi4<T>(a, m * cso + n, acc, btab + col, epi_bn, etab + col, 64, s1, s2, N - n);
+    const bool want_sums = a.out_sums || (epi_bn && a.epi_sums);
     if (want_sums) {
-        red[rg][col][0] = s1;
-        red[rg][col][1] = s2;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            red[row][col + r][0] = s1[r];
+            red[row][col + r][1] = s2[r];
+        }
         __syncthreads();
-        if (rg == 0 && n < N) {
-            double* sums = shard_ptr(a.epi_relu_bn_bwd ? a.epi_sums : a.out_sums, shards, N);
-            float t1 = red[0][col][0] + red[1][col][0] + red[2][col][0] + red[3][col][0];
-            float t2 = red[0][col][1] + red[1][col][1] + red[2][col][1] + red[3][col][1];
-            atomicAdd(&sums[n], (double)t1);
-            atomicAdd(&sums[N + n], (double)t2);
+        if (tid < 64 && n0 + tid < N) {
+            float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                t1 += red[r][tid][0];
+                t2 += red[r][tid][1];
+            }
+            double* sums = shard_ptr(epi_bn ? a.epi_sums : a.out_sums, shards, N);
+            atomicAdd(&sums[n0 + tid], (double)t1);
+            atomicAdd(&sums[N + n0 + tid], (double)t2);
         }
     }
 }
@@ -372,11 +373,16 @@ __global__ __launch_bounds__(256) void k_splitk_epi(rnvp_conv_args a, int splits
 // register-streaming conv for small channel counts (scales 1-2)
 // ---------------------------------------------------------------------------
 // For K <= ~600 and N <= 64 the whole packed weight matrix fits in LDS, and an
-// MFMA A-fragment row (lane&15) x k-group (lane>>4) is exactly one pixel's
-// 16-byte channel chunk: waves stream A fragments from global/L2 straight into
-// registers (BN+ReLU applied there), no LDS round trip and no barrier in the
-// main loop.  Each wave owns 64-pixel tiles (4 MFMA row tiles) and the next
-// k-step's fragments are loaded before the current MFMAs.
+// MFMA B-fragment column (lane&15) x k-group (lane>>4) is exactly one pixel's
+// 16-byte channel chunk: waves stream pixel fragments from global/L2 straight
+// into registers (BN+ReLU applied there), no LDS round trip and no barrier in
+// the main loop.  The product is formed transposed, D[n][m] = W[n][k] X[m][k]^T,
+// so a lane ends up owning 4 consecutive output channels of one pixel: the
+// epilogue reads/writes 8-byte (bf16) / 16-byte (f32) vectors.  Each wave owns
+// 64-pixel tiles (4 MFMA column tiles); the next k-step's (or the next tile's)
+// fragments are loaded before the current MFMAs, and the first tile's loads
+// are issued before the BN-table / weight prologue.
+
 template <typename T, int NT>
 __global__ __launch_bounds__(256) void k_conv_stream(rnvp_conv_args a, int shards) {
     constexpr int CH = Mf<T>::CH;
@@ -388,20 +394,60 @@ __global__ __launch_bounds__(256) void k_conv_stream(rnvp_conv_args a, int shard
     const int N = a.n, cs = a.cs_in, ks = a.ks, pad = ks >> 1;
     const int K = ks * ks * cs;
     const int nsteps = (K + KS - 1) / KS;
-    const int kpl = nsteps * KS + CH;      // LDS row pitch (+16 B: conflict-free column reads)
+    const int kpl = nsteps * KS + CH;      // LDS row pitch (+16 B: conflict-free row reads)
     const bool pro = a.pro_bn_relu != 0;
     const bool epi_bn = a.epi_relu_bn_bwd != 0;
     const int ntmp = cs > NC ? cs : NC;
 
     double* tmp = dsm;
     float* bnp = (float*)(dsm + 2 * ntmp);
-    float* etab = bnp + 2 * cs;
-    float* red = etab + 4 * NC;            // [4 waves][NC][2]
+    float* etab = bnp + 2 * cs;            // scale | shift | mean | rstd [NC each]
+    float* btab = etab + 4 * NC;           // bias [NC]
+    float* red = btab + NC;                // [4 waves][NC][2]
     T* Wl = (T*)(red + 4 * NC * 2);
+
+    // pixel decode of this wave's tile (4 column tiles of 16 pixels); M < 2^31
+    const int ntiles = (int)((M + 63) / 64);
+    const int tstride = gridDim.x * 4;
+    int mrow[4], yr[4], xr[4];
+    auto decode = [&](int t) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int m = t * 64 + i * 16 + li;
+            mrow[i] = (t < ntiles && m < M) ? m : -1;
+            const int mm = mrow[i] >= 0 ? m : 0;
+            xr[i] = mm % a.W;
+            yr[i] = (mm / a.W) % a.H;
+        }
+    };
+    const T* __restrict__ X = (const T*)a.x;
+    u32x4 ra[4];
+    unsigned msk = 0;
+    int cur_ci = 0;
+    auto load = [&](int s) {
+        const int k = s * KS + g * CH;
+        const int tap = k / cs, ci = k - tap * cs;
+        const int dy = tap / ks - pad, dx = tap % ks - pad;
+        cur_ci = ci;
+        msk = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            ra[i] = u32x4{0u, 0u, 0u, 0u};
+            const int yy = yr[i] + dy, xx = xr[i] + dx;
+            if (mrow[i] >= 0 && k < K && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) {
+                ra[i] = *(const u32x4*)(X + (long long)(mrow[i] + dy * a.W + dx) * cs + ci);
+                msk |= 1u << i;
+            }
+        }
+    };
+    // first tile's fragments in flight while the prologue runs
+    int t = blockIdx.x * 4 + wid;
+    decode(t);
+    load(0);
 
     if (pro) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + cs, nullptr, nullptr, tmp);
     if (epi_bn) block_bn_table(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp);
-    // weights -> LDS (rows >= N and k >= K zero)
+    // weights -> LDS (rows >= N and k >= K zero), bias -> LDS
     {
         const T* Wg = (const T*)a.w;
         const int cpr = kpl / CH;
@@ -411,70 +457,31 @@ __global__ __launch_bounds__(256) void k_conv_stream(rnvp_conv_args a, int shard
             if (r < N && c * CH < nsteps * KS) v = *(const u32x4*)(Wg + (long long)r * a.kp + c * CH);
             *(u32x4*)(Wl + r * kpl + c * CH) = v;
         }
+        for (int n = tid; n < NC; n += 256) btab[n] = (a.bias && n < N) ? a.bias[n] : 0.f;
     }
     __syncthreads();
 
-    const T* __restrict__ X = (const T*)a.x;
-    T* __restrict__ Y = (T*)a.y;
     const int cso = a.cs_out;
-    float bias[NT], e_sc[NT], e_sf[NT], e_mean[NT], e_rstd[NT], s1[NT], s2[NT];
+    float s1[NT][4], s2[NT][4];
 #pragma unroll
-    for (int j = 0; j < NT; ++j) {
-        const int n = j * 16 + li;
-        bias[j] = (a.bias && n < N) ? a.bias[n] : 0.f;
-        e_sc[j] = epi_bn ? etab[n] : 0.f;
-        e_sf[j] = epi_bn ? etab[NC + n] : 0.f;
-        e_mean[j] = epi_bn ? etab[2 * NC + n] : 0.f;
-        e_rstd[j] = epi_bn ? etab[3 * NC + n] : 1.f;
-        s1[j] = 0.f;
-        s2[j] = 0.f;
-    }
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.f;
 
-    const long long ntiles = (M + 63) / 64;
-    for (long long t = (long long)blockIdx.x * 4 + wid; t < ntiles; t += (long long)gridDim.x * 4) {
-        long long mrow[4];
-        int yr[4], xr[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const long long m = t * 64 + i * 16 + li;
-            mrow[i] = m < M ? m : -1;
-            const long long mm = m < M ? m : 0;
-            xr[i] = (int)(mm % a.W);
-            yr[i] = (int)((mm / a.W) % a.H);
-        }
+    for (; t < ntiles; t += tstride) {
         floatx4 acc[4][NT];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < NT; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-        u32x4 ra[4];
-        unsigned msk = 0;
-        int cur_ci = 0;
-        auto load = [&](int s) {
-            const int k = s * KS + g * CH;
-            const int tap = k / cs, ci = k - tap * cs;
-            const int dy = tap / ks - pad, dx = tap % ks - pad;
-            cur_ci = ci;
-            msk = 0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                ra[i] = u32x4{0u, 0u, 0u, 0u};
-                const int yy = yr[i] + dy, xx = xr[i] + dx;
-                if (mrow[i] >= 0 && k < K && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) {
-                    ra[i] = *(const u32x4*)(X + (mrow[i] + (long long)dy * a.W + dx) * cs + ci);
-                    msk |= 1u << i;
-                }
-            }
-        };
-        load(0);
         for (int s = 0; s < nsteps; ++s) {
             u32x4 av[4];
             const int ci = cur_ci;
             const unsigned mk = msk;
 #pragma unroll
             for (int i = 0; i < 4; ++i) av[i] = ra[i];
-            if (s + 1 < nsteps) load(s + 1);
+            if (s + 1 < nsteps) load(s + 1);   // next k-step in flight under these MFMAs
             if (pro) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
@@ -487,46 +494,48 @@ __global__ __launch_bounds__(256) void k_conv_stream(rnvp_conv_args a, int shard
                     }
                 }
             }
-            u32x4 bv[NT];
+            u32x4 wv[NT];
 #pragma unroll
-            for (int j = 0; j < NT; ++j) bv[j] = *(const u32x4*)(Wl + (j * 16 + li) * kpl + s * KS + g * CH);
+            for (int j = 0; j < NT; ++j) wv[j] = *(const u32x4*)(Wl + (j * 16 + li) * kpl + s * KS + g * CH);
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int j = 0; j < NT; ++j) Mf<T>::step(av[i], bv[j], acc[i][j]);
+                for (int j = 0; j < NT; ++j) Mf<T>::step(wv[j], av[i], acc[i][j]);
         }
-        // epilogue for this tile
+        // epilogue: lane owns channels j*16 + 4g .. +3 of pixel t*64 + i*16 + li
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i) {
+            const long long m = mrow[i];
+            if (m < 0) continue;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const long long m = t * 64 + i * 16 + g * 4 + r;
-                if (m >= M) continue;
-#pragma unroll
-                for (int j = 0; j < NT; ++j) {
-                    const int n = j * 16 + li;
-                    if (n >= cso) continue;
-                    const long long o = m * cso + n;
-                    float v = 0.f;
-                    if (n < N) v = epi_value<T>(a, o, acc[i][j][r], bias[j], e_sc[j], e_sf[j], e_mean[j], e_rstd[j],
-                                                s1[j], s2[j]);
-                    stv(&Y[o], v);
-                }
+            for (int j = 0; j < NT; ++j) {
+                const int n0 = j * 16 + 4 * g;
+                if (n0 >= cso) continue;
+                epi4<T>(a, m * cso + n0, acc[i][j], btab + n0, epi_bn, etab + n0, NC, s1[j], s2[j], N - n0);
             }
+        }
+        if (t + tstride < ntiles) {
+            decode(t + tstride);
+            load(0);
+        }
     }
     const bool want_sums = a.out_sums || (epi_bn && a.epi_sums);
     if (want_sums) {
 #pragma unroll
-        for (int j = 0; j < NT; ++j) {
-            s1[j] += __shfl_xor(s1[j], 16, 64);
-            s1[j] += __shfl_xor(s1[j], 32, 64);
-            s2[j] += __shfl_xor(s2[j], 16, 64);
-            s2[j] += __shfl_xor(s2[j], 32, 64);
-            if (lane < 16) {
-                red[(wid * NC + j * 16 + lane) * 2] = s1[j];
-                red[(wid * NC + j * 16 + lane) * 2 + 1] = s2[j];
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float u1 = s1[j][r], u2 = s2[j][r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    u1 += __shfl_xor(u1, o, 64);
+                    u2 += __shfl_xor(u2, o, 64);
+                }
+                if (li == 0) {
+                    red[(wid * NC + j * 16 + 4 * g + r) * 2] = u1;
+                    red[(wid * NC + j * 16 + 4 * g + r) * 2 + 1] = u2;
+                }
             }
-        }
         __syncthreads();
         double* sums = shard_ptr(epi_bn ? a.epi_sums : a.out_sums, shards, N);
         for (int n = tid; n < N; n += 256) {
@@ -548,7 +557,7 @@ size_t stream_lds_bytes(const rnvp_conv_args* a, int nt) {
     const int K = a->ks * a->ks * a->cs_in;
     const int kpl = ((K + KS - 1) / KS) * KS + CH;
     const int nc = 16 * nt, ntmp = a->cs_in > nc ? a->cs_in : nc;
-    return 16 * (size_t)ntmp + 8 * (size_t)a->cs_in + 16 * (size_t)nc + 32 * (size_t)nc +
+    return 16 * (size_t)ntmp + 8 * (size_t)a->cs_in + 16 * (size_t)nc + 4 * (size_t)nc + 32 * (size_t)nc +
            (size_t)nc * kpl * sizeof(T);
 }
 
@@ -588,13 +597,13 @@ int launch_conv(const rnvp_conv_args* a, hipStream_t s) {
     const long long grid = gm * gn;
     const int shards = rnvp_stat_shards(M);
     const int cs = a->cs_in;
-    const size_t shm = 16 * (size_t)(cs > BN ? cs : BN) + 8 * (size_t)cs + 16 * (size_t)BN;
+    const size_t shm = 16 * (size_t)(cs > BN ? cs : BN) + 8 * (size_t)cs + 20 * (size_t)BN;
     int splits = 1;
     if (a->ws && grid < 384 && nk >= 8) {
         splits = (int)((512 + grid - 1) / grid);
         if (splits > MAX_SPLITS) splits = MAX_SPLITS;
         if (splits > nk / 4) splits = nk / 4;
-        while (splits > 1 && (long long)splits * M * a->n > a->ws_elems) --splits;
+        while (splits > 1 && (long long)splits * M * a->cs_out > a->ws_elems) --splits;
     }
     if (splits > 1) {
         const int kps = (nk + splits - 1) / splits;
@@ -1054,6 +1063,7 @@ extern "C" int rnvp_conv2d(const rnvp_conv_args* a, void* stream) {
     if ((a->kp & 63) || a->kp < a->ks * a->ks * a->cs_in) return RNVP_E_INVALID;
     if (!al16(a->x) || !al16(a->w)) return RNVP_E_INVALID;
     if (a->epi_relu_bn_bwd && !a->epi_x) return RNVP_E_INVALID;
+    if ((long long)a->B * a->H * a->W >= (1ll << 31)) return RNVP_E_UNSUPPORTED;
     if (a->B == 0) return RNVP_OK;
     hipStream_t s = (hipStream_t)stream;
     return a->dtype == RNVP_F32 ? dispatch_conv<float>(a, s) : dispatch_conv<bf16_t>(a, s);

@@ -297,7 +297,7 @@ class CouplingEngine:
             e.db_off = self.layout[bname][0] if ob is not None else 0
             descs.append(e)
         tab = (WNDesc * len(descs))(*descs)
-        nmax = max(max(s.cin, s.cout) for s in self.P.convs.values())
+        nmax = max(max(chan_stride(s.cin), chan_stride(s.cout)) for s in self.P.convs.values())
         wse = splitk_elems(M, nmax)
         sc = dict(arena=ar, zero=zr, wn_table=torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(device),
                   wn_key=wsz["key"], wn_rows=wsz["rows"], n_wn=len(descs), shards=sh,

@@ -56,7 +56,7 @@ def conv_case(B, H, W, cin, cout, ks, pro=False, stats=False, residual=False, ac
     sums_out = torch.zeros(sh, 2, cout, device=dev, dtype=torch.float64)
     gam = torch.ones(max(cin, cout), device=dev)
     bet = torch.zeros(max(cin, cout), device=dev)
-    ws = splitk_workspace(dev, 8 * M * cout if M <= 16384 else 1)
+    ws = splitk_workspace(dev, 8 * M * cso if M <= 16384 else 1)
     L = _lib.lib()
     s = torch.cuda.current_stream().cuda_stream
     if wgrad:
