@@ -126,23 +126,46 @@ __device__ __forceinline__ void bn_affine(const rnvp_bn_src& s, int C, int c, fl
 
 // Whole-block reduction of sharded BN sums ([shards][2*C] fp64) for channels
 // [c0, c0+nc) into LDS s1[nc], s2[nc].  Every (channel, shard) pair is a
-// separate, independent load spread over the block (no per-thread serial
-// chain of dependent loads), accumulated with LDS fp64 atomics (ds_add_f64).
+// separate load spread over the block; a thread issues up to 4 pairs' loads
+// at once (the first round before the barrier that zeroes s1/s2), then
+// accumulates them with LDS fp64 atomics (ds_add_f64).
 // Must be reached by every thread of the block.
 __device__ __forceinline__ void block_shard_sums(const double* sums, int C, int shards, int c0, int nc, double* s1,
                                                  double* s2) {
+    constexpr int U = 4;
     if (shards < 1) shards = 1;
-    for (int i = threadIdx.x; i < nc; i += blockDim.x) {
-        s1[i] = 0.0;
-        s2[i] = 0.0;
-    }
-    __syncthreads();
     const int total = nc * shards;
-    for (int t = threadIdx.x; t < total; t += blockDim.x) {
-        const int c = t % nc, h = t / nc;
-        const double* p = sums + (long long)h * 2 * C + c0 + c;
-        atomicAdd(&s1[c], p[0]);
-        atomicAdd(&s2[c], p[C]);
+    auto zero = [&]() {
+        for (int i = threadIdx.x; i < nc; i += blockDim.x) {
+            s1[i] = 0.0;
+            s2[i] = 0.0;
+        }
+        __syncthreads();
+    };
+    if (total <= 0) zero();
+    for (int t0 = 0; t0 < total; t0 += U * blockDim.x) {
+        double v1[U], v2[U];
+        int cc[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int t = t0 + u * blockDim.x + threadIdx.x;
+            cc[u] = -1;
+            v1[u] = v2[u] = 0.0;
+            if (t < total) {
+                const int c = t % nc, h = t / nc;
+                const double* p = sums + (long long)h * 2 * C + c0 + c;
+                v1[u] = p[0];
+                v2[u] = p[C];
+                cc[u] = c;
+            }
+        }
+        if (t0 == 0) zero();
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (cc[u] >= 0) {
+                atomicAdd(&s1[cc[u]], v1[u]);
+                atomicAdd(&s2[cc[u]], v2[u]);
+            }
     }
     __syncthreads();
 }

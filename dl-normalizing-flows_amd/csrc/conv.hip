@@ -964,40 +964,101 @@ __device__ __forceinline__ int find_desc(const rnvp_wn_desc* d, int n, int row) 
     return lo;
 }
 
+__device__ __forceinline__ int find_col(const rnvp_wn_desc* d, int n, int col) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        int mid = (lo + hi + 1) >> 1;
+        if (d[mid].col0 <= col) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+constexpr int WN_ROW_LDS = 4608;
+
+// rows: block per output row co: v row staged in LDS (coalesced), norm,
+// then the packed forward row wf[co][tap*cs_in + ci] in 16-byte stores.
 template <typename T>
-__global__ void k_wn_fwd(const rnvp_wn_desc* __restrict__ descs, int n_desc) {
+__global__ __launch_bounds__(256) void k_wn_rows(const rnvp_wn_desc* __restrict__ descs, int n_desc) {
+    constexpr int CH = Chunk<T>::N;
     __shared__ double red[16];
+    __shared__ float rowbuf[WN_ROW_LDS];
     const int row = blockIdx.x;
     const rnvp_wn_desc d = descs[find_desc(descs, n_desc, row)];
     const int co = row - d.row0;
     const int kk = d.ks * d.ks, kr = d.cin * kk;
     const float* v = d.v + (long long)co * kr;
+    const bool in_lds = kr <= WN_ROW_LDS;
     double ss = 0;
-    for (int i = threadIdx.x; i < kr; i += blockDim.x) ss += (double)v[i] * v[i];
-    ss = block_sum(ss, red);
+    for (int i = threadIdx.x; i < kr; i += blockDim.x) {
+        const float x = v[i];
+        if (in_lds) rowbuf[i] = x;
+        ss += (double)x * x;
+    }
+    ss = block_sum(ss, red);   // (its barriers also publish rowbuf)
     const float nrm = (float)sqrt(ss);
     const float scale = d.g ? d.g[co] / nrm : 1.f;
     if (threadIdx.x == 0 && d.norm) d.norm[co] = nrm;
     T* wf = (T*)d.wf + (long long)co * d.kp_f;
-    for (int k = threadIdx.x; k < d.kp_f; k += blockDim.x) {
-        const int tap = k / d.cs_in, ci = k - tap * d.cs_in;
-        float w = 0.f;
-        if (tap < kk && ci < d.cin) w = scale * v[ci * kk + tap];
-        stv(&wf[k], w);
-    }
-    if (d.wd) {
-        T* wd = (T*)d.wd;
-        for (int i = threadIdx.x; i < kr; i += blockDim.x) {
-            const int ci = i / kk, tp = i - ci * kk;     // dgrad tap tp reads w tap kk-1-tp
-            stv(&wd[(long long)ci * d.kp_d + tp * d.cs_out + co], scale * v[ci * kk + (kk - 1 - tp)]);
+    for (int k0 = threadIdx.x * CH; k0 < d.kp_f; k0 += blockDim.x * CH) {
+        float w[CH];
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int k = k0 + j;
+            const int tap = k / d.cs_in, ci = k - tap * d.cs_in;
+            w[j] = 0.f;
+            if (tap < kk && ci < d.cin) w[j] = scale * (in_lds ? rowbuf[ci * kk + tap] : v[ci * kk + tap]);
         }
+        *(u32x4*)(wf + k0) = pack(w, T());
+    }
+}
+
+// cols: block per data-gradient row ci: the [cout][kk] slab of v that row
+// needs (cout runs of kk contiguous floats) staged in LDS with the per-row
+// scale applied, then wd[ci][tp*cs_out + co] = w[co][ci][kk-1-tp] in 16-byte
+// stores.  Needs k_wn_rows' norms (previous launch).
+template <typename T>
+__global__ __launch_bounds__(256) void k_wn_cols(const rnvp_wn_desc* __restrict__ descs, int n_desc) {
+    constexpr int CH = Chunk<T>::N;
+    __shared__ float sbuf[WN_ROW_LDS];
+    const int col = blockIdx.x;
+    const rnvp_wn_desc d = descs[find_col(descs, n_desc, col)];
+    if (!d.wd) return;
+    const int ci = col - d.col0;
+    const int kk = d.ks * d.ks, kr = d.cin * kk;
+    const int n = d.cout * kk;
+    const bool in_lds = n <= WN_ROW_LDS;
+    auto wval = [&](int co, int tap) {
+        const float sc = d.g ? d.g[co] / d.norm[co] : 1.f;
+        return sc * d.v[(long long)co * kr + ci * kk + tap];
+    };
+    if (in_lds) {
+        for (int q = threadIdx.x; q < n; q += blockDim.x) {
+            const int co = q / kk, tap = q - co * kk;
+            sbuf[q] = wval(co, tap);
+        }
+        __syncthreads();
+    }
+    T* wd = (T*)d.wd + (long long)ci * d.kp_d;
+    for (int k0 = threadIdx.x * CH; k0 < d.kp_d; k0 += blockDim.x * CH) {
+        float w[CH];
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int k = k0 + j;
+            const int tp = k / d.cs_out, co = k - tp * d.cs_out;
+            w[j] = 0.f;
+            if (tp < kk && co < d.cout) {
+                const int tap = kk - 1 - tp;
+                w[j] = in_lds ? sbuf[co * kk + tap] : wval(co, tap);
+            }
+        }
+        *(u32x4*)(wd + k0) = pack(w, T());
     }
 }
 
 // one block per output row co: dW row = sum of the nz partial slabs, gathered
 // into LDS in v's [ci][tap] order (coalesced over the packed k), then the
 // weight-norm backward and the bias partial sum.
-constexpr int WN_ROW_LDS = 4608;
 
 __global__ void k_wn_bwd(const rnvp_wn_desc* __restrict__ descs, int n_desc, float* gbase) {
     __shared__ double red[16];
@@ -1142,13 +1203,19 @@ extern "C" int rnvp_bn_bwd_apply(const rnvp_bn_bwd_args* a, void* stream) {
     return RNVP_OK;
 }
 
-extern "C" int rnvp_weight_norm_fwd(const rnvp_wn_desc* d, int n_desc, int total_rows, int dtype, void* stream) {
-    if (!d || n_desc <= 0 || total_rows <= 0) return RNVP_E_INVALID;
+extern "C" int rnvp_weight_norm_fwd(const rnvp_wn_desc* d, int n_desc, int total_rows, int total_cols, int dtype,
+                                    void* stream) {
+    if (!d || n_desc <= 0 || total_rows <= 0 || total_cols < 0) return RNVP_E_INVALID;
+    if (dtype != RNVP_F32 && dtype != RNVP_BF16) return RNVP_E_INVALID;
     hipStream_t s = (hipStream_t)stream;
-    if (dtype == RNVP_F32) k_wn_fwd<float><<<total_rows, 256, 0, s>>>(d, n_desc);
-    else if (dtype == RNVP_BF16) k_wn_fwd<bf16_t><<<total_rows, 256, 0, s>>>(d, n_desc);
-    else return RNVP_E_INVALID;
+    if (dtype == RNVP_F32) k_wn_rows<float><<<total_rows, 256, 0, s>>>(d, n_desc);
+    else k_wn_rows<bf16_t><<<total_rows, 256, 0, s>>>(d, n_desc);
     RNVP_LAUNCH_CHECK();
+    if (total_cols > 0) {
+        if (dtype == RNVP_F32) k_wn_cols<float><<<total_cols, 256, 0, s>>>(d, n_desc);
+        else k_wn_cols<bf16_t><<<total_cols, 256, 0, s>>>(d, n_desc);
+        RNVP_LAUNCH_CHECK();
+    }
     return RNVP_OK;
 }
 

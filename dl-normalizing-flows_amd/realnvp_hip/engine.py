@@ -186,7 +186,7 @@ class CouplingEngine:
             ar.add("norm:" + name, spec.cout * 4)
         ar.alloc(dev, zero=True)   # zero padding of the packed images, once
         descs = []
-        row0 = 0
+        row0 = col0 = 0
         for name, spec in self.P.convs.items():
             cs_in, cs_out, kp_f, kp_d = geo[name]
             vn, gn, _ = self._conv_names(spec)
@@ -200,18 +200,20 @@ class CouplingEngine:
             d.cout, d.cin, d.ks, d.cs_in, d.kp_f, d.cs_out, d.kp_d, d.row0 = (
                 spec.cout, spec.cin, spec.ks, cs_in, kp_f, cs_out, kp_d, row0)
             d.nz = 1
+            d.col0 = col0
             row0 += spec.cout
+            col0 += spec.cin
             descs.append(d)
         table = (WNDesc * len(descs))(*descs)
         dtab = torch.frombuffer(bytearray(bytes(table)), dtype=torch.uint8).to(dev)
-        ws = dict(key=key, arena=ar, geo=geo, descs=descs, table=dtab, rows=row0, dtype=dtype)
+        ws = dict(key=key, arena=ar, geo=geo, descs=descs, table=dtab, rows=row0, cols=col0, dtype=dtype)
         self._weights[dtype] = ws
         return ws
 
     def prepare_weights(self, dtype):
         ws = self.weights(dtype)
-        _lib.lib().weight_norm_fwd(ws["table"].data_ptr(), len(ws["descs"]), ws["rows"], DTYPES[dtype][0],
-                                   stream_ptr())
+        _lib.lib().weight_norm_fwd(ws["table"].data_ptr(), len(ws["descs"]), ws["rows"], ws["cols"],
+                                   DTYPES[dtype][0], stream_ptr())
         return ws
 
     # ------------------------------------------------------------ workspaces

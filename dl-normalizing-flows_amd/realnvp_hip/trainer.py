@@ -117,6 +117,29 @@ class FlowTrainer:
         self.z = cur
         # backward buffers: a gradient buffer per forward tensor
         self.gbuf = {}
+        self._build_wn_table()
+
+    def _build_wn_table(self):
+        """One weight-norm descriptor table over every conv of the model: the
+        packed bf16/fp32 weight images are refreshed by ONE forward weight-norm
+        call per step (2 launches) instead of one per coupling."""
+        import ctypes as C
+        from ._lib import WNDesc
+        descs = []
+        row0 = col0 = 0
+        for st in self.stages:
+            if st[0] != "coupling":
+                continue
+            for d in st[2].weights(self.dtype)["descs"]:
+                e = WNDesc()
+                C.memmove(C.addressof(e), C.addressof(d), C.sizeof(WNDesc))
+                e.row0, e.col0 = row0, col0
+                row0 += e.cout
+                col0 += e.cin
+                descs.append(e)
+        tab = (WNDesc * len(descs))(*descs)
+        self.wn_table = torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(self.dev)
+        self.wn_n, self.wn_rows, self.wn_cols = len(descs), row0, col0
 
     def _add_coupling(self, mod, x):
         eng = mod.engine()
@@ -153,10 +176,12 @@ class FlowTrainer:
             L.logit_fwd(self.pix.data_ptr(), None, self.seed, 0, self.step_t.data_ptr(), 0.9, self.xl.data_ptr(),
                         self.logdet.data_ptr(), B, n, s)
         self.ldj.zero_()
+        L.weight_norm_fwd(self.wn_table.data_ptr(), self.wn_n, self.wn_rows, self.wn_cols,
+                          1 if self.dtype == "bf16" else 0, s)
         for st in self.stages:
             if st[0] == "coupling":
                 _, mod, eng, x, z, sv, _ = st
-                eng.forward(x, True, self.dtype, False, saved=sv, prepare=True, ldj_sample=self.ldj, z_out=z)
+                eng.forward(x, True, self.dtype, False, saved=sv, prepare=False, ldj_sample=self.ldj, z_out=z)
             elif st[0] == "squeeze":
                 _, a, b = st
                 L.squeeze(a.data_ptr(), b.data_ptr(), *a.shape, s)

@@ -188,11 +188,15 @@ typedef struct rnvp_wn_desc {
     long long dv_off; long long dg_off;
     int cout, cin, ks, cs_in, kp_f, cs_out, kp_d;
     int row0;                          /* first global row (prefix sum of cout) */
+    int col0;                          /* first global wd row (prefix sum of cin) */
     int nz;                            /* dw partial slabs (>= 1) */
     const float* dbp;                  /* bias partials [nz][cout] or NULL */
     long long db_off;                  /* bias gradient offset (elements) */
 } rnvp_wn_desc;
-int rnvp_weight_norm_fwd(const rnvp_wn_desc* descs_device, int n_desc, int total_rows, int dtype, void* stream);
+/* fwd: one launch over the rows (norm + wf) and one over the wd rows
+ * (total_cols = sum of cin), for any number of convs (a whole model). */
+int rnvp_weight_norm_fwd(const rnvp_wn_desc* descs_device, int n_desc, int total_rows, int total_cols, int dtype,
+                         void* stream);
 int rnvp_weight_norm_bwd(const rnvp_wn_desc* descs_device, int n_desc, int total_rows, float* grad_base, void* stream);
 
 /* ---- affine coupling (modules_realnvp.py:239-370) -----------------------
