@@ -125,59 +125,78 @@ __device__ __forceinline__ void bn_affine(const rnvp_bn_src& s, int C, int c, fl
 }
 
 // Whole-block reduction of sharded BN sums ([shards][2*C] fp64) for channels
-// [c0, c0+nc) into LDS s1[nc], s2[nc].  Every (channel, shard) pair is a
-// separate load spread over the block; a thread issues up to 4 pairs' loads
-// at once (the first round before the barrier that zeroes s1/s2), then
-// accumulates them with LDS fp64 atomics (ds_add_f64).
-// Must be reached by every thread of the block.
-__device__ __forceinline__ void block_shard_sums(const double* sums, int C, int shards, int c0, int nc, double* s1,
-                                                 double* s2) {
+// [c0, c0+nc) into LDS s1[nc], s2[nc]; up to two independent sources in one
+// pass.  Every (channel, shard) pair is a separate load spread over the block;
+// a thread issues up to 4 pairs' loads at once (the first round before the
+// barrier that zeroes the outputs), then accumulates them with LDS fp64
+// atomics (ds_add_f64).  Must be reached by every thread of the block.
+struct ShardSrc {
+    const double* sums; int C, shards, c0, nc; double* s1; double* s2;
+};
+
+template <int NS>
+__device__ __forceinline__ void block_shard_sums_n(const ShardSrc (&src)[NS]) {
     constexpr int U = 4;
-    if (shards < 1) shards = 1;
-    const int total = nc * shards;
+    int total[NS], tmax = 0;
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+        total[q] = src[q].sums ? src[q].nc * (src[q].shards < 1 ? 1 : src[q].shards) : 0;
+        tmax = max(tmax, total[q]);
+    }
     auto zero = [&]() {
-        for (int i = threadIdx.x; i < nc; i += blockDim.x) {
-            s1[i] = 0.0;
-            s2[i] = 0.0;
-        }
+#pragma unroll
+        for (int q = 0; q < NS; ++q)
+            for (int i = threadIdx.x; i < src[q].nc; i += blockDim.x) {
+                src[q].s1[i] = 0.0;
+                src[q].s2[i] = 0.0;
+            }
         __syncthreads();
     };
-    if (total <= 0) zero();
-    for (int t0 = 0; t0 < total; t0 += U * blockDim.x) {
-        double v1[U], v2[U];
-        int cc[U];
+    if (tmax <= 0) zero();
+    for (int t0 = 0; t0 < tmax; t0 += U * blockDim.x) {
+        double v1[NS][U], v2[NS][U];
+        int cc[NS][U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int t = t0 + u * blockDim.x + threadIdx.x;
-            cc[u] = -1;
-            v1[u] = v2[u] = 0.0;
-            if (t < total) {
-                const int c = t % nc, h = t / nc;
-                const double* p = sums + (long long)h * 2 * C + c0 + c;
-                v1[u] = p[0];
-                v2[u] = p[C];
-                cc[u] = c;
+        for (int q = 0; q < NS; ++q)
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int t = t0 + u * blockDim.x + threadIdx.x;
+                cc[q][u] = -1;
+                v1[q][u] = v2[q][u] = 0.0;
+                if (t < total[q]) {
+                    const int c = t % src[q].nc, h = t / src[q].nc;
+                    const double* p = src[q].sums + (long long)h * 2 * src[q].C + src[q].c0 + c;
+                    v1[q][u] = p[0];
+                    v2[q][u] = p[src[q].C];
+                    cc[q][u] = c;
+                }
             }
-        }
         if (t0 == 0) zero();
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (cc[u] >= 0) {
-                atomicAdd(&s1[cc[u]], v1[u]);
-                atomicAdd(&s2[cc[u]], v2[u]);
-            }
+        for (int q = 0; q < NS; ++q)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (cc[q][u] >= 0) {
+                    atomicAdd(&src[q].s1[cc[q][u]], v1[q][u]);
+                    atomicAdd(&src[q].s2[cc[q][u]], v2[q][u]);
+                }
     }
     __syncthreads();
 }
 
-// Whole-block BN table for channels [c0, c0+nc): scale/shift such that
+__device__ __forceinline__ void block_shard_sums(const double* sums, int C, int shards, int c0, int nc, double* s1,
+                                                 double* s2) {
+    const ShardSrc src[1] = {{sums, C, shards, c0, nc, s1, s2}};
+    block_shard_sums_n<1>(src);
+}
+
+// BN table for channels [c0, c0+nc) from already-reduced sums tmp[0..nc) /
+// tmp[nc..2nc) (train) or the running stats (eval): scale/shift such that
 // bn(x) = x*scale + shift, plus mean / rstd when requested.  Channels >= C
-// (padding) get scale = shift = 0, mean = 0, rstd = 1.  tmp: 2*nc doubles of
-// LDS.  Must be reached by every thread of the block.
-__device__ __forceinline__ void block_bn_table(const rnvp_bn_src& s, int C, int c0, int nc, float* scale, float* shift,
-                                               float* mean_out, float* rstd_out, double* tmp) {
+// (padding) get scale = shift = 0, mean = 0, rstd = 1.
+__device__ __forceinline__ void block_bn_finish(const rnvp_bn_src& s, int C, int c0, int nc, float* scale, float* shift,
+                                                float* mean_out, float* rstd_out, const double* tmp) {
     const int nv = max(0, min(nc, C - c0));
-    if (s.sums) block_shard_sums(s.sums, C, s.shards, c0, nv, tmp, tmp + nc);
     for (int i = threadIdx.x; i < nc; i += blockDim.x) {
         const int c = c0 + i;
         float sc = 0.f, sf = 0.f, mo = 0.f, ro = 1.f;
@@ -205,6 +224,15 @@ __device__ __forceinline__ void block_bn_table(const rnvp_bn_src& s, int C, int 
         if (rstd_out) rstd_out[i] = ro;
     }
     __syncthreads();
+}
+
+// Whole-block BN table (shard reduction + finish).  tmp: 2*nc doubles of LDS.
+// Must be reached by every thread of the block.
+__device__ __forceinline__ void block_bn_table(const rnvp_bn_src& s, int C, int c0, int nc, float* scale, float* shift,
+                                               float* mean_out, float* rstd_out, double* tmp) {
+    const int nv = max(0, min(nc, C - c0));
+    if (s.sums) block_shard_sums(s.sums, C, s.shards, c0, nv, tmp, tmp + nc);
+    block_bn_finish(s, C, c0, nc, scale, shift, mean_out, rstd_out, tmp);
 }
 
 static inline int rnvp_grid(long long n, int block, int cap = 4096) {

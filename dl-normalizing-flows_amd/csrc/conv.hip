@@ -880,8 +880,10 @@ __global__ __launch_bounds__(256) void k_wgrad_grouped(rnvp_wgrad_group g) {
     const long long mb = (long long)z * cv.m_per_slab;
     const long long me = (mb + cv.m_per_slab < M) ? mb + cv.m_per_slab : M;
     const WgView v{cv.x, cv.dy, cv.pro, g.H, g.W, cv.ks, cv.cs_in, cv.cin, cv.cs_dy, cv.n, cv.kp, cv.pro_bn_relu};
-    wgrad_tile<T>(v, cot * 64, kt * 64, mb, me, M, cv.ws + (long long)z * cv.n * cv.kp, false,
-                  (cv.wsb && kt == 0) ? cv.wsb + (long long)z * cv.n : nullptr, false);
+    const int rep = z % cv.nrep;
+    const bool atomic = cv.nrep < cv.nz;
+    wgrad_tile<T>(v, cot * 64, kt * 64, mb, me, M, cv.ws + (long long)rep * cv.n * cv.kp, atomic,
+                  (cv.wsb && kt == 0) ? cv.wsb + (long long)rep * cv.n : nullptr, atomic);
 }
 
 // ---------------------------------------------------------------------------
@@ -896,8 +898,17 @@ __global__ void k_bn_bwd(rnvp_bn_bwd_args a) {
     double* gs = dsm + 2 * cs;
     float* p = (float*)(dsm + 4 * cs);   // per channel: coef, k1, k2, mean, rstd
     float* t_sc = p + 5 * cs;            // scratch: scale, shift, mean, rstd [cs each]
-    block_bn_table(a.bn, C, 0, cs, t_sc, t_sc + cs, t_sc + 2 * cs, t_sc + 3 * cs, dsm);
-    block_shard_sums(a.sums, C, a.sum_shards, 0, C, gs, gs + cs);
+    {   // both shard reductions (forward BN stats, backward g-sums) in one pass
+        if (a.bn.sums) {
+            const ShardSrc src[2] = {{a.sums, C, a.sum_shards, 0, C, gs, gs + cs},
+                                     {a.bn.sums, C, a.bn.shards, 0, C, dsm, dsm + cs}};
+            block_shard_sums_n<2>(src);
+        } else {
+            const ShardSrc src[1] = {{a.sums, C, a.sum_shards, 0, C, gs, gs + cs}};
+            block_shard_sums_n<1>(src);
+        }
+        block_bn_finish(a.bn, C, 0, cs, t_sc, t_sc + cs, t_sc + 2 * cs, t_sc + 3 * cs, dsm);
+    }
     for (int c = threadIdx.x; c < cs; c += blockDim.x) {
         float coef = 0.f, k1 = 0.f, k2 = 0.f, mean = 0.f, rstd = 1.f;
         if (c < C) {
@@ -1072,6 +1083,7 @@ __global__ void k_wn_bwd(const rnvp_wn_desc* __restrict__ descs, int n_desc, flo
     const float* v = d.v + (long long)co * kr;
     const float* dw = d.dw + (long long)co * d.kp_f;
     const bool in_lds = kr <= WN_ROW_LDS;
+    float* dwz = d.dw + (long long)co * d.kp_f;
     auto dw_at = [&](int k) {
         float t = 0.f;
         for (int z = 0; z < nz; ++z) t += dw[z * zs + k];
@@ -1108,7 +1120,14 @@ __global__ void k_wn_bwd(const rnvp_wn_desc* __restrict__ descs, int n_desc, flo
         for (int z = threadIdx.x; z < nz; z += blockDim.x) bs += d.dbp[(long long)z * d.cout + co];
         bs = block_sum(bs, (float*)red);
         if (threadIdx.x == 0) gbase[d.db_off + co] = bs;
+        __syncthreads();
+        for (int z = threadIdx.x; z < nz; z += blockDim.x) d.dbp[(long long)z * d.cout + co] = 0.f;
     }
+    // leave the partial-sum replicas zero for the next grouped wgrad
+    __syncthreads();
+    const int K = kk * d.cs_in;
+    for (int z = 0; z < nz; ++z)
+        for (int k = threadIdx.x; k < K; k += blockDim.x) dwz[z * zs + k] = 0.f;
 }
 
 inline bool al16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
@@ -1151,6 +1170,8 @@ extern "C" int rnvp_wgrad_slabs(long long M) {
     return (int)z;
 }
 
+extern "C" int rnvp_wgrad_replicas(int nz) { return nz < 8 ? (nz < 1 ? 1 : nz) : 8; }
+
 extern "C" int rnvp_conv2d_wgrad_grouped(const rnvp_wgrad_group* gin, void* stream) {
     if (!gin || gin->n_conv <= 0 || gin->n_conv > RNVP_WGRAD_GROUP_MAX) return RNVP_E_INVALID;
     if (gin->dtype != RNVP_F32 && gin->dtype != RNVP_BF16) return RNVP_E_INVALID;
@@ -1165,7 +1186,7 @@ extern "C" int rnvp_conv2d_wgrad_grouped(const rnvp_wgrad_group* gin, void* stre
         rnvp_wgrad_conv& v = g.conv[c];
         if (!v.x || !v.dy || !v.ws) return RNVP_E_INVALID;
         if (v.ks != 1 && v.ks != 3) return RNVP_E_UNSUPPORTED;
-        if (v.n <= 0 || v.cin <= 0 || v.nz <= 0) return RNVP_E_INVALID;
+        if (v.n <= 0 || v.cin <= 0 || v.nz <= 0 || v.nrep <= 0 || v.nrep > v.nz) return RNVP_E_INVALID;
         if ((v.cs_in & 7) || (v.cs_dy & 7) || v.cs_in < v.cin || v.cs_dy < v.n) return RNVP_E_INVALID;
         if (v.kp < v.ks * v.ks * v.cs_in) return RNVP_E_INVALID;
         if (!al16(v.x) || !al16(v.dy)) return RNVP_E_INVALID;

@@ -6,8 +6,9 @@
 // plus the exact inverse (reverse=True, running out_bn stats) and the
 // backward of both parts, including the cross-sample batch-variance gradient.
 //
-// Flow tensors are NCHW fp32; one block per (b, c) plane for the reductions
-// (coalesced over H*W), grid-stride elementwise passes otherwise.
+// Flow tensors are NCHW fp32, net tensors NHWC; the reductions and the
+// NHWC-touching passes run on pixel tiles (see "pixel tiles" below), the
+// purely elementwise NCHW passes grid-stride.
 #include <math.h>
 
 #include "common.h"
@@ -50,48 +51,116 @@ template <typename T>
 __device__ __forceinline__ const T* cptr(const void* p) { return (const T*)p; }
 
 // ---------------------------------------------------------------------------
-// in part, forward
+// pixel tiles
 // ---------------------------------------------------------------------------
-// one block per (b, cb) plane of the in_bn input: sums of xm and xm^2
-__global__ void k_in_stats(rnvp_coupling_args a) {
-    __shared__ double red[16];
-    const Geo g = geo(a);
-    const int b = blockIdx.x / g.Cb, cb = blockIdx.x % g.Cb;
-    const int c = (g.kind == 0) ? cb : g.off_base + cb;
-    const float* xp = a.x + ((long long)b * g.C + c) * g.HW;
-    float s = 0.f, s2 = 0.f;
-    for (int p = threadIdx.x; p < g.HW; p += blockDim.x) {
-        float v = xp[p];
-        if (g.kind == 0 && !ckbd_m(g, p)) v = 0.f;
-        s += v;
-        s2 += v * v;
-    }
-    double ds = block_sum((double)s, red);
-    double ds2 = block_sum((double)s2, red);
-    if (threadIdx.x == 0) {
-        atomicAdd(&a.in_sums[cb], ds);
-        atomicAdd(&a.in_sums[g.Cb + cb], ds2);
-    }
+// A workgroup owns TP consecutive pixels of one image (all channels): NCHW
+// flow-tensor planes are read/written as coalesced TP-runs per channel, the
+// NHWC net tensors (h0, st and their gradients) as one contiguous
+// [TP][cs] region staged through LDS, per-channel reductions are wave
+// segment sums (seg = min(TP, 64) lanes share a channel) folded into LDS and
+// then one global atomic per channel per workgroup.
+struct Tile {
+    int b, p0, tp;
+    long long m0;
+};
+
+__device__ __forceinline__ Tile tile_of(const Geo& g, int TP) {
+    const int tpi = (g.HW + TP - 1) / TP;
+    Tile t;
+    t.b = blockIdx.x / tpi;
+    t.p0 = (blockIdx.x - t.b * tpi) * TP;
+    t.tp = min(TP, g.HW - t.p0);
+    t.m0 = (long long)t.b * g.HW + t.p0;
+    return t;
 }
 
-// h0[m][ch] NHWC: relu(xa), relu(-xa) [, mask], zero pad.  One thread per (m, ch).
+// sum over groups of `seg` lanes (power of 2 <= 64; 1 = no reduction)
+__device__ __forceinline__ float seg_sum(float v, int seg) {
+    for (int o = 1; o < seg; o <<= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
 template <typename T>
-__global__ void k_in_apply(rnvp_coupling_args a) {
-    extern __shared__ float sh[];   // 2*Cb floats: scale, shift
-    const Geo g = geo(a);
-    const double cnt = (double)g.B * g.HW;
-    for (int c = threadIdx.x; c < g.Cb; c += blockDim.x) {
+__device__ __forceinline__ void tile_copy_in(const void* src, long long m0, int tp, int cs, T* lds) {
+    const int n16 = tp * cs * (int)sizeof(T) / 16;
+    const u32x4* s = (const u32x4*)((const T*)src + m0 * cs);
+    u32x4* d = (u32x4*)lds;
+    for (int i = threadIdx.x; i < n16; i += blockDim.x) d[i] = s[i];
+}
+
+template <typename T>
+__device__ __forceinline__ void tile_copy_out(const T* lds, long long m0, int tp, int cs, void* dst) {
+    const int n16 = tp * cs * (int)sizeof(T) / 16;
+    const u32x4* s = (const u32x4*)lds;
+    u32x4* d = (u32x4*)((T*)dst + m0 * cs);
+    for (int i = threadIdx.x; i < n16; i += blockDim.x) d[i] = s[i];
+}
+
+__device__ __forceinline__ void lds_zero(double* p, int n) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) p[i] = 0.0;
+}
+
+// per-channel in_bn table of the in part: scale, shift, mean, rstd [Cb each]
+__device__ __forceinline__ void in_bn_table(const rnvp_coupling_args& a, const Geo& g, float* t) {
+    for (int cb = threadIdx.x; cb < g.Cb; cb += blockDim.x) {
         rnvp_bn_src s;
         s.shards = 1;
         s.sums = a.training ? a.in_sums : nullptr;
-        s.count = cnt;
+        s.count = (double)g.B * g.HW;
         s.mean = a.in_rmean; s.var = a.in_rvar;
         s.gamma = a.in_gamma; s.beta = a.in_beta; s.eps = a.eps;
-        float sc, sf;
-        bn_affine(s, g.Cb, c, sc, sf);
-        sh[c] = sc;
-        sh[g.Cb + c] = sf;
-        if (blockIdx.x == 0 && a.training && a.in_rmean) {
+        float sc, sf, mean, rstd;
+        bn_affine(s, g.Cb, cb, sc, sf, &mean, &rstd);
+        t[cb] = sc;
+        t[g.Cb + cb] = sf;
+        t[2 * g.Cb + cb] = mean;
+        t[3 * g.Cb + cb] = rstd;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// in part, forward
+// ---------------------------------------------------------------------------
+// sums of xm and xm^2 per in_bn channel
+__global__ __launch_bounds__(256) void k_in_stats(rnvp_coupling_args a, int TP, int seg) {
+    extern __shared__ double red[];   // [2*Cb]
+    const Geo g = geo(a);
+    const Tile t = tile_of(g, TP);
+    const int lane = threadIdx.x & 63;
+    lds_zero(red, 2 * g.Cb);
+    __syncthreads();
+    const int total = g.Cb * t.tp;
+    for (int e0 = 0; e0 < total; e0 += blockDim.x) {
+        const int e = e0 + threadIdx.x;
+        const bool ok = e < total;
+        const int cb = ok ? e / t.tp : 0, p = t.p0 + (ok ? e - cb * t.tp : 0);
+        const int c = (g.kind == 0) ? cb : g.off_base + cb;
+        float v = ok ? a.x[((long long)t.b * g.C + c) * g.HW + p] : 0.f;
+        if (g.kind == 0 && !ckbd_m(g, p)) v = 0.f;
+        const float s1 = seg_sum(v, seg), s2 = seg_sum(v * v, seg);
+        if (ok && (lane & (seg - 1)) == 0) {
+            atomicAdd(&red[cb], (double)s1);
+            atomicAdd(&red[g.Cb + cb], (double)s2);
+        }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < 2 * g.Cb; c += blockDim.x) atomicAdd(&a.in_sums[c], red[c]);
+}
+
+// h0[m][ch] NHWC: relu(xa), relu(-xa) [, mask], zero pad; built in LDS, stored
+// as one contiguous region.  Block 0 updates the in_bn running stats.
+template <typename T>
+__global__ __launch_bounds__(256) void k_in_apply(rnvp_coupling_args a, int TP, int seg) {
+    extern __shared__ double dsm[];
+    const Geo g = geo(a);
+    const Tile t = tile_of(g, TP);
+    float* tab = (float*)dsm;                   // [4*Cb]
+    T* h = (T*)(tab + 4 * ((g.Cb + 3) / 4 * 4));  // [tp][cs_h0] (16-B aligned)
+    const int cs = a.cs_h0;
+    in_bn_table(a, g, tab);
+    if (blockIdx.x == 0 && a.training && a.in_rmean) {
+        const double cnt = (double)g.B * g.HW;
+        for (int c = threadIdx.x; c < g.Cb; c += blockDim.x) {
             double mean = a.in_sums[c] / cnt;
             double var = a.in_sums[g.Cb + c] / cnt - mean * mean;
             if (var < 0) var = 0;
@@ -99,74 +168,79 @@ __global__ void k_in_apply(rnvp_coupling_args a) {
             a.in_rmean[c] = (1.f - a.momentum) * a.in_rmean[c] + a.momentum * (float)mean;
             a.in_rvar[c] = (1.f - a.momentum) * a.in_rvar[c] + a.momentum * (float)unb;
         }
+        if (threadIdx.x == 0 && a.in_nbt) a.in_nbt[0] += 1;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0 && a.training && a.in_nbt) a.in_nbt[0] += 1;
-    __syncthreads();
-    T* h0 = (T*)a.h0;
-    const int cs = a.cs_h0;
-    const long long n = (long long)g.B * g.HW * cs;
-    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
-        const int ch = (int)(e % cs);
-        const long long m = e / cs;
-        const int p = (int)(m % g.HW);
-        const long long b = m / g.HW;
-        float out = 0.f;
-        if (ch < 2 * g.Cb) {
-            const int cb = ch < g.Cb ? ch : ch - g.Cb;
-            const int c = (g.kind == 0) ? cb : g.off_base + cb;
-            float v = a.x[(b * g.C + c) * g.HW + p];
-            if (g.kind == 0 && !ckbd_m(g, p)) v = 0.f;
-            float xa = v * sh[cb] + sh[g.Cb + cb];
-            out = ch < g.Cb ? fmaxf(xa, 0.f) : fmaxf(-xa, 0.f);
-        } else if (g.kind == 0 && ch == 2 * g.Cb) {
-            out = (float)ckbd_m(g, p);   // relu(mask) = mask
+    // padding channels (and the mask channel) first
+    for (int e = threadIdx.x; e < t.tp * cs; e += blockDim.x) {
+        const int pl = e / cs, ch = e - pl * cs;
+        if (ch >= 2 * g.Cb) {
+            float out = 0.f;
+            if (g.kind == 0 && ch == 2 * g.Cb) out = (float)ckbd_m(g, t.p0 + pl);   // relu(mask) = mask
+            stv(&h[e], out);
         }
-        stv(&h0[e], out);
     }
+    __syncthreads();
+    const int total = g.Cb * t.tp;
+    for (int e = threadIdx.x; e < total; e += blockDim.x) {
+        const int cb = e / t.tp, pl = e - cb * t.tp, p = t.p0 + pl;
+        const int c = (g.kind == 0) ? cb : g.off_base + cb;
+        float v = a.x[((long long)t.b * g.C + c) * g.HW + p];
+        if (g.kind == 0 && !ckbd_m(g, p)) v = 0.f;
+        const float xa = v * tab[cb] + tab[g.Cb + cb];
+        stv(&h[pl * cs + cb], fmaxf(xa, 0.f));
+        stv(&h[pl * cs + g.Cb + cb], fmaxf(-xa, 0.f));
+    }
+    __syncthreads();
+    tile_copy_out<T>(h, t.m0, t.tp, cs, a.h0);
 }
 
 // ---------------------------------------------------------------------------
 // out part, forward
 // ---------------------------------------------------------------------------
 // u = x*exp(lr)+shift on transformed positions (x elsewhere); stats of u over
-// the out_bn channels; ldj_sample[b] += sum lr.  One block per (b, c) plane.
+// the out_bn channels; ldj_sample[b] += sum lr.
 template <typename T>
-__global__ void k_out1(rnvp_coupling_args a) {
-    __shared__ double red[16];
+__global__ __launch_bounds__(256) void k_out1(rnvp_coupling_args a, int TP, int seg) {
+    extern __shared__ double dsm[];
     const Geo g = geo(a);
-    const int b = blockIdx.x / g.C, c = blockIdx.x % g.C;
-    const long long plane = ((long long)b * g.C + c) * g.HW;
-    const T* st = cptr<T>(a.st);
-    const bool chan_on = g.kind == 1 && c >= g.on_base && c < g.on_base + g.Cb;
-    const int cb = g.kind == 0 ? c : c - g.on_base;
+    const Tile t = tile_of(g, TP);
+    const int lane = threadIdx.x & 63;
+    double* red = dsm;                          // [2*Cb] (+ pad to 16 B)
+    __shared__ float redl[16];
+    T* st = (T*)(dsm + 2 * ((g.Cb + 1) / 2 * 2));   // [tp][cs_st]
+    lds_zero(red, 2 * g.Cb);
+    tile_copy_in<T>(a.st, t.m0, t.tp, a.cs_st, st);
+    __syncthreads();
     const float sc = a.scale[0], ss = a.scale_shift[0];
-    float s = 0.f, s2 = 0.f, sl = 0.f;
-    for (int p = threadIdx.x; p < g.HW; p += blockDim.x) {
-        float xv = a.x[plane + p];
-        float u = xv;
-        bool tr = g.kind == 0 ? !ckbd_m(g, p) : chan_on;
+    float sl = 0.f;
+    const int total = g.C * t.tp;
+    for (int e0 = 0; e0 < total; e0 += blockDim.x) {
+        const int e = e0 + threadIdx.x;
+        const bool ok = e < total;
+        const int c = ok ? e / t.tp : 0, pl = ok ? e - c * t.tp : 0, p = t.p0 + pl;
+        const long long idx = ((long long)t.b * g.C + c) * g.HW + p;
+        const bool chan_on = g.kind == 1 && c >= g.on_base && c < g.on_base + g.Cb;
+        const int cb = g.kind == 0 ? c : c - g.on_base;
+        const bool tr = ok && (g.kind == 0 ? !ckbd_m(g, p) : chan_on);
+        float u = ok ? a.x[idx] : 0.f;
         if (tr) {
-            const long long m = (long long)b * g.HW + p;
-            float sh = ldv(&st[m * a.cs_st + cb]);
-            float r = ldv(&st[m * a.cs_st + g.Cb + cb]);
-            float lr = sc * tanhf(r) + ss;
-            u = xv * expf(lr) + sh;
+            const float sh = ldv(&st[pl * a.cs_st + cb]);
+            const float r = ldv(&st[pl * a.cs_st + g.Cb + cb]);
+            const float lr = sc * tanhf(r) + ss;
+            u = u * expf(lr) + sh;
             sl += lr;
         }
-        a.u[plane + p] = u;
-        s += u;
-        s2 += u * u;
-    }
-    double ds = block_sum((double)s, red);
-    double ds2 = block_sum((double)s2, red);
-    double dl = block_sum((double)sl, red);
-    if (threadIdx.x == 0) {
-        if ((g.kind == 0 || chan_on) && a.out_sums) {
-            atomicAdd(&a.out_sums[cb], ds);
-            atomicAdd(&a.out_sums[g.Cb + cb], ds2);
+        if (ok) a.u[idx] = u;
+        const float s1 = seg_sum(u, seg), s2 = seg_sum(u * u, seg);
+        if (ok && (g.kind == 0 || chan_on) && (lane & (seg - 1)) == 0) {
+            atomicAdd(&red[cb], (double)s1);
+            atomicAdd(&red[g.Cb + cb], (double)s2);
         }
-        if (dl != 0.0) atomicAdd(&a.ldj_sample[b], (float)dl);
     }
+    const float dl = block_sum(sl, redl);   // (barriers also publish red)
+    if (threadIdx.x == 0 && dl != 0.f) atomicAdd(&a.ldj_sample[t.b], dl);
+    if (a.out_sums)
+        for (int c = threadIdx.x; c < 2 * g.Cb; c += blockDim.x) atomicAdd(&a.out_sums[c], red[c]);
 }
 
 // z = out_bn(u) on transformed positions; ldj var term; running stats.
@@ -288,194 +362,214 @@ __device__ __forceinline__ float gl_at(const rnvp_coupling_args& a, long long e,
     return a.gl_full ? a.gl_full[e] : (a.gl_sample ? a.gl_sample[b] : 0.f);
 }
 
-// per-channel A = sum t*gz, Bs = sum t*gz*xhat, G = sum t*gl over all (b, pos)
-__global__ void k_out_bwd_red(rnvp_coupling_args a) {
-    __shared__ double red[16];
-    const Geo g = geo(a);
-    const int b = blockIdx.x / g.Cb, cb = blockIdx.x % g.Cb;
-    const int c = g.kind == 0 ? cb : g.on_base + cb;
-    const long long plane = ((long long)b * g.C + c) * g.HW;
+// out_bn statistics of the forward (train) or running (eval) for channel cb
+__device__ __forceinline__ void out_bn_stats(const rnvp_coupling_args& a, const Geo& g, int cb, float& fm, float& rstd) {
     const double cnt = (double)g.B * g.HW;
-    double mean = a.out_sums[cb] / cnt;
-    double var = a.out_sums[g.Cb + cb] / cnt - mean * mean;
-    if (var < 0) var = 0;
-    const float fm = (float)mean, rstd = (float)(1.0 / sqrt(var + (double)a.eps));
-    float sA = 0.f, sB = 0.f, sG = 0.f;
-    for (int p = threadIdx.x; p < g.HW; p += blockDim.x) {
-        bool tr = g.kind == 0 ? !ckbd_m(g, p) : true;
-        if (!tr) continue;
-        const long long e = plane + p;
-        float gz = a.gz[e];
-        float xh = (a.u[e] - fm) * rstd;
-        sA += gz;
-        sB += gz * xh;
-        sG += gl_at(a, e, b);
+    double mean, var;
+    if (a.training) {
+        mean = a.out_sums[cb] / cnt;
+        var = a.out_sums[g.Cb + cb] / cnt - mean * mean;
+        if (var < 0) var = 0;
+    } else {
+        mean = a.out_rmean[cb];
+        var = a.out_rvar[cb];
     }
-    double dA = block_sum((double)sA, red);
-    double dB = block_sum((double)sB, red);
-    double dG = block_sum((double)sG, red);
-    if (threadIdx.x == 0) {
-        atomicAdd(&a.bwd_sums[cb], dA);
-        atomicAdd(&a.bwd_sums[g.Cb + cb], dB);
-        atomicAdd(&a.bwd_sums[2 * g.Cb + cb], dG);
-    }
+    fm = (float)mean;
+    rstd = (float)(1.0 / sqrt(var + (double)a.eps));
 }
 
-// gx (direct part), gst = [g_shift | g_r], g_scale, g_scale_shift.  One block
-// per (b, c) plane so the scale reductions stay block-local.
-template <typename T>
-__global__ void k_out_bwd_apply(rnvp_coupling_args a) {
-    __shared__ double red[16];
+// per-channel A = sum t*gz, Bs = sum t*gz*xhat, G = sum t*gl over all (b, pos)
+__global__ __launch_bounds__(256) void k_out_bwd_red(rnvp_coupling_args a, int TP, int seg) {
+    extern __shared__ double dsm[];
     const Geo g = geo(a);
-    const int b = blockIdx.x / g.C, c = blockIdx.x % g.C;
-    const long long plane = ((long long)b * g.C + c) * g.HW;
-    const bool chan_on = g.kind == 1 && c >= g.on_base && c < g.on_base + g.Cb;
-    const int cb = g.kind == 0 ? c : c - g.on_base;
-    const bool has_bn_chan = g.kind == 0 || chan_on;
-    const double cnt = (double)g.B * g.HW;
-    float fm = 0.f, rstd = 1.f, kA = 0.f, kB = 0.f;
-    if (a.coupling_bn && has_bn_chan) {
-        double mean, var;
-        if (a.training) {
-            mean = a.out_sums[cb] / cnt;
-            var = a.out_sums[g.Cb + cb] / cnt - mean * mean;
-            if (var < 0) var = 0;
-        } else {
-            mean = a.out_rmean[cb];
-            var = a.out_rvar[cb];
+    const Tile t = tile_of(g, TP);
+    const int lane = threadIdx.x & 63;
+    double* red = dsm;                           // [3*Cb]
+    float* tab = (float*)(dsm + 3 * g.Cb);       // mean | rstd [Cb each]
+    lds_zero(red, 3 * g.Cb);
+    for (int cb = threadIdx.x; cb < g.Cb; cb += blockDim.x) out_bn_stats(a, g, cb, tab[cb], tab[g.Cb + cb]);
+    __syncthreads();
+    const int total = g.Cb * t.tp;
+    for (int e0 = 0; e0 < total; e0 += blockDim.x) {
+        const int e = e0 + threadIdx.x;
+        const bool ok = e < total;
+        const int cb = ok ? e / t.tp : 0, p = t.p0 + (ok ? e - cb * t.tp : 0);
+        const int c = g.kind == 0 ? cb : g.on_base + cb;
+        const bool tr = ok && (g.kind == 0 ? !ckbd_m(g, p) : true);
+        float vA = 0.f, vB = 0.f, vG = 0.f;
+        if (tr) {
+            const long long idx = ((long long)t.b * g.C + c) * g.HW + p;
+            const float gz = a.gz[idx];
+            vA = gz;
+            vB = gz * (a.u[idx] - tab[cb]) * tab[g.Cb + cb];
+            vG = gl_at(a, idx, t.b);
         }
-        fm = (float)mean;
-        rstd = (float)(1.0 / sqrt(var + (double)a.eps));
-        if (a.training) {
-            kA = (float)(a.bwd_sums[cb] / cnt);
-            kB = (float)((a.bwd_sums[g.Cb + cb] + a.bwd_sums[2 * g.Cb + cb]) / cnt);
+        vA = seg_sum(vA, seg);
+        vB = seg_sum(vB, seg);
+        vG = seg_sum(vG, seg);
+        if (ok && (lane & (seg - 1)) == 0) {
+            atomicAdd(&red[cb], (double)vA);
+            atomicAdd(&red[g.Cb + cb], (double)vB);
+            atomicAdd(&red[2 * g.Cb + cb], (double)vG);
         }
     }
-    const T* st = cptr<T>(a.st);
-    T* gst = (T*)a.gst;
+    __syncthreads();
+    for (int c = threadIdx.x; c < 3 * g.Cb; c += blockDim.x) atomicAdd(&a.bwd_sums[c], red[c]);
+}
+
+// gx (direct part), gst = [g_shift | g_r] (built in LDS, stored as one
+// region incl. zero padding), g_scale, g_scale_shift (one atomic per block).
+template <typename T>
+__global__ __launch_bounds__(256) void k_out_bwd_apply(rnvp_coupling_args a, int TP, int seg) {
+    extern __shared__ double dsm[];
+    __shared__ float redl[16];
+    const Geo g = geo(a);
+    const Tile t = tile_of(g, TP);
+    float* tab = (float*)dsm;                         // fm | rstd | kA | kB [Cb each]
+    const int tabn = 4 * ((g.Cb + 3) / 4 * 4);
+    T* st = (T*)(tab + tabn);                         // [tp][cs_st]
+    T* gs = st + t.tp * a.cs_st;                      // [tp][cs_gst]
+    const double cnt = (double)g.B * g.HW;
+    for (int cb = threadIdx.x; cb < g.Cb; cb += blockDim.x) {
+        float fm = 0.f, rstd = 1.f, kA = 0.f, kB = 0.f;
+        if (a.coupling_bn) {
+            out_bn_stats(a, g, cb, fm, rstd);
+            if (a.training) {
+                kA = (float)(a.bwd_sums[cb] / cnt);
+                kB = (float)((a.bwd_sums[g.Cb + cb] + a.bwd_sums[2 * g.Cb + cb]) / cnt);
+            }
+        }
+        tab[cb] = fm; tab[g.Cb + cb] = rstd; tab[2 * g.Cb + cb] = kA; tab[3 * g.Cb + cb] = kB;
+    }
+    tile_copy_in<T>(a.st, t.m0, t.tp, a.cs_st, st);
+    for (int e = threadIdx.x; e < t.tp * a.cs_gst; e += blockDim.x) stv(&gs[e], 0.f);
+    __syncthreads();
     const float sc = a.scale[0], ss = a.scale_shift[0];
     float gsc = 0.f, gss = 0.f;
-    for (int p = threadIdx.x; p < g.HW; p += blockDim.x) {
-        const long long e = plane + p;
-        const long long m = (long long)b * g.HW + p;
-        bool tr = g.kind == 0 ? !ckbd_m(g, p) : chan_on;
-        float gz = a.gz[e];
+    const int total = g.C * t.tp;
+    for (int e = threadIdx.x; e < total; e += blockDim.x) {
+        const int c = e / t.tp, pl = e - c * t.tp, p = t.p0 + pl;
+        const long long idx = ((long long)t.b * g.C + c) * g.HW + p;
+        const bool chan_on = g.kind == 1 && c >= g.on_base && c < g.on_base + g.Cb;
+        const int cb = g.kind == 0 ? c : c - g.on_base;
+        const bool has_bn_chan = g.kind == 0 || chan_on;
+        const bool tr = g.kind == 0 ? !ckbd_m(g, p) : chan_on;
+        const float gz = a.gz[idx];
         float gu;
         if (!a.coupling_bn || !has_bn_chan) {
             gu = gz;
-        } else if (!tr) {
-            // ckbd kept position: z = u, but u still moves the batch stats
-            gu = gz;
-            if (a.training) gu += rstd * (-kA - (a.u[e] - fm) * rstd * kB);
         } else {
-            gu = rstd * gz;
-            if (a.training) gu = rstd * (gz - kA - (a.u[e] - fm) * rstd * kB);
+            const float fm = tab[cb], rstd = tab[g.Cb + cb], kA = tab[2 * g.Cb + cb], kB = tab[3 * g.Cb + cb];
+            if (!tr) {   // ckbd kept position: z = u, but u still moves the batch stats
+                gu = gz;
+                if (a.training) gu += rstd * (-kA - (a.u[idx] - fm) * rstd * kB);
+            } else {
+                gu = rstd * gz;
+                if (a.training) gu = rstd * (gz - kA - (a.u[idx] - fm) * rstd * kB);
+            }
         }
         if (tr) {
-            float r = ldv(&st[m * a.cs_st + g.Cb + cb]);
-            float th = tanhf(r);
-            float lr = sc * th + ss;
-            float ex = expf(lr);
-            float xv = a.x[e];
-            a.gx[e] = gu * ex;
-            float glr = gu * xv * ex + gl_at(a, e, b);
-            stv(&gst[m * a.cs_gst + cb], gu);
-            stv(&gst[m * a.cs_gst + g.Cb + cb], glr * sc * (1.f - th * th));
+            const float r = ldv(&st[pl * a.cs_st + g.Cb + cb]);
+            const float th = tanhf(r);
+            const float ex = expf(sc * th + ss);
+            a.gx[idx] = gu * ex;
+            const float glr = gu * a.x[idx] * ex + gl_at(a, idx, t.b);
+            stv(&gs[pl * a.cs_gst + cb], gu);
+            stv(&gs[pl * a.cs_gst + g.Cb + cb], glr * sc * (1.f - th * th));
             gsc += glr * th;
             gss += glr;
         } else {
-            a.gx[e] = gu;
-            if (g.kind == 0) {   // masked position: st gradients are zero
-                stv(&gst[m * a.cs_gst + cb], 0.f);
-                stv(&gst[m * a.cs_gst + g.Cb + cb], 0.f);
-            }
-        }
-        if (c == 0) {   // zero the padded channels of gst once per pixel
-            for (int ch = 2 * g.Cb; ch < a.cs_gst; ++ch) stv(&gst[m * a.cs_gst + ch], 0.f);
+            a.gx[idx] = gu;
         }
     }
-    double dsc = block_sum((double)gsc, red);
-    double dss = block_sum((double)gss, red);
-    if (threadIdx.x == 0 && (dsc != 0.0 || dss != 0.0)) {
-        atomicAdd(a.g_scale, (float)dsc);
-        atomicAdd(a.g_scale_shift, (float)dss);
+    const float dsc = block_sum(gsc, redl);   // (barriers also publish gs)
+    const float dss = block_sum(gss, redl);
+    tile_copy_out<T>(gs, t.m0, t.tp, a.cs_gst, a.gst);
+    if (threadIdx.x == 0 && (dsc != 0.f || dss != 0.f)) {
+        atomicAdd(a.g_scale, dsc);
+        atomicAdd(a.g_scale_shift, dss);
     }
 }
 
 // ---------------------------------------------------------------------------
 // in part, backward (through CReLU and in_bn)
 // ---------------------------------------------------------------------------
+// gxa = d/dxa of [relu(xa), relu(-xa)] . [g1, g2]; gh: LDS tile [tp][cs_gh0]
 template <typename T>
-__device__ __forceinline__ void in_bwd_vals(const rnvp_coupling_args& a, const Geo& g, long long b, int cb, int p,
-                                            float sc, float sf, float mean, float rstd, float& gxa, float& xh,
-                                            float& xm) {
+__device__ __forceinline__ void in_bwd_vals(const rnvp_coupling_args& a, const Geo& g, const Tile& t, const T* gh,
+                                            const float* tab, int cb, int pl, float& gxa, float& xh) {
     const int c = (g.kind == 0) ? cb : g.off_base + cb;
-    float v = a.x[(b * g.C + c) * g.HW + p];
+    const int p = t.p0 + pl;
+    float v = a.x[((long long)t.b * g.C + c) * g.HW + p];
     if (g.kind == 0 && !ckbd_m(g, p)) v = 0.f;
-    xm = v;
-    float xa = v * sc + sf;
-    const long long m = b * g.HW + p;
-    const T* gh = cptr<T>(a.gh0);
-    float g1 = ldv(&gh[m * a.cs_gh0 + cb]);
-    float g2 = ldv(&gh[m * a.cs_gh0 + g.Cb + cb]);
+    const float xa = v * tab[cb] + tab[g.Cb + cb];
+    const float g1 = ldv(&gh[pl * a.cs_gh0 + cb]);
+    const float g2 = ldv(&gh[pl * a.cs_gh0 + g.Cb + cb]);
     gxa = (xa > 0.f ? g1 : 0.f) - (xa < 0.f ? g2 : 0.f);
-    xh = (v - mean) * rstd;
-}
-
-__device__ __forceinline__ void in_bn_params(const rnvp_coupling_args& a, const Geo& g, int cb, float& sc, float& sf,
-                                             float& mean, float& rstd) {
-    rnvp_bn_src s;
-    s.shards = 1;
-    s.sums = a.training ? a.in_sums : nullptr;
-    s.count = (double)g.B * g.HW;
-    s.mean = a.in_rmean; s.var = a.in_rvar;
-    s.gamma = a.in_gamma; s.beta = a.in_beta; s.eps = a.eps;
-    bn_affine(s, g.Cb, cb, sc, sf, &mean, &rstd);
+    xh = (v - tab[2 * g.Cb + cb]) * tab[3 * g.Cb + cb];
 }
 
 template <typename T>
-__global__ void k_in_bwd_red(rnvp_coupling_args a) {
-    __shared__ double red[16];
+__global__ __launch_bounds__(256) void k_in_bwd_red(rnvp_coupling_args a, int TP, int seg) {
+    extern __shared__ double dsm[];
     const Geo g = geo(a);
-    const int b = blockIdx.x / g.Cb, cb = blockIdx.x % g.Cb;
-    float sc, sf, mean, rstd;
-    in_bn_params(a, g, cb, sc, sf, mean, rstd);
-    float s1 = 0.f, s2 = 0.f;
-    for (int p = threadIdx.x; p < g.HW; p += blockDim.x) {
-        float gxa, xh, xm;
-        in_bwd_vals<T>(a, g, b, cb, p, sc, sf, mean, rstd, gxa, xh, xm);
-        s1 += gxa;
-        s2 += gxa * xh;
+    const Tile t = tile_of(g, TP);
+    const int lane = threadIdx.x & 63;
+    double* red = dsm;                                   // [2*Cb]
+    float* tab = (float*)(dsm + 2 * g.Cb);               // [4*Cb]
+    T* gh = (T*)(tab + 4 * ((g.Cb + 3) / 4 * 4));        // [tp][cs_gh0]
+    lds_zero(red, 2 * g.Cb);
+    in_bn_table(a, g, tab);
+    tile_copy_in<T>(a.gh0, t.m0, t.tp, a.cs_gh0, gh);
+    __syncthreads();
+    const int total = g.Cb * t.tp;
+    for (int e0 = 0; e0 < total; e0 += blockDim.x) {
+        const int e = e0 + threadIdx.x;
+        const bool ok = e < total;
+        const int cb = ok ? e / t.tp : 0, pl = ok ? e - cb * t.tp : 0;
+        float gxa = 0.f, xh = 0.f;
+        if (ok) in_bwd_vals<T>(a, g, t, gh, tab, cb, pl, gxa, xh);
+        const float s1 = seg_sum(gxa, seg), s2 = seg_sum(gxa * xh, seg);
+        if (ok && (lane & (seg - 1)) == 0) {
+            atomicAdd(&red[cb], (double)s1);
+            atomicAdd(&red[g.Cb + cb], (double)s2);
+        }
     }
-    double d1 = block_sum((double)s1, red);
-    double d2 = block_sum((double)s2, red);
-    if (threadIdx.x == 0) {
-        atomicAdd(&a.in_bwd_sums[cb], d1);
-        atomicAdd(&a.in_bwd_sums[g.Cb + cb], d2);
-    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < 2 * g.Cb; c += blockDim.x) atomicAdd(&a.in_bwd_sums[c], red[c]);
 }
 
 template <typename T>
-__global__ void k_in_bwd_apply(rnvp_coupling_args a) {
+__global__ __launch_bounds__(256) void k_in_bwd_apply(rnvp_coupling_args a, int TP, int seg) {
+    extern __shared__ double dsm[];
     const Geo g = geo(a);
-    const int b = blockIdx.x / g.Cb, cb = blockIdx.x % g.Cb;
-    float sc, sf, mean, rstd;
-    in_bn_params(a, g, cb, sc, sf, mean, rstd);
+    const Tile t = tile_of(g, TP);
+    float* tab = (float*)dsm;                            // sc | sf | mean | rstd | coef | k1 | k2 [Cb each]
+    const int tabn = 8 * ((g.Cb + 3) / 4 * 4);
+    T* gh = (T*)(tab + tabn);
+    in_bn_table(a, g, tab);
     const double cnt = (double)g.B * g.HW;
-    const float gam = a.in_gamma ? a.in_gamma[cb] : 1.f;
-    const float k1 = a.training ? (float)(a.in_bwd_sums[cb] / cnt) : 0.f;
-    const float k2 = a.training ? (float)(a.in_bwd_sums[g.Cb + cb] / cnt) : 0.f;
-    const int c = (g.kind == 0) ? cb : g.off_base + cb;
-    if (blockIdx.x == cb && threadIdx.x == 0) {   // b == 0 block writes the affine grads
-        if (a.g_in_beta) a.g_in_beta[cb] = (float)a.in_bwd_sums[cb];
-        if (a.g_in_gamma) a.g_in_gamma[cb] = (float)a.in_bwd_sums[g.Cb + cb];
+    for (int cb = threadIdx.x; cb < g.Cb; cb += blockDim.x) {
+        const float gam = a.in_gamma ? a.in_gamma[cb] : 1.f;
+        tab[4 * g.Cb + cb] = gam * tab[3 * g.Cb + cb];
+        tab[5 * g.Cb + cb] = a.training ? (float)(a.in_bwd_sums[cb] / cnt) : 0.f;
+        tab[6 * g.Cb + cb] = a.training ? (float)(a.in_bwd_sums[g.Cb + cb] / cnt) : 0.f;
+        if (blockIdx.x == 0) {   // the affine grads, once
+            if (a.g_in_beta) a.g_in_beta[cb] = (float)a.in_bwd_sums[cb];
+            if (a.g_in_gamma) a.g_in_gamma[cb] = (float)a.in_bwd_sums[g.Cb + cb];
+        }
     }
-    for (int p = threadIdx.x; p < g.HW; p += blockDim.x) {
-        float gxa, xh, xm;
-        in_bwd_vals<T>(a, g, b, cb, p, sc, sf, mean, rstd, gxa, xh, xm);
-        float gxm = gam * rstd * (gxa - k1 - xh * k2);
+    tile_copy_in<T>(a.gh0, t.m0, t.tp, a.cs_gh0, gh);
+    __syncthreads();
+    const int total = g.Cb * t.tp;
+    for (int e = threadIdx.x; e < total; e += blockDim.x) {
+        const int cb = e / t.tp, pl = e - cb * t.tp, p = t.p0 + pl;
+        float gxa, xh;
+        in_bwd_vals<T>(a, g, t, gh, tab, cb, pl, gxa, xh);
+        float gxm = tab[4 * g.Cb + cb] * (gxa - tab[5 * g.Cb + cb] - xh * tab[6 * g.Cb + cb]);
         if (g.kind == 0 && !ckbd_m(g, p)) gxm = 0.f;   // xm = x * mask
-        a.gx[((long long)b * g.C + c) * g.HW + p] += gxm;
+        const int c = (g.kind == 0) ? cb : g.off_base + cb;
+        a.gx[((long long)t.b * g.C + c) * g.HW + p] += gxm;
     }
 }
 
@@ -489,6 +583,29 @@ int check(const rnvp_coupling_args* a) {
 
 inline int cb_of(const rnvp_coupling_args* a) { return a->kind == 0 ? a->C : a->C / 2; }
 
+// pixel-tile geometry: TP pixels per workgroup (<= 256, LDS-bounded by the
+// widest NHWC tile), seg = lanes sharing a channel in the reductions
+struct TileCfg {
+    int TP, seg, grid;
+};
+inline TileCfg tile_cfg(const rnvp_coupling_args* a) {
+    const int HW = a->H * a->W;
+    const int esz = a->dtype == RNVP_F32 ? 4 : 2;
+    int cs = a->cs_h0;
+    if (a->cs_st + a->cs_gst > cs) cs = a->cs_st + a->cs_gst;
+    if (a->cs_gh0 > cs) cs = a->cs_gh0;
+    if (cs < 8) cs = 8;
+    TileCfg c;
+    c.TP = HW < 256 ? HW : 256;
+    while (c.TP > 16 && (long long)c.TP * cs * esz > 32 * 1024) c.TP /= 2;
+    int seg = 1;
+    while (seg < 64 && c.TP % (2 * seg) == 0 && HW % (2 * seg) == 0) seg *= 2;
+    c.seg = seg;
+    c.grid = a->B * ((HW + c.TP - 1) / c.TP);
+    return c;
+}
+inline int r4(int x) { return (x + 3) / 4 * 4; }
+
 }  // namespace
 
 extern "C" int rnvp_coupling_in_fwd(const rnvp_coupling_args* a, void* stream) {
@@ -499,14 +616,15 @@ extern "C" int rnvp_coupling_in_fwd(const rnvp_coupling_args* a, void* stream) {
     if (a->cs_h0 < (a->kind == 0 ? 2 * Cb + 1 : 2 * Cb)) return RNVP_E_INVALID;
     if (a->B == 0) return RNVP_OK;
     hipStream_t s = (hipStream_t)stream;
+    const TileCfg tc = tile_cfg(a);
+    const int esz = a->dtype == RNVP_F32 ? 4 : 2;
     if (a->training) {
-        k_in_stats<<<a->B * Cb, 256, 0, s>>>(*a);
+        k_in_stats<<<tc.grid, 256, 16 * Cb, s>>>(*a, tc.TP, tc.seg);
         RNVP_LAUNCH_CHECK();
     }
-    long long n = (long long)a->B * a->H * a->W * a->cs_h0;
-    size_t shm = 2 * Cb * sizeof(float);
-    if (a->dtype == RNVP_F32) k_in_apply<float><<<rnvp_grid(n, 256, 2048), 256, shm, s>>>(*a);
-    else k_in_apply<bf16_t><<<rnvp_grid(n, 256, 2048), 256, shm, s>>>(*a);
+    const size_t shm = 16 * r4(Cb) + (size_t)tc.TP * a->cs_h0 * esz;
+    if (a->dtype == RNVP_F32) k_in_apply<float><<<tc.grid, 256, shm, s>>>(*a, tc.TP, tc.seg);
+    else k_in_apply<bf16_t><<<tc.grid, 256, shm, s>>>(*a, tc.TP, tc.seg);
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
 }
@@ -521,8 +639,11 @@ extern "C" int rnvp_coupling_out_fwd(const rnvp_coupling_args* a, void* stream) 
     if (a->cs_st < 2 * Cb) return RNVP_E_INVALID;
     if (a->B == 0) return RNVP_OK;
     hipStream_t s = (hipStream_t)stream;
-    if (a->dtype == RNVP_F32) k_out1<float><<<a->B * a->C, 256, 0, s>>>(*a);
-    else k_out1<bf16_t><<<a->B * a->C, 256, 0, s>>>(*a);
+    const TileCfg tc = tile_cfg(a);
+    const int esz = a->dtype == RNVP_F32 ? 4 : 2;
+    const size_t shm1 = 16 * ((Cb + 1) / 2 * 2) + (size_t)tc.TP * a->cs_st * esz;
+    if (a->dtype == RNVP_F32) k_out1<float><<<tc.grid, 256, shm1, s>>>(*a, tc.TP, tc.seg);
+    else k_out1<bf16_t><<<tc.grid, 256, shm1, s>>>(*a, tc.TP, tc.seg);
     RNVP_LAUNCH_CHECK();
     long long n = (long long)a->B * a->C * a->H * a->W;
     size_t shm = 3 * Cb * sizeof(float);
@@ -558,12 +679,15 @@ extern "C" int rnvp_coupling_out_bwd(const rnvp_coupling_args* a, void* stream) 
     if (a->coupling_bn && !a->training && (!a->out_rmean || !a->out_rvar)) return RNVP_E_INVALID;
     if (a->B == 0) return RNVP_OK;
     hipStream_t s = (hipStream_t)stream;
+    const TileCfg tc = tile_cfg(a);
+    const int esz = a->dtype == RNVP_F32 ? 4 : 2;
     if (stats) {
-        k_out_bwd_red<<<a->B * Cb, 256, 0, s>>>(*a);
+        k_out_bwd_red<<<tc.grid, 256, 24 * Cb + 8 * Cb, s>>>(*a, tc.TP, tc.seg);
         RNVP_LAUNCH_CHECK();
     }
-    if (a->dtype == RNVP_F32) k_out_bwd_apply<float><<<a->B * a->C, 256, 0, s>>>(*a);
-    else k_out_bwd_apply<bf16_t><<<a->B * a->C, 256, 0, s>>>(*a);
+    const size_t shm = 16 * r4(Cb) + (size_t)tc.TP * (a->cs_st + a->cs_gst) * esz;
+    if (a->dtype == RNVP_F32) k_out_bwd_apply<float><<<tc.grid, 256, shm, s>>>(*a, tc.TP, tc.seg);
+    else k_out_bwd_apply<bf16_t><<<tc.grid, 256, shm, s>>>(*a, tc.TP, tc.seg);
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
 }
@@ -578,14 +702,19 @@ extern "C" int rnvp_coupling_in_bwd(const rnvp_coupling_args* a, void* stream) {
     if (a->cs_gh0 < 2 * Cb) return RNVP_E_INVALID;
     if (a->B == 0) return RNVP_OK;
     hipStream_t s = (hipStream_t)stream;
+    const TileCfg tc = tile_cfg(a);
+    const int esz = a->dtype == RNVP_F32 ? 4 : 2;
+    const size_t gsh = (size_t)tc.TP * a->cs_gh0 * esz;
     if (a->training || a->g_in_gamma || a->g_in_beta) {
         if (!a->in_bwd_sums) return RNVP_E_INVALID;
-        if (a->dtype == RNVP_F32) k_in_bwd_red<float><<<a->B * Cb, 256, 0, s>>>(*a);
-        else k_in_bwd_red<bf16_t><<<a->B * Cb, 256, 0, s>>>(*a);
+        const size_t shm = 16 * Cb + 16 * r4(Cb) + gsh;
+        if (a->dtype == RNVP_F32) k_in_bwd_red<float><<<tc.grid, 256, shm, s>>>(*a, tc.TP, tc.seg);
+        else k_in_bwd_red<bf16_t><<<tc.grid, 256, shm, s>>>(*a, tc.TP, tc.seg);
         RNVP_LAUNCH_CHECK();
     }
-    if (a->dtype == RNVP_F32) k_in_bwd_apply<float><<<a->B * Cb, 256, 0, s>>>(*a);
-    else k_in_bwd_apply<bf16_t><<<a->B * Cb, 256, 0, s>>>(*a);
+    const size_t shm = 32 * r4(Cb) + gsh;
+    if (a->dtype == RNVP_F32) k_in_bwd_apply<float><<<tc.grid, 256, shm, s>>>(*a, tc.TP, tc.seg);
+    else k_in_bwd_apply<bf16_t><<<tc.grid, 256, shm, s>>>(*a, tc.TP, tc.seg);
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
 }

@@ -69,7 +69,8 @@ WGRAD_GROUP_MAX = 24
 class WgradConv(C.Structure):
     _fields_ = [("x", vp), ("dy", vp), ("ws", vp), ("wsb", vp), ("pro", BNSrc),
                 ("cs_in", i32), ("cin", i32), ("ks", i32), ("cs_dy", i32), ("n", i32), ("kp", i32),
-                ("pro_bn_relu", i32), ("nz", i32), ("m_per_slab", i64), ("task0", i32), ("tk", i32)]
+                ("pro_bn_relu", i32), ("nz", i32), ("nrep", i32), ("m_per_slab", i64), ("task0", i32),
+                ("tk", i32)]
 
 
 class WgradGroup(C.Structure):
@@ -118,6 +119,7 @@ _SIGS = {
     "rnvp_conv2d": (i32, [C.POINTER(ConvArgs), vp]),
     "rnvp_conv2d_wgrad": (i32, [C.POINTER(WgradArgs), vp]),
     "rnvp_wgrad_slabs": (i32, [i64]),
+    "rnvp_wgrad_replicas": (i32, [i32]),
     "rnvp_conv2d_wgrad_grouped": (i32, [C.POINTER(WgradGroup), vp]),
     "rnvp_bn_bwd_apply": (i32, [C.POINTER(BNBwdArgs), vp]),
     "rnvp_weight_norm_fwd": (i32, [vp, i32, i32, i32, i32, vp]),
@@ -145,7 +147,7 @@ class _Lib:
             fn = getattr(self.dll, name)
             fn.restype = res
             fn.argtypes = args
-            raw = name in ("rnvp_version", "rnvp_stat_shards", "rnvp_wgrad_slabs") or res is not i32
+            raw = name in ("rnvp_version", "rnvp_stat_shards", "rnvp_wgrad_slabs", "rnvp_wgrad_replicas") or res is not i32
             setattr(self, name[len("rnvp_"):], fn if raw else self._wrap(name, fn))
 
     def _wrap(self, name, fn):

@@ -117,12 +117,13 @@ _WGRAD_WS = {}
 
 
 def wgrad_workspace(device, elems):
-    """Per-device fp32 workspace for the grouped weight-gradient partial slabs
-    (one coupling's backward at a time, all on the caller's stream)."""
+    """Per-device fp32 workspace for the grouped weight-gradient partial sums
+    (one coupling's backward at a time, all on the caller's stream).  Zero
+    between uses: the weight-norm backward re-zeroes what it consumed."""
     key = str(device)
     t = _WGRAD_WS.get(key)
     if t is None or t.numel() < elems:
-        t = torch.empty(max(elems, 1 << 16), dtype=torch.float32, device=device)
+        t = torch.zeros(max(elems, 1 << 16), dtype=torch.float32, device=device)
         _WGRAD_WS[key] = t
     return t
 
@@ -270,18 +271,19 @@ class CouplingEngine:
         cmax = max([chan_stride(s.cin) for s in self.P.convs.values()])
         ar.add("gtmp", M * cmax * esz)
         ar.alloc(device)
-        # grouped weight-gradient partial slabs: [nz][cout][kp_f] (+ bias [nz][cout])
+        # grouped weight-gradient partial sums: [nrep][cout][kp_f] (+ bias [nrep][cout])
         nz = int(_lib.lib().wgrad_slabs(M))
+        nrep = int(_lib.lib().wgrad_replicas(nz))
         wg = {}
         off = 0
         for name, spec in self.P.convs.items():
             kp_f = wsz["geo"][name][2]
             ow = off
-            off += nz * spec.cout * kp_f
+            off += nrep * spec.cout * kp_f
             ob = None
             if spec.bias:
                 ob = off
-                off += nz * spec.cout
+                off += nrep * spec.cout
             wg[name] = (ow, ob)
             off = round_up(off, 64)
         wgws = wgrad_workspace(device, off)
@@ -293,7 +295,7 @@ class CouplingEngine:
             C.memmove(C.addressof(e), C.addressof(d), C.sizeof(WNDesc))
             ow, ob = wg[name]
             e.dw = wbase + 4 * ow
-            e.nz = nz
+            e.nz = nrep
             _, _, bname = self._conv_names(spec)
             e.dbp = wbase + 4 * ob if ob is not None else None
             e.db_off = self.layout[bname][0] if ob is not None else 0
@@ -304,7 +306,7 @@ class CouplingEngine:
         sc = dict(arena=ar, zero=zr, wn_table=torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(device),
                   wn_key=wsz["key"], wn_rows=wsz["rows"], n_wn=len(descs), shards=sh,
                   ws=splitk_workspace(device, wse) if wse else None, ws_elems=wse,
-                  wg=wg, wg_nz=nz, wg_ws=wgws)
+                  wg=wg, wg_nz=nz, wg_nrep=nrep, wg_ws=wgws)
         self._scratch[key] = sc
         return sc
 
@@ -526,10 +528,10 @@ class CouplingEngine:
                     c.pro_bn_relu = 1
                     c.pro = self._bn(T, op.pro_bn, training, ar.ptr("s:" + op.pro_bn), M)
                 c.dy, c.cs_dy, c.n = sar.ptr(st.gy), cs_out, spec.cout
-                c.ws, c.kp, c.nz = wbase + 4 * ow, kp_f, sc["wg_nz"]
+                c.ws, c.kp, c.nz, c.nrep = wbase + 4 * ow, kp_f, sc["wg_nz"], sc["wg_nrep"]
                 c.wsb = wbase + 4 * ob if ob is not None else None
                 esz = DTYPES[dtype][1]
-                wg_bytes += esz * (M * cs_in + M * cs_out) + 4 * sc["wg_nz"] * spec.cout * kp_f
+                wg_bytes += esz * (M * cs_in + M * cs_out) + 4 * sc["wg_nz"] * spec.cout * spec.ks * spec.ks * cs_in
                 wg_flops += 2.0 * M * spec.cout * spec.ks * spec.ks * spec.cin
         if grp.n_conv:
             _launch("conv_wgrad", wg_bytes, wg_flops, L.conv2d_wgrad_grouped, C.byref(grp), s)

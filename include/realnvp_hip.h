@@ -138,19 +138,21 @@ int rnvp_conv2d_wgrad(const rnvp_wgrad_args* a, void* stream);
 /* grouped weight gradient: the wgrads of every conv of one coupling's s/t
  * network in ONE launch (they are independent of each other once the
  * coupling's data-gradient chain has run).  Conv c's pixel range is cut into
- * nz slabs; a workgroup owns one [64 n] x [64 k] tile of one slab and stores
- * its fp32 partial to ws[z][n][kp] (plain stores, no atomics, deterministic);
- * the bias partial of k tile 0 goes to wsb[z][n].  The weight-norm backward
- * (rnvp_weight_norm_bwd with nz slabs) sums the partials.  The library fills
- * m_per_slab / task0 / tk.  Replaces the per-conv backward of
- * WeightNormConv2d (modules_realnvp.py:53-59) for the whole ResidualModule. */
+ * nz slabs; a workgroup owns one [64 n] x [64 k] tile of one slab and adds
+ * its fp32 partial into replica z % nrep of ws[nrep][n][kp] (fp32 atomics,
+ * <= nz/nrep adders per word; plain stores when nrep == nz); the bias partial
+ * of k tile 0 goes to wsb[nrep][n] the same way.  ws / wsb must be zero on
+ * entry; the weight-norm backward (rnvp_weight_norm_bwd, nz = nrep) sums the
+ * replicas and zeroes them again.  The library fills m_per_slab / task0 / tk.
+ * Replaces the per-conv backward of WeightNormConv2d (modules_realnvp.py:53-59)
+ * for the whole ResidualModule. */
 #define RNVP_WGRAD_GROUP_MAX 24
 typedef struct rnvp_wgrad_conv {
     const void* x; const void* dy;
-    float* ws;                          /* [nz][n][kp] fp32 partials */
-    float* wsb;                         /* [nz][n] bias partials or NULL */
+    float* ws;                          /* [nrep][n][kp] fp32 partial sums */
+    float* wsb;                         /* [nrep][n] bias partial sums or NULL */
     rnvp_bn_src pro;
-    int cs_in, cin, ks, cs_dy, n, kp, pro_bn_relu, nz;
+    int cs_in, cin, ks, cs_dy, n, kp, pro_bn_relu, nz, nrep;
     long long m_per_slab;               /* filled by the library */
     int task0, tk;                      /* filled by the library */
 } rnvp_wgrad_conv;
@@ -158,8 +160,10 @@ typedef struct rnvp_wgrad_group {
     int dtype, B, H, W, n_conv;
     rnvp_wgrad_conv conv[RNVP_WGRAD_GROUP_MAX];
 } rnvp_wgrad_group;
-/* slab count the grouped wgrad uses for a conv over M pixels (size ws with it) */
+/* slab count the grouped wgrad uses for a conv over M pixels, and the
+ * replica count (size ws with the latter) */
 int rnvp_wgrad_slabs(long long M);
+int rnvp_wgrad_replicas(int nz);
 int rnvp_conv2d_wgrad_grouped(const rnvp_wgrad_group* g, void* stream);
 
 /* batch-norm backward apply (train mode), the second half of BN backward:
@@ -184,13 +188,14 @@ int rnvp_bn_bwd_apply(const rnvp_bn_bwd_args* a, void* stream);
 typedef struct rnvp_wn_desc {
     const float* v; const float* g;
     void* wf; void* wd; float* norm;
-    const float* dw;                   /* packed [nz][cout][kp_f] fp32 (bwd), summed over nz */
+    float* dw;                         /* packed [nz][cout][kp_f] fp32 (bwd), summed over nz,
+                                          zeroed after use */
     long long dv_off; long long dg_off;
     int cout, cin, ks, cs_in, kp_f, cs_out, kp_d;
     int row0;                          /* first global row (prefix sum of cout) */
     int col0;                          /* first global wd row (prefix sum of cin) */
     int nz;                            /* dw partial slabs (>= 1) */
-    const float* dbp;                  /* bias partials [nz][cout] or NULL */
+    float* dbp;                        /* bias partials [nz][cout] or NULL, zeroed after use */
     long long db_off;                  /* bias gradient offset (elements) */
 } rnvp_wn_desc;
 /* fwd: one launch over the rows (norm + wf) and one over the wd rows
