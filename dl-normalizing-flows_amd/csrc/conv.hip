@@ -131,7 +131,8 @@ __global__ __launch_bounds__(256) void k_conv(rnvp_conv_args a, int kt_per_split
     const T* __restrict__ X = (const T*)a.x;
     const T* __restrict__ Wt = (const T*)a.w;
     const bool pro = a.pro_bn_relu != 0;
-    const bool epi_bn = !PARTIAL && a.epi_relu_bn_bwd;
+    const bool epi_bn = a.epi_relu_bn_bwd != 0;
+    const bool handoff = PARTIAL && a.tile_counters != nullptr;
 
     double* tmp = dsm;
     float* bnp = (float*)(dsm + 2 * max(cs, BN));   // prologue scale [cs] | shift [cs]
@@ -219,9 +220,9 @@ __global__ __launch_bounds__(256) void k_conv(rnvp_conv_args a, int kt_per_split
     // the first stage's loads are in flight while the BN tables are built
     if (kt0 < kt1) gload(kt0);
     if (pro) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + cs, nullptr, nullptr, tmp);
-    if (epi_bn) block_bn_table(a.epi, N, n0, BN, etab, etab + BN, etab + 2 * BN, etab + 3 * BN, tmp);
-    if (!PARTIAL)
-        for (int c = tid; c < BN; c += 256) btab[c] = (a.bias && n0 + c < N) ? a.bias[n0 + c] : 0.f;
+    if (epi_bn && (!PARTIAL || handoff))
+        block_bn_table(a.epi, N, n0, BN, etab, etab + BN, etab + 2 * BN, etab + 3 * BN, tmp);
+    for (int c = tid; c < BN; c += 256) btab[c] = (a.bias && n0 + c < N) ? a.bias[n0 + c] : 0.f;
     __syncthreads();   // bnp / etab / btab ready
     if (kt0 < kt1) lstore(0);
     __syncthreads();
@@ -260,8 +261,46 @@ __global__ __launch_bounds__(256) void k_conv(rnvp_conv_args a, int kt_per_split
                 if (n < cso) *(floatx4*)(ws + m * cso + n) = acc[i][j];
             }
         }
-        return;
-    } else {
+        if (!handoff) return;
+        // In-launch hand-off: the tile's last split to arrive sums the other
+        // slabs and runs the epilogue (agent-scope release -> counter ->
+        // acquire; the counter is reset for the next launch).
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        int* flag = (int*)red;
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            unsigned int* cnt = a.tile_counters + (blockIdx.y * gridDim.x + blockIdx.x);
+            const unsigned int old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int last = old == gridDim.z - 1;
+            if (last) {
+                __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            flag[0] = last;
+        }
+        __syncthreads();
+        const int last = flag[0];
+        __syncthreads();   // flag read by all before red is reused below
+        if (!last) return;
+        for (int z = 0; z < (int)gridDim.z; ++z) {
+            if (z == (int)blockIdx.z) continue;
+            const float* wz = a.ws + (long long)z * M * cso;
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const long long m = m0 + wm * WTM + i * 16 + li;
+                if (m >= M) continue;
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int n = n0 + wn * WTN + j * 16 + 4 * g;
+                    if (n < cso) acc[i][j] += *(const floatx4*)(wz + m * cso + n);
+                }
+            }
+        }
+    }
+    {
         // ---- fused epilogue (4 channels of one pixel per lane) ----
         const bool want_sums = a.out_sums || (a.epi_relu_bn_bwd && a.epi_sums);
         float s1[TN][4], s2[TN][4];
@@ -609,7 +648,14 @@ int launch_conv(const rnvp_conv_args* a, hipStream_t s) {
         const int kps = (nk + splits - 1) / splits;
         splits = (nk + kps - 1) / kps;
         dim3 g1((unsigned)gm, (unsigned)gn, (unsigned)splits);
-        k_conv<T, BM, BN, WM, WN, true><<<g1, 256, shm, s>>>(*a, kps, shards);
+        if (a->tile_counters && gm * gn <= a->n_counters) {   // in-launch reduction
+            k_conv<T, BM, BN, WM, WN, true><<<g1, 256, shm, s>>>(*a, kps, shards);
+            RNVP_LAUNCH_CHECK();
+            return RNVP_OK;
+        }
+        rnvp_conv_args b = *a;
+        b.tile_counters = nullptr;
+        k_conv<T, BM, BN, WM, WN, true><<<g1, 256, shm, s>>>(b, kps, shards);
         RNVP_LAUNCH_CHECK();
         dim3 g2((unsigned)((M + 15) / 16), (unsigned)((a->cs_out + 63) / 64));
         k_splitk_epi<T><<<g2, 256, 0, s>>>(*a, splits, shards);
@@ -1120,14 +1166,17 @@ __global__ void k_wn_bwd(const rnvp_wn_desc* __restrict__ descs, int n_desc, flo
         for (int z = threadIdx.x; z < nz; z += blockDim.x) bs += d.dbp[(long long)z * d.cout + co];
         bs = block_sum(bs, (float*)red);
         if (threadIdx.x == 0) gbase[d.db_off + co] = bs;
-        __syncthreads();
-        for (int z = threadIdx.x; z < nz; z += blockDim.x) d.dbp[(long long)z * d.cout + co] = 0.f;
+        if (d.zero_after) {
+            __syncthreads();
+            for (int z = threadIdx.x; z < nz; z += blockDim.x) d.dbp[(long long)z * d.cout + co] = 0.f;
+        }
     }
-    // leave the partial-sum replicas zero for the next grouped wgrad
-    __syncthreads();
-    const int K = kk * d.cs_in;
-    for (int z = 0; z < nz; ++z)
-        for (int k = threadIdx.x; k < K; k += blockDim.x) dwz[z * zs + k] = 0.f;
+    if (d.zero_after) {   // leave the replicas zero for the next atomic accumulation
+        __syncthreads();
+        const int K = kk * d.cs_in;
+        for (int z = 0; z < nz; ++z)
+            for (int k = threadIdx.x; k < K; k += blockDim.x) dwz[z * zs + k] = 0.f;
+    }
 }
 
 inline bool al16(const void* p) { return (((uintptr_t)p) & 15) == 0; }

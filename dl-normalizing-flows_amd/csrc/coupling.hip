@@ -100,11 +100,23 @@ __device__ __forceinline__ void lds_zero(double* p, int n) {
     for (int i = threadIdx.x; i < n; i += blockDim.x) p[i] = 0.0;
 }
 
+// coupling reductions: [RNVP_COUPLING_SHARDS][k*Cb] fp64, this block's shard
+__device__ __forceinline__ double* cshard(double* sums, int width) {
+    return sums + (long long)(blockIdx.x % RNVP_COUPLING_SHARDS) * width;
+}
+// sum over the shards of entry i of a [shards][width] reduction
+__device__ __forceinline__ double csum(const double* sums, int width, int i) {
+    double t = 0.0;
+#pragma unroll 8
+    for (int h = 0; h < RNVP_COUPLING_SHARDS; ++h) t += sums[(long long)h * width + i];
+    return t;
+}
+
 // per-channel in_bn table of the in part: scale, shift, mean, rstd [Cb each]
 __device__ __forceinline__ void in_bn_table(const rnvp_coupling_args& a, const Geo& g, float* t) {
     for (int cb = threadIdx.x; cb < g.Cb; cb += blockDim.x) {
         rnvp_bn_src s;
-        s.shards = 1;
+        s.shards = RNVP_COUPLING_SHARDS;
         s.sums = a.training ? a.in_sums : nullptr;
         s.count = (double)g.B * g.HW;
         s.mean = a.in_rmean; s.var = a.in_rvar;
@@ -144,7 +156,8 @@ __global__ __launch_bounds__(256) void k_in_stats(rnvp_coupling_args a, int TP, 
         }
     }
     __syncthreads();
-    for (int c = threadIdx.x; c < 2 * g.Cb; c += blockDim.x) atomicAdd(&a.in_sums[c], red[c]);
+    double* dst = cshard(a.in_sums, 2 * g.Cb);
+    for (int c = threadIdx.x; c < 2 * g.Cb; c += blockDim.x) atomicAdd(&dst[c], red[c]);
 }
 
 // h0[m][ch] NHWC: relu(xa), relu(-xa) [, mask], zero pad; built in LDS, stored
@@ -161,8 +174,8 @@ __global__ __launch_bounds__(256) void k_in_apply(rnvp_coupling_args a, int TP, 
     if (blockIdx.x == 0 && a.training && a.in_rmean) {
         const double cnt = (double)g.B * g.HW;
         for (int c = threadIdx.x; c < g.Cb; c += blockDim.x) {
-            double mean = a.in_sums[c] / cnt;
-            double var = a.in_sums[g.Cb + c] / cnt - mean * mean;
+            double mean = csum(a.in_sums, 2 * g.Cb, c) / cnt;
+            double var = csum(a.in_sums, 2 * g.Cb, g.Cb + c) / cnt - mean * mean;
             if (var < 0) var = 0;
             double unb = cnt > 1 ? var * cnt / (cnt - 1) : var;
             a.in_rmean[c] = (1.f - a.momentum) * a.in_rmean[c] + a.momentum * (float)mean;
@@ -239,8 +252,10 @@ __global__ __launch_bounds__(256) void k_out1(rnvp_coupling_args a, int TP, int 
     }
     const float dl = block_sum(sl, redl);   // (barriers also publish red)
     if (threadIdx.x == 0 && dl != 0.f) atomicAdd(&a.ldj_sample[t.b], dl);
-    if (a.out_sums)
-        for (int c = threadIdx.x; c < 2 * g.Cb; c += blockDim.x) atomicAdd(&a.out_sums[c], red[c]);
+    if (a.out_sums) {
+        double* dst = cshard(a.out_sums, 2 * g.Cb);
+        for (int c = threadIdx.x; c < 2 * g.Cb; c += blockDim.x) atomicAdd(&dst[c], red[c]);
+    }
 }
 
 // z = out_bn(u) on transformed positions; ldj var term; running stats.
@@ -253,8 +268,8 @@ __global__ void k_out2(rnvp_coupling_args a) {
         double mean = 0, var = 1;
         if (a.coupling_bn) {
             if (a.training) {
-                mean = a.out_sums[cb] / cnt;
-                var = a.out_sums[g.Cb + cb] / cnt - mean * mean;
+                mean = csum(a.out_sums, 2 * g.Cb, cb) / cnt;
+                var = csum(a.out_sums, 2 * g.Cb, g.Cb + cb) / cnt - mean * mean;
                 if (var < 0) var = 0;
             } else {
                 mean = a.out_rmean[cb];
@@ -367,8 +382,8 @@ __device__ __forceinline__ void out_bn_stats(const rnvp_coupling_args& a, const 
     const double cnt = (double)g.B * g.HW;
     double mean, var;
     if (a.training) {
-        mean = a.out_sums[cb] / cnt;
-        var = a.out_sums[g.Cb + cb] / cnt - mean * mean;
+        mean = csum(a.out_sums, 2 * g.Cb, cb) / cnt;
+        var = csum(a.out_sums, 2 * g.Cb, g.Cb + cb) / cnt - mean * mean;
         if (var < 0) var = 0;
     } else {
         mean = a.out_rmean[cb];
@@ -414,7 +429,8 @@ __global__ __launch_bounds__(256) void k_out_bwd_red(rnvp_coupling_args a, int T
         }
     }
     __syncthreads();
-    for (int c = threadIdx.x; c < 3 * g.Cb; c += blockDim.x) atomicAdd(&a.bwd_sums[c], red[c]);
+    double* dst = cshard(a.bwd_sums, 3 * g.Cb);
+    for (int c = threadIdx.x; c < 3 * g.Cb; c += blockDim.x) atomicAdd(&dst[c], red[c]);
 }
 
 // gx (direct part), gst = [g_shift | g_r] (built in LDS, stored as one
@@ -435,8 +451,8 @@ __global__ __launch_bounds__(256) void k_out_bwd_apply(rnvp_coupling_args a, int
         if (a.coupling_bn) {
             out_bn_stats(a, g, cb, fm, rstd);
             if (a.training) {
-                kA = (float)(a.bwd_sums[cb] / cnt);
-                kB = (float)((a.bwd_sums[g.Cb + cb] + a.bwd_sums[2 * g.Cb + cb]) / cnt);
+                kA = (float)(csum(a.bwd_sums, 3 * g.Cb, cb) / cnt);
+                kB = (float)((csum(a.bwd_sums, 3 * g.Cb, g.Cb + cb) + csum(a.bwd_sums, 3 * g.Cb, 2 * g.Cb + cb)) / cnt);
             }
         }
         tab[cb] = fm; tab[g.Cb + cb] = rstd; tab[2 * g.Cb + cb] = kA; tab[3 * g.Cb + cb] = kB;
@@ -536,7 +552,8 @@ __global__ __launch_bounds__(256) void k_in_bwd_red(rnvp_coupling_args a, int TP
         }
     }
     __syncthreads();
-    for (int c = threadIdx.x; c < 2 * g.Cb; c += blockDim.x) atomicAdd(&a.in_bwd_sums[c], red[c]);
+    double* dst = cshard(a.in_bwd_sums, 2 * g.Cb);
+    for (int c = threadIdx.x; c < 2 * g.Cb; c += blockDim.x) atomicAdd(&dst[c], red[c]);
 }
 
 template <typename T>
@@ -552,11 +569,13 @@ __global__ __launch_bounds__(256) void k_in_bwd_apply(rnvp_coupling_args a, int 
     for (int cb = threadIdx.x; cb < g.Cb; cb += blockDim.x) {
         const float gam = a.in_gamma ? a.in_gamma[cb] : 1.f;
         tab[4 * g.Cb + cb] = gam * tab[3 * g.Cb + cb];
-        tab[5 * g.Cb + cb] = a.training ? (float)(a.in_bwd_sums[cb] / cnt) : 0.f;
-        tab[6 * g.Cb + cb] = a.training ? (float)(a.in_bwd_sums[g.Cb + cb] / cnt) : 0.f;
+        const double s1 = a.in_bwd_sums ? csum(a.in_bwd_sums, 2 * g.Cb, cb) : 0.0;
+        const double s2 = a.in_bwd_sums ? csum(a.in_bwd_sums, 2 * g.Cb, g.Cb + cb) : 0.0;
+        tab[5 * g.Cb + cb] = a.training ? (float)(s1 / cnt) : 0.f;
+        tab[6 * g.Cb + cb] = a.training ? (float)(s2 / cnt) : 0.f;
         if (blockIdx.x == 0) {   // the affine grads, once
-            if (a.g_in_beta) a.g_in_beta[cb] = (float)a.in_bwd_sums[cb];
-            if (a.g_in_gamma) a.g_in_gamma[cb] = (float)a.in_bwd_sums[g.Cb + cb];
+            if (a.g_in_beta) a.g_in_beta[cb] = (float)s1;
+            if (a.g_in_gamma) a.g_in_gamma[cb] = (float)s2;
         }
     }
     tile_copy_in<T>(a.gh0, t.m0, t.tp, a.cs_gh0, gh);
@@ -596,8 +615,11 @@ inline TileCfg tile_cfg(const rnvp_coupling_args* a) {
     if (a->cs_gh0 > cs) cs = a->cs_gh0;
     if (cs < 8) cs = 8;
     TileCfg c;
+    // largest power-of-2-ish tile (<= 256 px) that still gives >= 512
+    // workgroups (each thread then touches <= ~3 elements per pass)
     c.TP = HW < 256 ? HW : 256;
     while (c.TP > 16 && (long long)c.TP * cs * esz > 32 * 1024) c.TP /= 2;
+    while (c.TP > 4 && c.TP % 2 == 0 && (long long)a->B * ((HW + c.TP - 1) / c.TP) < 512) c.TP /= 2;
     int seg = 1;
     while (seg < 64 && c.TP % (2 * seg) == 0 && HW % (2 * seg) == 0) seg *= 2;
     c.seg = seg;

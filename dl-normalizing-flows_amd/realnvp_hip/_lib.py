@@ -37,7 +37,7 @@ class ConvArgs(C.Structure):
                 ("pro_bn_relu", i32), ("pro", BNSrc),
                 ("out_sums", vp),
                 ("epi_relu_bn_bwd", i32), ("epi_x", vp), ("epi", BNSrc), ("epi_sums", vp),
-                ("ws", vp), ("ws_elems", i64)]
+                ("ws", vp), ("ws_elems", i64), ("tile_counters", vp), ("n_counters", i32)]
 
 
 class WgradArgs(C.Structure):
@@ -60,7 +60,7 @@ class WNDesc(C.Structure):
                 ("dw", vp), ("dv_off", i64), ("dg_off", i64),
                 ("cout", i32), ("cin", i32), ("ks", i32), ("cs_in", i32), ("kp_f", i32),
                 ("cs_out", i32), ("kp_d", i32), ("row0", i32), ("col0", i32),
-                ("nz", i32), ("dbp", vp), ("db_off", i64)]
+                ("nz", i32), ("dbp", vp), ("db_off", i64), ("zero_after", i32)]
 
 
 WGRAD_GROUP_MAX = 24

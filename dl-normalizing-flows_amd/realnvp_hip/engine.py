@@ -23,6 +23,7 @@ from ._lib import (BNBwdArgs, BNRunning, BNSrc, ConvArgs, CouplingArgs, WgradCon
 from .net import backward_program, build_program, chan_stride, round_up
 
 BN_EPS = 1e-5
+COUPLING_SHARDS = 32      # RNVP_COUPLING_SHARDS (include/realnvp_hip.h)
 BN_MOMENTUM = 0.1
 
 DTYPES = {"fp32": (RNVP_F32, 4, torch.float32), "bf16": (RNVP_BF16, 2, torch.bfloat16)}
@@ -109,23 +110,23 @@ def splitk_workspace(device, elems):
     return t
 
 
+_COUNTERS = {}
+N_COUNTERS = 1 << 16
+
+
+def tile_counters(device):
+    """Per-device zeroed uint32 hand-off counters of the in-launch split-K
+    reduction (every use leaves them zero)."""
+    key = str(device)
+    t = _COUNTERS.get(key)
+    if t is None:
+        t = torch.zeros(N_COUNTERS, dtype=torch.int32, device=device)
+        _COUNTERS[key] = t
+    return t
+
+
 def splitk_elems(M, nmax):
     return 8 * M * nmax if M <= 16384 else 0
-
-
-_WGRAD_WS = {}
-
-
-def wgrad_workspace(device, elems):
-    """Per-device fp32 workspace for the grouped weight-gradient partial sums
-    (one coupling's backward at a time, all on the caller's stream).  Zero
-    between uses: the weight-norm backward re-zeroes what it consumed."""
-    key = str(device)
-    t = _WGRAD_WS.get(key)
-    if t is None or t.numel() < elems:
-        t = torch.zeros(max(elems, 1 << 16), dtype=torch.float32, device=device)
-        _WGRAD_WS[key] = t
-    return t
 
 
 class CouplingEngine:
@@ -227,8 +228,8 @@ class CouplingEngine:
             if b != "h0":
                 ar.add(b, M * chan_stride(ch) * esz)
         ar.add("u", B * self.C * H * W * 4)
-        ar.add("in_sums", 2 * self.Cb * 8)
-        ar.add("out_sums", 2 * self.Cb * 8)
+        ar.add("in_sums", COUPLING_SHARDS * 2 * self.Cb * 8)
+        ar.add("out_sums", COUPLING_SHARDS * 2 * self.Cb * 8)
         sh = stat_shards(M)
         for bn, spec in self.P.bns.items():
             ar.add("s:" + bn, sh * 2 * spec.c * 8)
@@ -258,8 +259,8 @@ class CouplingEngine:
         ar = Arena()
         # zeroed every backward: the reductions (kept contiguous)
         wsz = self.weights(dtype)
-        ar.add("bwd_sums", 3 * self.Cb * 8)
-        ar.add("in_bwd_sums", 2 * self.Cb * 8)
+        ar.add("bwd_sums", COUPLING_SHARDS * 3 * self.Cb * 8)
+        ar.add("in_bwd_sums", COUPLING_SHARDS * 2 * self.Cb * 8)
         first, last = "bwd_sums", "in_bwd_sums"
         sh = stat_shards(M)
         for bn, spec in self.P.bns.items():
@@ -286,7 +287,9 @@ class CouplingEngine:
                 off += nrep * spec.cout
             wg[name] = (ow, ob)
             off = round_up(off, 64)
-        wgws = wgrad_workspace(device, off)
+        # per-coupling (zeroed once): replica regions are re-zeroed by the
+        # weight-norm backward, plain-store regions are fully overwritten
+        wgws = torch.zeros(max(off, 64), dtype=torch.float32, device=device)
         wbase = wgws.data_ptr()
         # weight-norm backward table (sums the slabs, writes dv / dg / dbias)
         descs = []
@@ -299,6 +302,7 @@ class CouplingEngine:
             _, _, bname = self._conv_names(spec)
             e.dbp = wbase + 4 * ob if ob is not None else None
             e.db_off = self.layout[bname][0] if ob is not None else 0
+            e.zero_after = int(nrep < nz)
             descs.append(e)
         tab = (WNDesc * len(descs))(*descs)
         nmax = max(max(chan_stride(s.cin), chan_stride(s.cout)) for s in self.P.convs.values())
@@ -306,7 +310,7 @@ class CouplingEngine:
         sc = dict(arena=ar, zero=zr, wn_table=torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(device),
                   wn_key=wsz["key"], wn_rows=wsz["rows"], n_wn=len(descs), shards=sh,
                   ws=splitk_workspace(device, wse) if wse else None, ws_elems=wse,
-                  wg=wg, wg_nz=nz, wg_nrep=nrep, wg_ws=wgws)
+                  wg=wg, wg_nz=nz, wg_nrep=nrep, wg_ws=wgws, counters=tile_counters(device))
         self._scratch[key] = sc
         return sc
 

@@ -119,6 +119,10 @@ typedef struct rnvp_conv_args {
     double* out_sums;
     int epi_relu_bn_bwd; const void* epi_x; rnvp_bn_src epi; double* epi_sums;
     float* ws; long long ws_elems;      /* split-K workspace (optional) */
+    unsigned int* tile_counters;        /* split-K hand-off counters, zero on entry and left
+                                           zero (optional: without them a separate reduce
+                                           launch runs the epilogue) */
+    int n_counters;
 } rnvp_conv_args;
 int rnvp_conv2d(const rnvp_conv_args* a, void* stream);
 
@@ -143,7 +147,7 @@ int rnvp_conv2d_wgrad(const rnvp_wgrad_args* a, void* stream);
  * <= nz/nrep adders per word; plain stores when nrep == nz); the bias partial
  * of k tile 0 goes to wsb[nrep][n] the same way.  ws / wsb must be zero on
  * entry; the weight-norm backward (rnvp_weight_norm_bwd, nz = nrep) sums the
- * replicas and zeroes them again.  The library fills m_per_slab / task0 / tk.
+ * replicas (and re-zeroes them when zero_after).  The library fills m_per_slab / task0 / tk.
  * Replaces the per-conv backward of WeightNormConv2d (modules_realnvp.py:53-59)
  * for the whole ResidualModule. */
 #define RNVP_WGRAD_GROUP_MAX 24
@@ -184,19 +188,20 @@ int rnvp_bn_bwd_apply(const rnvp_bn_bwd_args* a, void* stream);
  * (w[co][ci][ks-1-ky'][ks-1-kx']).  g == NULL means a plain conv (w = v).
  * bwd: dv = (g/|v|)(dw - (v.dw/|v|^2) v), dg = v.dw/|v| from the packed dw
  * (sum of nz slabs), written at grad_base + dv_off / dg_off (elements;
- * dg_off < 0 = frozen g); dbias = sum of the nz bias partials at db_off. */
+ * dg_off < 0 = frozen g); dbias = sum of the nz bias partials at db_off;
+ * zero_after: leave the slabs zero for the next atomic accumulation. */
 typedef struct rnvp_wn_desc {
     const float* v; const float* g;
     void* wf; void* wd; float* norm;
-    float* dw;                         /* packed [nz][cout][kp_f] fp32 (bwd), summed over nz,
-                                          zeroed after use */
+    float* dw;                         /* packed [nz][cout][kp_f] fp32 (bwd), summed over nz */
     long long dv_off; long long dg_off;
     int cout, cin, ks, cs_in, kp_f, cs_out, kp_d;
     int row0;                          /* first global row (prefix sum of cout) */
     int col0;                          /* first global wd row (prefix sum of cin) */
     int nz;                            /* dw partial slabs (>= 1) */
-    float* dbp;                        /* bias partials [nz][cout] or NULL, zeroed after use */
+    float* dbp;                        /* bias partials [nz][cout] or NULL */
     long long db_off;                  /* bias gradient offset (elements) */
+    int zero_after;                    /* re-zero dw / dbp after use (atomic accumulation) */
 } rnvp_wn_desc;
 /* fwd: one launch over the rows (norm + wf) and one over the wd rows
  * (total_cols = sum of cin), for any number of convs (a whole model). */
@@ -210,19 +215,22 @@ int rnvp_weight_norm_bwd(const rnvp_wn_desc* descs_device, int n_desc, int total
  * Net input h0 = relu(cat(bn_in(xm), -bn_in(xm)[, mask])) with xm = x*mask
  * (ckbd, 2C+1 channels) or the "off" half (chan, C channels).  Net output
  * st = [shift | log_rescale] (2*Cb channels). */
+/* the coupling's per-channel fp64 reductions are spread over this many
+ * shards (workgroup % shards) so no word takes more than ~32 atomic adders */
+#define RNVP_COUPLING_SHARDS 32
 typedef struct rnvp_coupling_args {
     int kind, B, C, H, W, mask_config, coupling_bn, training, dtype;
     float momentum, eps;
     const float* x;                       /* coupling input (reverse: the output) */
     const float* in_gamma; const float* in_beta;
     float* in_rmean; float* in_rvar; long long* in_nbt;
-    double* in_sums;                      /* [2*Cb] */
+    double* in_sums;                      /* [RNVP_COUPLING_SHARDS][2*Cb] */
     void* h0; int cs_h0;
     const void* st; int cs_st;
     const float* scale; const float* scale_shift;
     float* u;                             /* pre-out_bn value, [B,C,H,W] */
     float* z;                             /* output [B,C,H,W] */
-    double* out_sums;                     /* [2*Cb] */
+    double* out_sums;                     /* [RNVP_COUPLING_SHARDS][2*Cb] */
     float* out_rmean; float* out_rvar; long long* out_nbt;
     float* ldj_sample;                    /* [B], += */
     float* ldj_full;                      /* [B,C,H,W] or NULL, written */
@@ -232,10 +240,10 @@ typedef struct rnvp_coupling_args {
     const float* gl_sample;               /* [B] used when gl_full == NULL */
     float* gx;                            /* [B,C,H,W] */
     void* gst; int cs_gst;
-    double* bwd_sums;                     /* [3*Cb] */
+    double* bwd_sums;                     /* [RNVP_COUPLING_SHARDS][3*Cb] */
     float* g_scale; float* g_scale_shift; /* += */
     const void* gh0; int cs_gh0;
-    double* in_bwd_sums;                  /* [2*Cb] */
+    double* in_bwd_sums;                  /* [RNVP_COUPLING_SHARDS][2*Cb] */
     float* g_in_gamma; float* g_in_beta;  /* written */
 } rnvp_coupling_args;
 int rnvp_coupling_in_fwd(const rnvp_coupling_args* a, void* stream);   /* in_sums must be zeroed */
