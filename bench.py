@@ -46,6 +46,7 @@ def parse():
     p.add_argument("--base-dim", type=int, default=32)
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--overlap", action="store_true", help="side stream for weight gradients (HIP graphs serialise it today)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-batch", type=int, default=16)
     p.add_argument("--cpu-steps", type=int, default=2)
@@ -167,7 +168,8 @@ def main():
     hp = utils.Hyperparameters(args.base_dim, args.res_blocks, True, True, True, True)
     model = flow_realnvp.RealNVP(3, args.size, prior, hp).to(dev)
     from realnvp_hip.dist import max_over_ranks, mean_over_ranks, rank_seed
-    tr = FlowTrainer(model, args.batch, dtype=args.dtype, seed=rank_seed(1000, rank), process_group=pg)
+    tr = FlowTrainer(model, args.batch, dtype=args.dtype, seed=rank_seed(1000, rank), process_group=pg,
+                     overlap=args.overlap)
     tr.set_pixels(synthetic_pixels(args.batch, 3, args.size, seed=rank_seed(0, rank)).to(dev))
 
     if not args.no_graph:
@@ -217,7 +219,7 @@ def main():
                                                                 args.batch),
                        "global_batch": world * args.batch, "image_size": args.size, "res_blocks": args.res_blocks,
                        "base_dim": args.base_dim, "parallelism": "dp%d" % world,
-                       "graph": not args.no_graph},
+                       "graph": not args.no_graph, "side_stream": args.overlap},
             "bits_per_dim": round(bpd, 4),
             "step_roofline_frac": round(value / world * ALG_BYTES_PER_IMG / (HBM_PEAK_GBS * 1e9), 5),
             "roofline": roof,

@@ -30,6 +30,13 @@ extern "C" int rnvp_stat_shards(long long M) {
     return r;
 }
 
+// selects the pre-v3 LDS-tiled split-K path for small pixel counts (A/B
+// microbenchmarks; set by rnvp_conv_set_variant)
+static int rnvp_conv_legacy = 0;
+// phase timestamps of the halo kernel (diagnostic builds of a measurement:
+// rnvp_conv_debug_stamps), one row of 8 s_memrealtime values per workgroup
+static unsigned long long* rnvp_conv_stamps = nullptr;
+
 namespace {
 
 template <typename T> struct Mf;
@@ -668,10 +675,679 @@ int launch_conv(const rnvp_conv_args* a, hipStream_t s) {
     return RNVP_OK;
 }
 
+
+// ---------------------------------------------------------------------------
+// deep-K conv for small pixel counts (scales 3-5: M = 1,024..16,384, K up to
+// 4,608): split K over the workgroup's waves instead of over workgroups
+// ---------------------------------------------------------------------------
+// Tile [BM pixels] x [64 channels] per workgroup; every wave computes the
+// whole tile over the k-steps s = wave, wave+4, ... (interleaved, so the four
+// waves read neighbouring bytes of the same pixel rows and weight rows at the
+// same time).  Operands go global -> registers in MFMA fragment layout (an A
+// fragment lane = one pixel's 16-byte channel chunk, a B fragment lane = one
+// weight row's chunk), DK k-steps in flight per wave, BN+ReLU applied in
+// registers; no LDS and no barrier in the main loop.  The four partial tiles
+// are summed through LDS and the fused epilogue (bias / residual / skip
+// accumulation / next-BN statistics, or the dgrad ReLU+BN-backward mask and
+// sums) runs in the same launch: no split-K workspace, no second kernel.
+// Blocks are mapped channel-tile-major so the blocks of one XCD (b % 8) share
+// a slice of the weight matrix in their L2.
+constexpr int DK_MAX_CS = 1024;      // prologue BN table capacity (channels)
+
+template <typename T, int BM>
+struct DkSmem {
+    static constexpr int BN = 64, PITCH = BN + 4;
+    float bnp[2 * DK_MAX_CS];                 // prologue scale | shift
+    float etab[4 * BN];                       // epilogue scale | shift | mean | rstd
+    float btab[BN];
+    float sred[4][BN][2];                     // per-wave BN-stat partials
+    union {
+        double tmp[2 * DK_MAX_CS];            // shard reduction (prologue)
+        float red[4][BM][PITCH];              // partial tiles (end)
+    } u;
+};
+
+template <typename T, int BM, int DK, bool PRO>
+__global__ __launch_bounds__(256, 2) void k_conv_dk(rnvp_conv_args a, int shards) {
+    constexpr int CH = Mf<T>::CH;
+    constexpr int KS = 4 * CH;                 // K per k-step (bf16 32, f32 16)
+    constexpr int BN = 64, TM = BM / 16, TN = BN / 16;
+    constexpr int PITCH = DkSmem<T, BM>::PITCH;
+    constexpr int FR = TM * TN / 4;            // epilogue fragments per wave
+    __shared__ DkSmem<T, BM> sm;
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, li = lane & 15;
+    const int M = a.B * a.H * a.W;
+    const int N = a.n, cs = a.cs_in, ks = a.ks, pad = ks >> 1;
+    const int K = ks * ks * cs;
+    const int nsteps = (K + KS - 1) / KS;
+    const int gm = (M + BM - 1) / BM, gn = (N + BN - 1) / BN;
+    // channel-tile-major, XCD-contiguous tile index (bijective remap)
+    const int nb = gridDim.x, b = blockIdx.x;
+    const int q8 = nb / 8, r8 = nb % 8, xcd = b % 8;
+    const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
+    const int nt = t / gm, mt = t - nt * gm;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const T* __restrict__ X = (const T*)a.x;
+    const T* __restrict__ Wt = (const T*)a.w;
+    constexpr bool pro = PRO;
+    const bool epi_bn = a.epi_relu_bn_bwd != 0;
+
+    // A rows of this lane (fixed over K)
+    int am[TM], ay[TM], ax[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int m = m0 + i * 16 + li;
+        am[i] = m < M ? m : -1;
+        const int mm = m < M ? m : 0;
+        ax[i] = mm % a.W;
+        ay[i] = (mm / a.W) % a.H;
+    }
+    bool bok[TN];
+    const T* wrow[TN];   // this lane's weight rows (clamped in-bounds)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        bok[j] = n0 + j * 16 + li < N;
+        wrow[j] = Wt + (long long)(bok[j] ? n0 + j * 16 + li : 0) * a.kp;
+    }
+
+    // k-step ring
+    u32x4 ra[DK][TM], rb[DK][TN];
+    unsigned amask[DK];
+    int aci[DK];
+    const int my_steps = wid < nsteps ? (nsteps - wid + 3) / 4 : 0;
+    // Every load is unconditional (invalid lanes read a clamped, in-bounds
+    // address and are zeroed at use by a select): a load under a branch makes
+    // hipcc drain vmcnt(0) at each use, which would serialise the ring.  Steps
+    // past my_steps are "dead" (mask 0, MFMA on zeros), so the ring runs in
+    // whole groups of DK with no guard.
+    auto load = [&](int u, int it) {
+        const bool live = it < my_steps;
+        const int k = (wid + 4 * (live ? it : 0)) * KS + g * CH;
+        const int tap = k / cs, ci = k - tap * cs;
+        const int dy = tap / ks - pad, dx = tap % ks - pad;
+        aci[u] = ci;
+        unsigned mk = 0;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int yy = ay[i] + dy, xx = ax[i] + dx;
+            // bitwise, not short-circuit: no control flow around the load
+            const bool ok = live & (am[i] >= 0) & (k < K) & (yy >= 0) & (yy < a.H) & (xx >= 0) & (xx < a.W);
+            const long long off = ok ? (long long)(am[i] + dy * a.W + dx) * cs + ci : 0;
+            ra[u][i] = *(const u32x4*)(X + off);
+            mk |= (ok ? 1u : 0u) << i;
+        }
+        amask[u] = mk;
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+            rb[u][j] = *(const u32x4*)(wrow[j] + k);
+    };
+    // the first DK k-steps are in flight while the tables are built
+#pragma unroll
+    for (int u = 0; u < DK; ++u) load(u, u);
+
+    if (pro) block_bn_table(a.pro, a.cin, 0, cs, sm.bnp, sm.bnp + cs, nullptr, nullptr, sm.u.tmp);
+    if (epi_bn) block_bn_table(a.epi, N, n0, BN, sm.etab, sm.etab + BN, sm.etab + 2 * BN, sm.etab + 3 * BN, sm.u.tmp);
+    for (int c = tid; c < BN; c += 256) sm.btab[c] = (a.bias && n0 + c < N) ? a.bias[n0 + c] : 0.f;
+    __syncthreads();
+
+    floatx4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    for (int it0 = 0; it0 < my_steps; it0 += DK) {
+#pragma unroll
+        for (int u = 0; u < DK; ++u) {
+            const int it = it0 + u;
+            u32x4 av[TM], bv[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) av[i] = ra[u][i];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const uint32_t keep = bok[j] ? ~0u : 0u;
+                bv[j] = rb[u][j] & u32x4{keep, keep, keep, keep};
+            }
+            const unsigned mk = amask[u];
+            const int ci = aci[u];
+            load(u, it + DK);
+            if constexpr (pro) {
+                float sc[CH], sh[CH];
+#pragma unroll
+                for (int c = 0; c < CH; c += 4) {
+                    const floatx4 a4 = *(const floatx4*)&sm.bnp[ci + c];
+                    const floatx4 b4 = *(const floatx4*)&sm.bnp[cs + ci + c];
+                    sc[c] = a4.x; sc[c + 1] = a4.y; sc[c + 2] = a4.z; sc[c + 3] = a4.w;
+                    sh[c] = b4.x; sh[c + 1] = b4.y; sh[c + 2] = b4.z; sh[c + 3] = b4.w;
+                }
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    float f[CH];
+                    unpack(av[i], f, T());
+#pragma unroll
+                    for (int c = 0; c < CH; ++c) f[c] = fmaxf(f[c] * sc[c] + sh[c], 0.f);
+                    // zero padding AFTER act, by an AND (a select here becomes a branch)
+                    const uint32_t keep = 0u - ((mk >> i) & 1u);
+                    av[i] = pack(f, T()) & u32x4{keep, keep, keep, keep};
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const uint32_t keep = 0u - ((mk >> i) & 1u);
+                    av[i] &= u32x4{keep, keep, keep, keep};
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) Mf<T>::step(bv[j], av[i], acc[i][j]);
+        }
+    }
+
+    // ---- reduce the four partial tiles through LDS ----
+    __syncthreads();   // tables done with u.tmp (all waves past the prologue)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) *(floatx4*)&sm.u.red[wid][i * 16 + li][j * 16 + 4 * g] = acc[i][j];
+    __syncthreads();
+
+    // this wave's epilogue fragments: row tile fi, column tiles fj0 .. fj0+FR-1
+    const int fi = wid % TM, fj0 = (wid / TM) * FR;
+    const int m = m0 + fi * 16 + li;
+    const int cso = a.cs_out;
+    float s1[FR][4], s2[FR][4];
+#pragma unroll
+    for (int f = 0; f < FR; ++f)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s1[f][r] = s2[f][r] = 0.f;
+    if (m < M) {
+#pragma unroll
+        for (int f = 0; f < FR; ++f) {
+            const int col = (fj0 + f) * 16 + 4 * g;
+            const int n = n0 + col;
+            if (n >= cso) continue;
+            floatx4 v = *(const floatx4*)&sm.u.red[0][fi * 16 + li][col];
+#pragma unroll
+            for (int w = 1; w < 4; ++w) v += *(const floatx4*)&sm.u.red[w][fi * 16 + li][col];
+            epi4<T>(a, (long long)m * cso + n, v, sm.btab + col, epi_bn, sm.etab + col, BN, s1[f], s2[f], N - n);
+        }
+    }
+    const bool want_sums = a.out_sums || (epi_bn && a.epi_sums);
+    if (want_sums) {
+        // reduce over the 16 pixels of the fragment, then over the waves that
+        // share a column tile (through LDS), one fp64 atomic per channel
+#pragma unroll
+        for (int f = 0; f < FR; ++f)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float u1 = s1[f][r], u2 = s2[f][r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    u1 += __shfl_xor(u1, o, 64);
+                    u2 += __shfl_xor(u2, o, 64);
+                }
+                if (li == 0) {
+                    const int col = (fj0 + f) * 16 + 4 * g + r;
+                    sm.sred[fi][col][0] = u1;
+                    sm.sred[fi][col][1] = u2;
+                }
+            }
+        __syncthreads();
+        double* sums = (epi_bn ? a.epi_sums : a.out_sums);
+        sums += (long long)(blockIdx.x % shards) * 2 * N;
+        for (int col = tid; col < BN; col += 256) {
+            const int n = n0 + col;
+            if (n >= N) continue;
+            float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+            for (int w = 0; w < TM; ++w) {
+                t1 += sm.sred[w][col][0];
+                t2 += sm.sred[w][col][1];
+            }
+            atomicAdd(&sums[n], (double)t1);
+            atomicAdd(&sums[N + n], (double)t2);
+        }
+    }
+}
+
+template <typename T, int BM>
+int launch_dk(const rnvp_conv_args* a, hipStream_t s) {
+    const long long M = (long long)a->B * a->H * a->W;
+    const long long gm = (M + BM - 1) / BM, gn = (a->n + 63) / 64;
+    constexpr int DK = BM >= 64 ? 2 : 4;
+    if (a->pro_bn_relu)
+        k_conv_dk<T, BM, DK, true><<<(unsigned)(gm * gn), 256, 0, s>>>(*a, rnvp_stat_shards(M));
+    else
+        k_conv_dk<T, BM, DK, false><<<(unsigned)(gm * gn), 256, 0, s>>>(*a, rnvp_stat_shards(M));
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+// small pixel count, channel counts the prologue table holds
+template <typename T>
+bool dk_ok(const rnvp_conv_args* a) {
+    const long long M = (long long)a->B * a->H * a->W;
+    return M <= 16384 && a->cs_in <= DK_MAX_CS && a->n > 16;
+}
+
+template <typename T>
+int dispatch_dk(const rnvp_conv_args* a, hipStream_t s) {
+    const long long M = (long long)a->B * a->H * a->W;
+    const long long tiles64 = ((M + 63) / 64) * ((a->n + 63) / 64);
+    if (tiles64 >= 256) return launch_dk<T, 64>(a, s);
+    return launch_dk<T, 32>(a, s);
+}
+
+
+// ---------------------------------------------------------------------------
+// halo-tile conv (deep scales): act(x) staged ONCE per workgroup in LDS
+// ---------------------------------------------------------------------------
+// A workgroup owns 64 consecutive output pixels (NHW order: a band of image
+// rows, or several whole 4x4 / 8x8 images) x BN channels.  Its input rows
+// [m0 - hal, m0 + 64 + hal) (hal = one image row + 1 for 3x3) are loaded
+// once, BN+ReLU'd once and kept in LDS; every tap of the 3x3 then reads its
+// A fragments from LDS (tap validity from a per-pixel 9-bit mask, invalid
+// taps read a zero row), so the transform and the activation traffic are not
+// repeated per tap and per channel tile.  Only the weights stream from global
+// memory (register ring, DK k-steps ahead; every load unconditional).  The
+// four waves split K (interleaved k-steps) and their partial tiles are summed
+// through LDS for the fused epilogue, as in k_conv_dk.
+template <typename T>
+__host__ __device__ constexpr int halo_pitch(int cs) { return cs + Mf<T>::CH; }
+
+
+// BN table for channels [c0, c0+nc) of a source with <= 2 stat shards, in
+// registers (CPT channels per thread, no LDS atomics): tab_issue loads
+// (unconditional, clamped addresses, so the loads can stay in flight behind
+// later ones), tab_finish forms scale/shift (+ mean, rstd) into LDS.
+template <int CPT>
+struct BnTab {
+    double a1[CPT], a2[CPT], b1[CPT], b2[CPT];
+    float gam[CPT], bet[CPT];
+};
+
+template <int CPT>
+__device__ __forceinline__ void tab_issue(const rnvp_bn_src& s, int C, int c0, int nc, BnTab<CPT>& t) {
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+        const int c = threadIdx.x + 256 * j;
+        const int cc = (c < nc && c0 + c < C) ? c0 + c : 0;
+        if (s.sums) {
+            t.a1[j] = s.sums[cc];
+            t.a2[j] = s.sums[C + cc];
+            const int h1 = s.shards > 1 ? 1 : 0;
+            t.b1[j] = s.sums[(long long)h1 * 2 * C + cc];
+            t.b2[j] = s.sums[(long long)h1 * 2 * C + C + cc];
+        } else {
+            t.a1[j] = s.mean[cc];
+            t.a2[j] = s.var[cc];
+            t.b1[j] = t.b2[j] = 0.0;
+        }
+        t.gam[j] = s.gamma ? s.gamma[cc] : 1.f;
+        t.bet[j] = s.beta ? s.beta[cc] : 0.f;
+    }
+}
+
+template <int CPT>
+__device__ __forceinline__ void tab_finish(const rnvp_bn_src& s, int C, int c0, int nc, const BnTab<CPT>& t,
+                                           float* scale, float* shift, float* mean_out, float* rstd_out) {
+    const double inv = s.sums ? 1.0 / s.count : 0.0;
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+        const int c = threadIdx.x + 256 * j;
+        if (c >= nc) continue;
+        float sc = 0.f, sf = 0.f, mo = 0.f, ro = 1.f;
+        if (c0 + c < C) {
+            double mean, var;
+            if (s.sums) {
+                const double s1 = t.a1[j] + (s.shards > 1 ? t.b1[j] : 0.0);
+                const double s2 = t.a2[j] + (s.shards > 1 ? t.b2[j] : 0.0);
+                mean = s1 * inv;
+                var = s2 * inv - mean * mean;
+                if (var < 0) var = 0;
+            } else {
+                mean = t.a1[j];
+                var = t.a2[j];
+            }
+            const float rstd = (float)(1.0 / sqrt(var + (double)s.eps));
+            sc = t.gam[j] * rstd;
+            sf = t.bet[j] - (float)mean * t.gam[j] * rstd;
+            mo = (float)mean;
+            ro = rstd;
+        }
+        scale[c] = sc;
+        shift[c] = sf;
+        if (mean_out) mean_out[c] = mo;
+        if (rstd_out) rstd_out[c] = ro;
+    }
+}
+
+// floor(q / d) for 0 <= q < 2^22 from a float reciprocal r = 1/d: q + 0.5 is
+// >= 0.5 away from any multiple of d, far more than the rounding error.
+__device__ __forceinline__ int fdiv_small(int q, float r) { return (int)(((float)q + 0.5f) * r); }
+
+template <typename T, int BN>
+size_t halo_lds_bytes(int cs, int W, int ks) {
+    constexpr int BM = 64, TM = BM / 16;
+    const int pad = ks / 2, hal = pad * (W + 1), R = BM + 2 * hal;
+    const size_t head = 4 * (4 * BN + BN + 2 * TM * BN);
+    const size_t zrow = (size_t)halo_pitch<T>(cs) * sizeof(T);
+    size_t act = (size_t)R * halo_pitch<T>(cs) * sizeof(T);
+    const size_t red = 4 * (size_t)BM * (BN + 4) * 4;
+    if (red > act) act = red;
+    const size_t tail = 8 * 2 * (size_t)(cs > BN ? cs : BN) + 4 * 2 * (size_t)cs;
+    return head + zrow + act + tail;
+}
+
+template <typename T, int BN, int KSZ, bool PRO, int DK, bool UNI>
+__global__ __launch_bounds__(256) void k_conv_halo(rnvp_conv_args a, int shards, unsigned long long* stamps) {
+#define HALO_STAMP(i) do { if (stamps && threadIdx.x == 0) stamps[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+    HALO_STAMP(0);
+    if (stamps && threadIdx.x == 0) stamps[blockIdx.x * 8 + 6] = __builtin_amdgcn_s_memtime();
+    constexpr int BM = 64;
+    constexpr int CH = Mf<T>::CH, KS = 4 * CH;
+    constexpr int TM = BM / 16, TN = BN / 16;
+    constexpr int PAD = KSZ / 2;
+    constexpr int RP = BN + 4;
+    constexpr int FR = TM * TN / 4;
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, li = lane & 15;
+    const int M = a.B * a.H * a.W, W = a.W, H = a.H;
+    const int N = a.n, cs = a.cs_in;
+    const int K = KSZ * KSZ * cs;
+    const int nsteps = (K + KS - 1) / KS;
+    const int gm = (M + BM - 1) / BM;
+    const int nb = gridDim.x, b = blockIdx.x;
+    const int q8 = nb / 8, r8 = nb % 8, xcd = b % 8;
+    const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
+    const int nt = t / gm, mt = t - nt * gm;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const T* __restrict__ X = (const T*)a.x;
+    const T* __restrict__ Wt = (const T*)a.w;
+    const bool epi_bn = a.epi_relu_bn_bwd != 0;
+
+    const int hal = PAD * (W + 1);
+    const int R = BM + 2 * hal;
+    const int pitch = halo_pitch<T>(cs);
+    float* etab = (float*)lds;                 // scale | shift | mean | rstd [BN each]
+    float* btab = etab + 4 * BN;
+    float* sred = btab + BN;                   // [TM][BN][2]
+    T* zrow = (T*)(sred + TM * BN * 2);
+    T* act = zrow + pitch;
+    size_t act_bytes = (size_t)R * pitch * sizeof(T);
+    if (act_bytes < 4 * (size_t)BM * RP * 4) act_bytes = 4 * (size_t)BM * RP * 4;
+    double* tmp = (double*)((char*)act + act_bytes);
+    float* bnp = (float*)(tmp + 2 * (cs > BN ? cs : BN));
+    float* red = (float*)act;                  // [4][BM][RP], after the K loop
+
+    // ---- prologue, ordered for the in-order vmcnt: staging loads, then the
+    // BN-table loads (the table code waits for both), then the weight ring
+    // (stays in flight across the transform and the barrier) ----
+    const int cpr = cs / CH;
+    const int total = R * cpr;
+    const float rcpr = 1.0f / (float)cpr;
+    constexpr int SB = 20;                     // chunks per thread per batch (deep scales: one batch)
+    u32x4 sv[SB];
+    auto stage_load = [&](int q0) {
+#pragma unroll
+        for (int u = 0; u < SB; ++u) {
+            const int q = q0 + u * 256 + tid;
+            const int r = fdiv_small(q, rcpr), c = q - r * cpr;
+            const int p = m0 - hal + r;
+            const bool ok = (q < total) & (p >= 0) & (p < M);
+            sv[u] = *(const u32x4*)(X + (ok ? (long long)p * cs + c * CH : 0));
+        }
+    };
+    auto stage_store = [&](int q0) {
+#pragma unroll
+        for (int u = 0; u < SB; ++u) {
+            const int q = q0 + u * 256 + tid;
+            if (q >= total) continue;
+            const int r = fdiv_small(q, rcpr), c = q - r * cpr;
+            const int p = m0 - hal + r;
+            u32x4 w = sv[u];
+            if (PRO) {
+                float f[CH];
+                unpack(w, f, T());
+                const int c0 = c * CH;
+#pragma unroll
+                for (int e = 0; e < CH; e += 4) {
+                    const floatx4 sc = *(const floatx4*)&bnp[c0 + e];
+                    const floatx4 sh = *(const floatx4*)&bnp[cs + c0 + e];
+                    f[e] = fmaxf(f[e] * sc.x + sh.x, 0.f);
+                    f[e + 1] = fmaxf(f[e + 1] * sc.y + sh.y, 0.f);
+                    f[e + 2] = fmaxf(f[e + 2] * sc.z + sh.z, 0.f);
+                    f[e + 3] = fmaxf(f[e + 3] * sc.w + sh.w, 0.f);
+                }
+                w = pack(f, T());
+            }
+            const uint32_t keep = (p >= 0 && p < M) ? ~0u : 0u;
+            *(u32x4*)(act + r * pitch + c * CH) = w & u32x4{keep, keep, keep, keep};
+        }
+    };
+    BnTab<DK_MAX_CS / 256> ptab;
+    BnTab<1> etb;
+    if (PRO) tab_issue(a.pro, a.cin, 0, cs, ptab);
+    if (epi_bn) tab_issue(a.epi, N, n0, BN, etb);
+    stage_load(0);
+    if (PRO) tab_finish(a.pro, a.cin, 0, cs, ptab, bnp, bnp + cs, nullptr, nullptr);
+    if (epi_bn) tab_finish(a.epi, N, n0, BN, etb, etab, etab + BN, etab + 2 * BN, etab + 3 * BN);
+    for (int c = tid; c < BN; c += 256) btab[c] = (a.bias && n0 + c < N) ? a.bias[n0 + c] : 0.f;
+    for (int c = tid * CH; c < pitch; c += 256 * CH) *(u32x4*)(zrow + c) = u32x4{0u, 0u, 0u, 0u};
+    __syncthreads();
+    HALO_STAMP(1);
+
+    const T* wrow[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        // rows >= N (clamped to row 0) only feed output columns that are never stored
+        const int row = n0 + j * 16 + li;
+        wrow[j] = Wt + (long long)(row < N ? row : 0) * a.kp + g * CH;
+    }
+    const int wv = __builtin_amdgcn_readfirstlane(wid);     // wave-uniform: step math on the SALU
+    const int my_steps = wv < nsteps ? (nsteps - wv + 3) / 4 : 0;
+    u32x4 rb[DK][TN];
+    auto bload = [&](int u, int it) {
+        const int st = wv + 4 * (it < my_steps ? it : 0);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) rb[u][j] = *(const u32x4*)(wrow[j] + st * KS);
+    };
+#pragma unroll
+    for (int u = 0; u < DK; ++u) bload(u, u);
+
+    // ---- act(x) rows [m0 - hal, m0 + BM + hal) -> LDS (transformed once) ----
+    stage_store(0);
+    for (int q0 = 256 * SB; q0 < total; q0 += 256 * SB) {   // wide channels only
+        stage_load(q0);
+        stage_store(q0);
+    }
+    __syncthreads();
+    HALO_STAMP(2);
+
+    // ---- per-lane pixel state ----
+    int rowoff[TM];      // LDS element offset of the pixel's own row
+    unsigned tvm[TM];    // bit tap set iff that tap of this output pixel is inside the image
+    const float rW = 1.0f / (float)W, rH = 1.0f / (float)H;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int lp = i * 16 + li, m = m0 + lp;
+        rowoff[i] = (lp + hal) * pitch;
+        const int mm = m < M ? m : 0;
+        const int row = fdiv_small(mm, rW);
+        const int x = mm - row * W, y = row - fdiv_small(row, rH) * H;
+        unsigned bits = 0;
+#pragma unroll
+        for (int tp = 0; tp < KSZ * KSZ; ++tp) {
+            const int yy = y + tp / KSZ - PAD, xx = x + tp % KSZ - PAD;
+            bits |= (unsigned)((m < M) & (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W)) << tp;
+        }
+        tvm[i] = bits;
+    }
+    // K position of k = (wid + 4 it) * KS (+ g * CH for this lane).  UNI
+    // (cs % KS == 0): a k-step never straddles a tap, so (tap, ci) are
+    // wave-uniform (SALU) and the lane offset g * CH folds into rowoff.
+    int tap, ci;
+    {
+        const int k = wv * KS + (UNI ? 0 : g * CH);
+        tap = k / cs;
+        ci = k - tap * cs;
+    }
+    if (UNI) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) rowoff[i] += g * CH;
+    }
+    const int zoff = UNI ? 0 : 0;
+
+    floatx4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    for (int it0 = 0; it0 < my_steps; it0 += DK) {
+#pragma unroll
+        for (int u = 0; u < DK; ++u) {
+            const int it = it0 + u;
+            const int dy = tap / KSZ - PAD, dx = tap - (tap / KSZ) * KSZ - PAD;
+            const int toff = (dy * W + dx) * pitch + ci;
+            const bool live = it < my_steps;
+            const int tsh = live ? tap : 31;   // bit 31 of tvm is never set
+            u32x4 av[TM];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const bool ok = (tvm[i] >> tsh) & 1u;
+                const T* src = ok ? act + rowoff[i] + toff : zrow + zoff;
+                av[i] = *(const u32x4*)src;
+            }
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) Mf<T>::step(rb[u][j], av[i], acc[i][j]);
+            // refill this ring slot after its MFMAs (no register copies)
+            bload(u, it + DK);
+            // advance (tap, ci) by 4 k-steps; cs >= 2 * 4 * KS / 2 -> at most two wraps
+            ci += 4 * KS;
+            if (ci >= cs) { ci -= cs; ++tap; }
+            if (ci >= cs) { ci -= cs; ++tap; }
+        }
+    }
+
+    HALO_STAMP(3);
+    // ---- reduce the four partial tiles through LDS (aliases the act tile) ----
+    __syncthreads();
+    HALO_STAMP(4);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) *(floatx4*)&red[(wid * BM + i * 16 + li) * RP + j * 16 + 4 * g] = acc[i][j];
+    __syncthreads();
+
+    const int fi = wid % TM, fj0 = (wid / TM) * FR;
+    const int m = m0 + fi * 16 + li;
+    const int cso = a.cs_out;
+    float s1[FR][4], s2[FR][4];
+#pragma unroll
+    for (int f = 0; f < FR; ++f)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s1[f][r] = s2[f][r] = 0.f;
+    if (m < M) {
+#pragma unroll
+        for (int f = 0; f < FR; ++f) {
+            const int col = (fj0 + f) * 16 + 4 * g;
+            const int n = n0 + col;
+            if (n >= cso) continue;
+            floatx4 v = *(const floatx4*)&red[(fi * 16 + li) * RP + col];
+#pragma unroll
+            for (int w = 1; w < 4; ++w) v += *(const floatx4*)&red[(w * BM + fi * 16 + li) * RP + col];
+            epi4<T>(a, (long long)m * cso + n, v, btab + col, epi_bn, etab + col, BN, s1[f], s2[f], N - n);
+        }
+    }
+    const bool want_sums = a.out_sums || (epi_bn && a.epi_sums);
+    if (want_sums) {
+#pragma unroll
+        for (int f = 0; f < FR; ++f)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float u1 = s1[f][r], u2 = s2[f][r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    u1 += __shfl_xor(u1, o, 64);
+                    u2 += __shfl_xor(u2, o, 64);
+                }
+                if (li == 0) {
+                    const int col = (fj0 + f) * 16 + 4 * g + r;
+                    sred[(fi * BN + col) * 2] = u1;
+                    sred[(fi * BN + col) * 2 + 1] = u2;
+                }
+            }
+        __syncthreads();
+        double* sums = (epi_bn ? a.epi_sums : a.out_sums) + (long long)(blockIdx.x % shards) * 2 * N;
+        for (int col = tid; col < BN; col += 256) {
+            const int n = n0 + col;
+            if (n >= N) continue;
+            float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+            for (int w = 0; w < TM; ++w) {
+                t1 += sred[(w * BN + col) * 2];
+                t2 += sred[(w * BN + col) * 2 + 1];
+            }
+            atomicAdd(&sums[n], (double)t1);
+            atomicAdd(&sums[N + n], (double)t2);
+        }
+    }
+    HALO_STAMP(5);
+    if (stamps && threadIdx.x == 0) stamps[blockIdx.x * 8 + 7] = __builtin_amdgcn_s_memtime();
+#undef HALO_STAMP
+}
+
+template <typename T, int BN, int KSZ>
+int launch_halo(const rnvp_conv_args* a, hipStream_t s) {
+    const long long M = (long long)a->B * a->H * a->W;
+    const long long gm = (M + 63) / 64, gn = (a->n + BN - 1) / BN;
+    const size_t shm = halo_lds_bytes<T, BN>(a->cs_in, a->W, KSZ);
+    const int sh = rnvp_stat_shards(M);
+    const bool uni = a->cs_in % (4 * Mf<T>::CH) == 0;
+    constexpr int DK = BN >= 64 ? 6 : 8;      // weight k-steps in flight per wave
+    const unsigned grid = (unsigned)(gm * gn);
+    if (a->pro_bn_relu) {
+        if (uni) k_conv_halo<T, BN, KSZ, true, DK, true><<<grid, 256, shm, s>>>(*a, sh, rnvp_conv_stamps);
+        else k_conv_halo<T, BN, KSZ, true, DK, false><<<grid, 256, shm, s>>>(*a, sh, rnvp_conv_stamps);
+    } else {
+        if (uni) k_conv_halo<T, BN, KSZ, false, DK, true><<<grid, 256, shm, s>>>(*a, sh, rnvp_conv_stamps);
+        else k_conv_halo<T, BN, KSZ, false, DK, false><<<grid, 256, shm, s>>>(*a, sh, rnvp_conv_stamps);
+    }
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+// deep scales: few pixels, wide channels, the halo tile fits LDS
+template <typename T>
+bool halo_ok(const rnvp_conv_args* a) {
+    const long long M = (long long)a->B * a->H * a->W;
+    if (M > 16384 || a->cs_in < 64 || a->cs_in > DK_MAX_CS || a->n <= 16) return false;
+    if (a->pro_bn_relu && a->pro.sums && a->pro.shards > 2) return false;
+    if (a->epi_relu_bn_bwd && a->epi.sums && a->epi.shards > 2) return false;
+    return halo_lds_bytes<T, 64>(a->cs_in, a->W, a->ks) <= 150 * 1024;
+}
+
+template <typename T>
+int dispatch_halo(const rnvp_conv_args* a, hipStream_t s) {
+    const long long M = (long long)a->B * a->H * a->W;
+    // 64-channel tiles when that still gives >= 256 workgroups
+    const bool wide = ((M + 63) / 64) * ((a->n + 63) / 64) >= 256;
+    if (a->ks == 3) return wide ? launch_halo<T, 64, 3>(a, s) : launch_halo<T, 32, 3>(a, s);
+    return wide ? launch_halo<T, 64, 1>(a, s) : launch_halo<T, 32, 1>(a, s);
+}
+
 template <typename T>
 int dispatch_conv(const rnvp_conv_args* a, hipStream_t s) {
     const long long M = (long long)a->B * a->H * a->W;
     if (stream_ok<T>(a)) return dispatch_stream<T>(a, s);
+    if (rnvp_conv_legacy == 0 && halo_ok<T>(a)) return dispatch_halo<T>(a, s);
+    if (rnvp_conv_legacy == 2 && dk_ok<T>(a)) return dispatch_dk<T>(a, s);
     // largest tile that still gives >= 512 workgroups (2 per CU); small grids
     // fall through to 64x64 tiles and split K
     if (a->n <= 16) return launch_conv<T, 128, 16, 4, 1>(a, s);
@@ -1196,6 +1872,16 @@ extern "C" int rnvp_conv2d(const rnvp_conv_args* a, void* stream) {
     if (a->B == 0) return RNVP_OK;
     hipStream_t s = (hipStream_t)stream;
     return a->dtype == RNVP_F32 ? dispatch_conv<float>(a, s) : dispatch_conv<bf16_t>(a, s);
+}
+
+extern "C" int rnvp_conv_debug_stamps(unsigned long long* device_buf) {
+    rnvp_conv_stamps = device_buf;
+    return RNVP_OK;
+}
+
+extern "C" int rnvp_conv_set_variant(int legacy) {
+    rnvp_conv_legacy = legacy;
+    return RNVP_OK;
 }
 
 extern "C" int rnvp_conv2d_wgrad(const rnvp_wgrad_args* a, void* stream) {

@@ -306,11 +306,11 @@ extern "C" int rnvp_sumsq_bwd_multi(const rnvp_tensor_ref* refs, int n_refs, con
 __global__ void k_step_inc(long long* step) { step[0] += 1; }
 
 __global__ void k_adam(float4* __restrict__ p, const float4* __restrict__ g, float4* __restrict__ m,
-                       float4* __restrict__ v, long long n4, const long long* step, float lr, float b1, float b2,
-                       float eps, float wd, const uint32_t* __restrict__ regm, float reg) {
+                       float4* __restrict__ v, long long n4, const long long* step, long long step_add, float lr,
+                       float b1, float b2, float eps, float wd, const uint32_t* __restrict__ regm, float reg) {
     __shared__ float sh[2];
     if (threadIdx.x == 0) {
-        double t = (double)step[0];
+        double t = (double)(step[0] + step_add);
         double bc1 = 1.0 - pow((double)b1, t), bc2 = 1.0 - pow((double)b2, t);
         sh[0] = (float)(lr / bc1);
         sh[1] = (float)(1.0 / sqrt(bc2));
@@ -348,8 +348,30 @@ extern "C" int rnvp_adam_step(float* param, float* grad, float* exp_avg, float* 
     if (n == 0) return RNVP_OK;
     long long n4 = n / 4;
     k_adam<<<rnvp_grid(n4, 256, 8192), 256, 0, s>>>((float4*)param, (const float4*)grad, (float4*)exp_avg,
-                                                   (float4*)exp_avg_sq, n4, step, lr, beta1, beta2, eps, weight_decay,
+                                                   (float4*)exp_avg_sq, n4, step, 0, lr, beta1, beta2, eps, weight_decay,
                                                    (const uint32_t*)reg_mask, reg_coef);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+extern "C" int rnvp_adam_update(float* param, float* grad, float* exp_avg, float* exp_avg_sq, long long n,
+                                const long long* step, long long step_add, float lr, float beta1, float beta2,
+                                float eps, float weight_decay, const uint8_t* reg_mask, float reg_coef, void* stream) {
+    if (!param || !grad || !exp_avg || !exp_avg_sq || !step || n < 0 || (n & 3)) return RNVP_E_INVALID;
+    if ((((uintptr_t)param) | ((uintptr_t)grad) | ((uintptr_t)exp_avg) | ((uintptr_t)exp_avg_sq)) & 15) return RNVP_E_INVALID;
+    if (reg_mask && (((uintptr_t)reg_mask) & 3)) return RNVP_E_INVALID;
+    if (n == 0) return RNVP_OK;
+    const long long n4 = n / 4;
+    k_adam<<<rnvp_grid(n4, 256, 8192), 256, 0, (hipStream_t)stream>>>(
+        (float4*)param, (const float4*)grad, (float4*)exp_avg, (float4*)exp_avg_sq, n4, step, step_add, lr, beta1,
+        beta2, eps, weight_decay, (const uint32_t*)reg_mask, reg_coef);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+extern "C" int rnvp_step_increment(long long* step, void* stream) {
+    if (!step) return RNVP_E_INVALID;
+    k_step_inc<<<1, 1, 0, (hipStream_t)stream>>>(step);
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
 }

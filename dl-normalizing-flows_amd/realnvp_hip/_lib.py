@@ -117,6 +117,8 @@ _SIGS = {
     "rnvp_bn_running_update": (i32, [vp, i32, i32, f32, vp]),
     "rnvp_stat_shards": (i32, [i64]),
     "rnvp_conv2d": (i32, [C.POINTER(ConvArgs), vp]),
+    "rnvp_conv_set_variant": (i32, [i32]),
+    "rnvp_conv_debug_stamps": (i32, [vp]),
     "rnvp_conv2d_wgrad": (i32, [C.POINTER(WgradArgs), vp]),
     "rnvp_wgrad_slabs": (i32, [i64]),
     "rnvp_wgrad_replicas": (i32, [i32]),
@@ -132,6 +134,8 @@ _SIGS = {
     "rnvp_sumsq_multi": (i32, [vp, i32, vp, vp]),
     "rnvp_sumsq_bwd_multi": (i32, [vp, i32, vp, f32, vp]),
     "rnvp_adam_step": (i32, [vp, vp, vp, vp, i64, vp, f32, f32, f32, f32, f32, vp, f32, vp]),
+    "rnvp_adam_update": (i32, [vp, vp, vp, vp, i64, vp, i64, f32, f32, f32, f32, f32, vp, f32, vp]),
+    "rnvp_step_increment": (i32, [vp, vp]),
     "rnvp_fill_f64": (i32, [vp, i64, f64, vp]),
 }
 

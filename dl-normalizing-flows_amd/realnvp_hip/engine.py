@@ -432,7 +432,7 @@ class CouplingEngine:
         return out, ldj
 
     # --------------------------------------------------------------- backward
-    def backward(self, sv, gz, gl_full, gl_sample, grad_block, gx=None):
+    def backward(self, sv, gz, gl_full, gl_sample, grad_block, gx=None, side=None, after=None):
         """Returns dL/dx; parameter gradients are written into grad_block
         (flat fp32, zeroed by the caller; scale/shift grads accumulate).
 
@@ -537,11 +537,32 @@ class CouplingEngine:
                 esz = DTYPES[dtype][1]
                 wg_bytes += esz * (M * cs_in + M * cs_out) + 4 * sc["wg_nz"] * spec.cout * spec.ks * spec.ks * cs_in
                 wg_flops += 2.0 * M * spec.cout * spec.ks * spec.ks * spec.cin
-        if grp.n_conv:
-            _launch("conv_wgrad", wg_bytes, wg_flops, L.conv2d_wgrad_grouped, C.byref(grp), s)
-        L.weight_norm_bwd(sc["wn_table"].data_ptr(), sc["n_wn"], sc["wn_rows"], gbase, s)
+        # in_bn backward closes the critical path (dL/dx of the coupling) ...
         a.gh0, a.cs_gh0 = sar.ptr("g:h0"), chan_stride(self.P.buf_ch["h0"])
         a.in_bwd_sums = sar.ptr("in_bwd_sums")
         a.g_in_gamma, a.g_in_beta = gp("in_bn.weight"), gp("in_bn.bias")
         L.coupling_in_bwd(C.byref(a), s)
+
+        # ... while the weight gradients (grouped wgrad + weight-norm backward)
+        # only feed the optimizer: on a side stream they overlap the backward
+        # of the couplings before this one.  They read this coupling's saved
+        # activations and gradient scratch, which nothing later in the step
+        # rewrites; `after` runs behind them on the same stream (per-coupling
+        # optimizer update).
+        def weight_grads():
+            ss = stream_ptr()
+            if grp.n_conv:
+                _launch("conv_wgrad", wg_bytes, wg_flops, L.conv2d_wgrad_grouped, C.byref(grp), ss)
+            L.weight_norm_bwd(sc["wn_table"].data_ptr(), sc["n_wn"], sc["wn_rows"], gbase, ss)
+            if after is not None:
+                after()
+
+        if side is None:
+            weight_grads()
+        else:
+            ev = torch.cuda.Event()
+            ev.record()
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                weight_grads()
         return gx

@@ -28,7 +28,7 @@ from .engine import stream_ptr
 
 class FlowTrainer:
     def __init__(self, model, batch_size, lr=5e-4, weight_decay=5e-5, betas=(0.9, 0.999), eps=1e-8,
-                 scale_reg=5e-5, dtype="bf16", seed=0, process_group=None, bucket_mb=64):
+                 scale_reg=5e-5, dtype="bf16", seed=0, process_group=None, bucket_mb=64, overlap=False):
         self.model = model
         self.dev = next(model.parameters()).device
         if self.dev.type != "cuda":
@@ -46,6 +46,12 @@ class FlowTrainer:
         self.graph_opt = None
         self.external_input = False
         self.bucket_elems = max(1, int(bucket_mb * 2 ** 20 // 4))
+        # side stream: weight gradients, weight-norm of the late couplings and
+        # (single process) the per-coupling optimizer update run beside the
+        # critical path (the forward/data-gradient chain)
+        self.overlap = overlap
+        self.side = torch.cuda.Stream(device=self.dev) if overlap else None
+        self._build_adam_ranges()
 
     # ----------------------------------------------------------------- arenas
     def _build_arenas(self):
@@ -120,26 +126,56 @@ class FlowTrainer:
         self._build_wn_table()
 
     def _build_wn_table(self):
-        """One weight-norm descriptor table over every conv of the model: the
-        packed bf16/fp32 weight images are refreshed by ONE forward weight-norm
-        call per step (2 launches) instead of one per coupling."""
+        """Weight-norm descriptor tables over the model's convs: the packed
+        bf16/fp32 weight images are refreshed by two forward weight-norm calls
+        per step (2 launches each) instead of one per coupling.  The first
+        table covers the early couplings (few parameters, needed at once), the
+        second the late, deep couplings (most of the parameters), which the
+        side stream prepares while the early couplings run."""
         import ctypes as C
         from ._lib import WNDesc
-        descs = []
-        row0 = col0 = 0
-        for st in self.stages:
-            if st[0] != "coupling":
+        couplings = [st for st in self.stages if st[0] == "coupling"]
+        self.wn_split = min(len(couplings), max(1, len(couplings) * 3 // 7))
+        self.wn_tables = []
+        for part in (couplings[:self.wn_split], couplings[self.wn_split:]):
+            descs = []
+            row0 = col0 = 0
+            for st in part:
+                for d in st[2].weights(self.dtype)["descs"]:
+                    e = WNDesc()
+                    C.memmove(C.addressof(e), C.addressof(d), C.sizeof(WNDesc))
+                    e.row0, e.col0 = row0, col0
+                    row0 += e.cout
+                    col0 += e.cin
+                    descs.append(e)
+            if not descs:
                 continue
-            for d in st[2].weights(self.dtype)["descs"]:
-                e = WNDesc()
-                C.memmove(C.addressof(e), C.addressof(d), C.sizeof(WNDesc))
-                e.row0, e.col0 = row0, col0
-                row0 += e.cout
-                col0 += e.cin
-                descs.append(e)
-        tab = (WNDesc * len(descs))(*descs)
-        self.wn_table = torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(self.dev)
-        self.wn_n, self.wn_rows, self.wn_cols = len(descs), row0, col0
+            tab = (WNDesc * len(descs))(*descs)
+            t = torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(self.dev)
+            self.wn_tables.append((t, len(descs), row0, col0))
+
+    def _wn_fwd(self, table):
+        t, n, rows, cols = table
+        _lib.lib().weight_norm_fwd(t.data_ptr(), n, rows, cols, 1 if self.dtype == "bf16" else 0, stream_ptr())
+
+    def _build_adam_ranges(self):
+        """Per-coupling optimizer ranges [ru4(off_i), ru4(off_next)) of the flat
+        arena (float4 granules).  A granule straddling two couplings belongs to
+        the range of the coupling at the LOWER offset, whose update runs after
+        the other's in backward order -- so every gradient in a range is final
+        when its update runs.  Disabled (one update at the end) unless the
+        backward visits couplings in descending arena offset."""
+        self.adam_ranges = None
+        if self.pg is not None or not self.overlap:
+            return
+        blocks = [st[6] for st in self.stages if st[0] == "coupling"]
+        base = self.grad.data_ptr()
+        offs = [(b.data_ptr() - base) // 4 for b in blocks]
+        if offs != sorted(offs) or offs[0] != 0:
+            return
+        ru = lambda v: (v + 3) // 4 * 4  # noqa: E731
+        ends = offs[1:] + [self.n]
+        self.adam_ranges = [(ru(o), (ru(e) if e < self.n else self.n)) for o, e in zip(offs, ends)]
 
     def _add_coupling(self, mod, x):
         eng = mod.engine()
@@ -176,10 +212,25 @@ class FlowTrainer:
             L.logit_fwd(self.pix.data_ptr(), None, self.seed, 0, self.step_t.data_ptr(), 0.9, self.xl.data_ptr(),
                         self.logdet.data_ptr(), B, n, s)
         self.ldj.zero_()
-        L.weight_norm_fwd(self.wn_table.data_ptr(), self.wn_n, self.wn_rows, self.wn_cols,
-                          1 if self.dtype == "bf16" else 0, s)
+        late_ready = None
+        if len(self.wn_tables) > 1 and self.side is not None:
+            ev = torch.cuda.Event()
+            ev.record()
+            self.side.wait_event(ev)
+            with torch.cuda.stream(self.side):
+                self._wn_fwd(self.wn_tables[1])
+                late_ready = torch.cuda.Event()
+                late_ready.record()
+            self._wn_fwd(self.wn_tables[0])
+        else:
+            for t in self.wn_tables:
+                self._wn_fwd(t)
+        ci = 0
         for st in self.stages:
             if st[0] == "coupling":
+                if ci == self.wn_split and late_ready is not None:
+                    torch.cuda.current_stream().wait_event(late_ready)
+                ci += 1
                 _, mod, eng, x, z, sv, _ = st
                 eng.forward(x, True, self.dtype, False, saved=sv, prepare=False, ldj_sample=self.ldj, z_out=z)
             elif st[0] == "squeeze":
@@ -203,10 +254,16 @@ class FlowTrainer:
         B = self.B
         gz = self._g(self.z)
         L.prior_logprob_bwd(self.z.data_ptr(), self.g_lp.data_ptr(), gz.data_ptr(), B, self.z[0].numel(), s)
+        ci = sum(1 for st in self.stages if st[0] == "coupling")
         for st in reversed(self.stages):
             if st[0] == "coupling":
+                ci -= 1
                 _, mod, eng, x, z, sv, block = st
-                eng.backward(sv, self._g(z), None, self.g_lp, block, gx=self._g(x))
+                after = None
+                if self.adam_ranges is not None:
+                    lo, hi = self.adam_ranges[ci]
+                    after = (lambda lo=lo, hi=hi: self._adam_range(lo, hi))
+                eng.backward(sv, self._g(z), None, self.g_lp, block, gx=self._g(x), side=self.side, after=after)
             elif st[0] == "squeeze":
                 _, a, b = st
                 L.undo_squeeze(self._g(b).data_ptr(), self._g(a).data_ptr(), *a.shape, s)
@@ -221,7 +278,20 @@ class FlowTrainer:
                 L.factor_out(self._g(full).data_ptr(), self._g(on).data_ptr(), self._g(off).data_ptr(),
                              *full.shape, s)
 
+    def _adam_range(self, lo, hi):
+        b1, b2 = self.betas
+        if hi <= lo:
+            return
+        _lib.lib().adam_update(self.param.data_ptr() + 4 * lo, self.grad.data_ptr() + 4 * lo,
+                               self.exp_avg.data_ptr() + 4 * lo, self.exp_avg_sq.data_ptr() + 4 * lo, hi - lo,
+                               self.step_t.data_ptr(), 1, self.lr, b1, b2, self.eps, self.wd,
+                               self.mask.data_ptr() + lo, self.reg, stream_ptr())
+
     def _optimizer(self):
+        if self.adam_ranges is not None:
+            # the per-coupling updates already ran (side stream, t = step + 1)
+            _lib.lib().step_increment(self.step_t.data_ptr(), stream_ptr())
+            return
         b1, b2 = self.betas
         _lib.lib().adam_step(self.param.data_ptr(), self.grad.data_ptr(), self.exp_avg.data_ptr(),
                              self.exp_avg_sq.data_ptr(), self.n, self.step_t.data_ptr(), self.lr, b1, b2, self.eps,
@@ -237,6 +307,8 @@ class FlowTrainer:
         self.grad.zero_()
         self._forward()
         self._backward()
+        if self.side is not None:
+            torch.cuda.current_stream().wait_stream(self.side)
 
     def step_eager(self):
         self._fwd_bwd()

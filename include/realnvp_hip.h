@@ -125,6 +125,16 @@ typedef struct rnvp_conv_args {
     int n_counters;
 } rnvp_conv_args;
 int rnvp_conv2d(const rnvp_conv_args* a, void* stream);
+/* kernel family for small pixel counts: 0 = halo tile (default: the
+ * workgroup's BN+ReLU'd input rows staged once in LDS, K split over its
+ * waves, one launch), 1 = the LDS-tiled kernel with split-K over workgroups
+ * (+ reduce launch), 2 = deep-K with register operands.  Process-wide; for
+ * A/B measurements. */
+int rnvp_conv_set_variant(int legacy);
+/* diagnostics: when device_buf != NULL the halo-tile conv writes 8
+ * s_memrealtime stamps (100 MHz) per workgroup at its phase boundaries
+ * (start, tables, staging, K loop, reduction, end) to device_buf[wg*8 + i]. */
+int rnvp_conv_debug_stamps(unsigned long long* device_buf);
 
 /* weight gradient: dw[n, k] += sum_m dy[m, n] * act(x)[m + tap(k), ci(k)]
  * (fp32 atomics, dw must be zeroed by the caller), dbias[n] += sum_m dy[m, n]. */
@@ -269,6 +279,16 @@ int rnvp_sumsq_bwd_multi(const rnvp_tensor_ref* refs_device, int n_refs, const f
 int rnvp_adam_step(float* param, float* grad, float* exp_avg, float* exp_avg_sq, long long n,
                    long long* step, float lr, float beta1, float beta2, float eps, float weight_decay,
                    const uint8_t* mask, float reg_coef, void* stream);
+
+/* the same update over one range [param, param+n) of the arena WITHOUT
+ * touching the step counter: bias corrections use t = *step + step_add.  Lets
+ * the optimizer run per parameter group as soon as that group's gradient is
+ * final (e.g. per coupling, overlapped with the rest of the backward); the
+ * caller advances the counter once per step with rnvp_step_increment. */
+int rnvp_adam_update(float* param, float* grad, float* exp_avg, float* exp_avg_sq, long long n,
+                     const long long* step, long long step_add, float lr, float beta1, float beta2, float eps,
+                     float weight_decay, const uint8_t* mask, float reg_coef, void* stream);
+int rnvp_step_increment(long long* step, void* stream);
 
 /* misc */
 int rnvp_fill_f64(double* p, long long n, double v, void* stream);

@@ -1,0 +1,191 @@
+"""Kernel-level parity of rnvp_conv2d (every kernel family it dispatches to:
+register-streaming, deep-K, LDS-tiled + split-K) against a float64 torch CPU
+restatement of the same fused op:
+
+    y[m, n] = sum_k act(x)[m + tap(k), ci(k)] * w[n, k] + bias[n] (+ residual) (+ y)
+    act     = relu(bn(x)) (batch statistics from the given sharded sums) or x
+    stats   = {sum y, sum y^2} per channel           (forward epilogue)
+    dgrad   = y * [relu(bn(epi_x)) > 0], stats {sum, sum * xhat}
+
+which is what WeightNormConv2d inside ResidualBlock computes
+(modules_realnvp.py:64-114) once BatchNorm/ReLU and the residual/skip adds are
+fused.  Tolerances: fp32 1e-5 relative (normwise); bf16 operands are rounded
+the way the kernels round them (act -> bf16 before the product), 4e-3.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+EPS = 1e-5
+
+
+def rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+
+
+def bf16_round(t):
+    return t.to(torch.bfloat16).to(torch.float64)
+
+
+def run_case(B, H, W, cin, cout, ks, dtype, pro=False, residual=False, acc=False, stats=False, dgrad=False,
+             bias=True, variant=0, seed=0):
+    from realnvp_hip import _lib
+    from realnvp_hip._lib import BNSrc, ConvArgs
+    from realnvp_hip.engine import splitk_workspace, stat_shards
+    from realnvp_hip.net import chan_stride, round_up
+    g = torch.Generator().manual_seed(seed)
+    tdt = torch.float32 if dtype == "fp32" else torch.bfloat16
+    M = B * H * W
+    csi, cso = chan_stride(cin), chan_stride(cout)
+    kp = round_up(ks * ks * csi, 64)
+    x = torch.randn(M, cin, generator=g, dtype=torch.float64)
+    w = torch.randn(cout, ks, ks, cin, generator=g, dtype=torch.float64) / np.sqrt(ks * ks * cin)
+    bvec = torch.randn(cout, generator=g, dtype=torch.float64) if bias else torch.zeros(cout, dtype=torch.float64)
+    res = torch.randn(M, cout, generator=g, dtype=torch.float64)
+    yold = torch.randn(M, cout, generator=g, dtype=torch.float64)
+    ex = torch.randn(M, cout, generator=g, dtype=torch.float64)
+    rnd = (lambda t: t.float().double()) if dtype == "fp32" else bf16_round
+    x, w, res, yold, ex, bvec = rnd(x), rnd(w), rnd(res), rnd(yold), rnd(ex), bvec.float().double()
+
+    def nhwc(t, cs):
+        out = torch.zeros(t.shape[0], cs, dtype=tdt)
+        out[:, :t.shape[1]] = t.to(tdt)
+        return out.to(DEV)
+
+    # packed weights: wf[n][(ky*ks+kx)*cs_in + ci]
+    wp = torch.zeros(cout, kp, dtype=tdt)
+    for ky in range(ks):
+        for kx in range(ks):
+            base = (ky * ks + kx) * csi
+            wp[:, base:base + cin] = w[:, ky, kx, :].to(tdt)
+    dx, dw = nhwc(x, csi), wp.to(DEV)
+    dy = nhwc(yold, cso) if acc else torch.zeros(M, cso, dtype=tdt, device=DEV)
+    dres, dex = nhwc(res, cso), nhwc(ex, cso)
+    db = bvec.float().to(DEV)
+
+    # BN statistics for the prologue / dgrad epilogue, as sharded fp64 sums
+    def bn_src(t, C_):
+        sh = stat_shards(M)
+        s1 = t.sum(0)
+        s2 = (t * t).sum(0)
+        sums = torch.zeros(sh, 2, C_, dtype=torch.float64)
+        sums[0, 0], sums[0, 1] = s1, s2   # shard 0 holds everything, others zero
+        gam = (torch.rand(C_, generator=g, dtype=torch.float64) + 0.5).float().double()
+        bet = (torch.randn(C_, generator=g, dtype=torch.float64) * 0.3).float().double()
+        dsums = sums.to(DEV)
+        dg, dbt = gam.float().to(DEV), bet.float().to(DEV)
+        src = BNSrc(dsums.data_ptr(), float(M), None, None, dg.data_ptr(), dbt.data_ptr(), EPS, sh)
+        mean = s1 / M
+        var = (s2 / M - mean * mean).clamp_min(0)
+        rstd = (1.0 / torch.sqrt(var + EPS)).float().double()
+        return src, (dsums, dg, dbt), gam, bet, mean, rstd
+
+    keep = []
+    a = ConvArgs()
+    a.dtype = 0 if dtype == "fp32" else 1
+    a.B, a.H, a.W, a.ks = B, H, W, ks
+    a.x, a.cs_in, a.cin = dx.data_ptr(), csi, cin
+    a.w, a.kp = dw.data_ptr(), kp
+    a.y, a.cs_out, a.n = dy.data_ptr(), cso, cout
+    a.bias = db.data_ptr() if bias else None
+    a.residual = dres.data_ptr() if residual else None
+    a.accumulate = int(acc)
+    act = x
+    if pro:
+        src, k1, gam, bet, mean, rstd = bn_src(x, cin)
+        keep.append(k1)
+        a.pro_bn_relu, a.pro = 1, src
+        # the kernels form fp32 scale/shift, then round act to the operand type
+        scale = (gam * rstd).float().double()
+        shift = (bet - mean.float().double() * gam * rstd).float().double()
+        act = rnd(torch.relu(x * scale + shift))
+    sh = stat_shards(M)
+    osums = torch.zeros(sh, 2, cout, dtype=torch.float64, device=DEV)
+    if stats and not dgrad:
+        a.out_sums = osums.data_ptr()
+    if dgrad:
+        src, k2, egam, ebet, emean, erstd = bn_src(ex, cout)
+        keep.append(k2)
+        a.epi_relu_bn_bwd, a.epi_x, a.epi, a.epi_sums = 1, dex.data_ptr(), src, osums.data_ptr()
+    ws = splitk_workspace(DEV, 8 * M * max(cso, csi) if M <= 16384 else 1)
+    a.ws, a.ws_elems = ws.data_ptr(), ws.numel()
+    L = _lib.lib()
+    L.conv_set_variant(variant)
+    try:
+        L.conv2d(C.byref(a), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+    finally:
+        L.conv_set_variant(0)
+    full = dy.float().cpu()
+    got = full.double()[:, :cout]
+    assert torch.count_nonzero(full[:, cout:]) == 0, "channel padding must stay zero"
+
+    # float64 reference
+    a4 = act.reshape(B, H, W, cin).permute(0, 3, 1, 2)
+    w4 = w.permute(0, 3, 1, 2)
+    ref = torch.nn.functional.conv2d(a4, w4, bias=bvec, padding=ks // 2).permute(0, 2, 3, 1).reshape(M, cout)
+    if residual:
+        ref = ref + res
+    if acc:
+        ref = ref + yold
+    s1 = s2 = None
+    if dgrad:
+        escale = (egam * erstd).float().double()
+        eshift = (ebet - emean.float().double() * egam * erstd).float().double()
+        ref = ref * ((ex * escale + eshift) > 0)
+        xhat = (ex - emean.float().double()) * erstd
+        s1, s2 = ref.sum(0), (ref * xhat).sum(0)
+    elif stats:
+        s1, s2 = ref.sum(0), (ref * ref).sum(0)
+    sums = osums.sum(0).cpu() if (stats or dgrad) else None
+    return got, ref, sums, s1, s2
+
+
+CASES = [
+    # name, B, H, W, cin, cout, ks, flags            (kernel family at this size)
+    ("s5_3x3_pro_stats", 8, 4, 4, 512, 512, 3, dict(pro=True, stats=True, bias=False)),   # deep-K, 32-pixel tiles
+    ("s5_1x1_pro_res", 8, 4, 4, 512, 512, 1, dict(pro=True, residual=True, stats=True)),
+    ("s5_in_3x3", 8, 4, 4, 97, 512, 3, dict(stats=True)),                                 # cin 97 (cs 104)
+    ("s5_out_1x1", 8, 4, 4, 512, 96, 1, dict(pro=True)),
+    ("s5_skip_acc", 8, 4, 4, 512, 512, 1, dict(acc=True, stats=True)),
+    ("s5_3x3_dgrad", 8, 4, 4, 512, 512, 3, dict(dgrad=True, bias=False)),
+    ("s4_3x3_dgrad_res_acc", 16, 8, 8, 256, 256, 3, dict(dgrad=True, residual=True, acc=True, bias=False)),
+    ("s3_3x3_pro_stats", 16, 16, 16, 128, 128, 3, dict(pro=True, stats=True)),            # deep-K, 64-pixel tiles
+    ("s3_1x1_odd", 4, 16, 16, 120, 200, 1, dict(pro=True, stats=True)),                   # ragged N / K
+    ("s2_3x3_stream", 4, 32, 32, 64, 64, 3, dict(pro=True, stats=True)),                  # streaming kernel
+    ("s1_in_3x3_stream", 2, 64, 64, 7, 32, 3, dict(stats=True)),
+    ("big_m_n128", 8, 64, 64, 64, 128, 3, dict(pro=True, stats=True)),                    # LDS-tiled kernel
+]
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_conv_vs_float64(case, dtype):
+    name, B, H, W, cin, cout, ks, fl = case
+    got, ref, sums, s1, s2 = run_case(B, H, W, cin, cout, ks, dtype, **fl)
+    tol = 1e-5 if dtype == "fp32" else 4e-3
+    assert rel(got, ref) < tol, rel(got, ref)
+    if s1 is not None:
+        assert rel(sums[0], s1) < 10 * tol, rel(sums[0], s1)
+        assert rel(sums[1], s2) < 10 * tol, rel(sums[1], s2)
+
+
+DEEP = [c for c in CASES if c[0].startswith(("s5", "s4", "s3"))]
+
+
+@pytest.mark.parametrize("case", DEEP, ids=[c[0] for c in DEEP])
+def test_conv_variants_agree(case):
+    """the small-pixel-count kernel families (halo tile: default; LDS-tiled
+    split-K + reduce launch; deep-K register operands) give the same fp32
+    result"""
+    name, B, H, W, cin, cout, ks, fl = case
+    a, ref, _, _, _ = run_case(B, H, W, cin, cout, ks, "fp32", variant=0, **fl)
+    for v in (1, 2):    # LDS-tiled split-K; deep-K register operands
+        b, _, _, _, _ = run_case(B, H, W, cin, cout, ks, "fp32", variant=v, **fl)
+        assert rel(a, b) < 2e-6, v
+        assert rel(b, ref) < 1e-5, v

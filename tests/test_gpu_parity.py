@@ -171,6 +171,26 @@ def make_model(size, bd, rb):
     return m.to(DEV)
 
 
+def oracle_grads64(size, bd, rb, x, logdet, names):
+    """fp64 CPU oracle gradients of the train.py loss at the formula init
+    (test infrastructure: the truth the fp32 paths are measured against)."""
+    import realnvp_oracle as O
+    from formula_init import formula_value
+    spec = O.FlowSpec(3, size, O.HP(bd, rb))
+    e = O.flow_spec_entries(spec)
+    S = {k: (v.double() if v.is_floating_point() else v) for k, v in O.build_state(e, formula_value).items()}
+    trainable = set(O.trainable_names(e))
+    for n in names:
+        S[n] = S[n].requires_grad_(True)
+    x64 = torch.from_numpy(np.asarray(x)).double()
+    ld64 = torch.from_numpy(np.asarray(logdet)).double()
+    lp = O.log_prob(S, spec, x64, training=True)
+    ws = O.weight_scale(S, O.param_names(e), lambda n: n in trainable)
+    loss = -(lp + ld64).mean() + 5e-5 * ws
+    grads = torch.autograd.grad(loss, [S[n] for n in names])
+    return {n: gr.numpy() for n, gr in zip(names, grads)}
+
+
 @pytest.mark.parametrize("case", MODELS, ids=[c[0] for c in MODELS])
 def test_model_vs_reference(case):
     name, size, bd, rb = case
@@ -198,11 +218,18 @@ def test_model_vs_reference(case):
     # at m32, larger at m64 B=2): allow a 2% tail beyond 8%
     off = np.abs(norms[big] - g["grad_norms"][big]) > 8e-2 * g["grad_norms"][big]
     assert off.mean() <= 0.02, (off.sum(), big.sum())
-    # full tensors stored for scale / scale_shift / in_bn grads: the reference
-    # itself is 2.4e-2 off fp64 in norm on s3_ckbd.2.in_bn.weight (measured)
-    for k in g.files:
-        if k.startswith("grad."):
-            assert rel(params[k[5:]].grad.cpu().numpy(), g[k]) < (1e-1 if size == 32 else 2.5e-1), k
+    # full tensors stored for scale / scale_shift / in_bn grads: sums over the
+    # whole batch that nearly cancel, so fp32 summation order alone moves them
+    # by several percent (the reference itself is 2.4e-2 off fp64 in norm on
+    # s3_ckbd.2.in_bn.weight).  Anchor on the fp64 oracle: ours must be within
+    # the fixed band of the fp64 value, or within 3x the reference's own fp32
+    # error for that tensor.
+    gkeys = [k[5:] for k in g.files if k.startswith("grad.")]
+    g64 = oracle_grads64(size, bd, rb, g["x"], g["logdet"], gkeys)
+    tol = 1e-1 if size == 32 else 2.5e-1
+    for n in gkeys:
+        ours, ref, truth = params[n].grad.cpu().numpy(), g["grad." + n], g64[n]
+        assert rel(ours, truth) < max(tol, 3 * rel(ref, truth)), (n, rel(ours, truth), rel(ref, truth))
     with torch.no_grad():
         z, ldj = model.f(T(g["x"]))
     np.testing.assert_allclose(z.cpu().numpy(), g["train_z"], rtol=1e-3, atol=1e-4)

@@ -98,3 +98,27 @@ def test_bench_config_step_bf16_graph():
     later = tr.mean_logll(10)
     assert np.isfinite(first) and np.isfinite(later)
     assert later > first      # same batch: log-likelihood goes up
+
+
+def test_side_stream_overlap_matches_single_stream():
+    """Weight gradients, late weight norm and per-coupling Adam on the side
+    stream give the same step as the single-stream schedule.  Gradients and
+    first moments are compared normwise (the grouped wgrad's replica atomics
+    make the summation order vary run to run); parameters elementwise within
+    Adam's per-step bound 2*lr (sign flips of near-zero gradients)."""
+    from realnvp_hip.trainer import FlowTrainer
+    res = []
+    for overlap in (False, True):
+        model = make_model(32, 8, 1)
+        tr = FlowTrainer(model, 4, dtype="fp32", overlap=overlap)
+        tr.set_pixels(pixels(4, 3, 32, seed=5).to(DEV))
+        for _ in range(3):
+            tr.step()
+        torch.cuda.synchronize()
+        res.append((tr.param.clone(), tr.grad.clone(), tr.exp_avg.clone(), int(tr.step_t.item()), tr.lr))
+    (p0, g0, m0, s0, lr), (p1, g1, m1, s1, _) = res
+    assert s0 == s1 == 3
+    assert float((g1 - g0).norm() / g0.norm()) < 1e-4
+    assert float((m1 - m0).norm() / m0.norm()) < 1e-4
+    assert float((p1 - p0).abs().max()) <= 3 * 2 * lr * 1.01
+    assert float((p1 - p0).norm() / p0.norm()) < 1e-4

@@ -21,19 +21,29 @@ from realnvp_hip.engine import splitk_workspace, stat_shards  # noqa: E402
 from realnvp_hip.net import chan_stride, round_up  # noqa: E402
 
 
-def bench(fn, iters=20):
-    s = torch.cuda.current_stream()
+def bench(fn, iters=20, reps=5):
+    """Per-launch time inside a captured graph of `iters` back-to-back
+    launches (no per-launch host or event cost; includes the dependent-kernel
+    boundary, as in the training step).  Median over `reps` replays."""
     for _ in range(3):
         fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
     ts = []
-    for _ in range(iters):
+    s = torch.cuda.current_stream()
+    for _ in range(reps):
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record(s)
-        fn()
+        g.replay()
         e1.record(s)
         e1.synchronize()
-        ts.append(e0.elapsed_time(e1))
+        ts.append(e0.elapsed_time(e1) / iters)
     ts.sort()
     return ts[len(ts) // 2] * 1e3   # us
 
@@ -70,7 +80,7 @@ def conv_case(B, H, W, cin, cout, ks, pro=False, stats=False, residual=False, ac
             a.pro = BNSrc(sums_in.data_ptr(), float(M), None, None, gam.data_ptr(), bet.data_ptr(), 1e-5, sh)
         a.dy, a.cs_dy, a.n = y.data_ptr(), cso, cout
         a.dw, a.kp = dw.data_ptr(), kp
-        fn = lambda: L.conv2d_wgrad(C.byref(a), s)  # noqa: E731
+        fn = lambda: L.conv2d_wgrad(C.byref(a), torch.cuda.current_stream().cuda_stream)  # noqa: E731
         nbytes = esz * M * (csi + cso) + 4 * cout * ks * ks * cin
     else:
         a = ConvArgs()
@@ -92,44 +102,95 @@ def conv_case(B, H, W, cin, cout, ks, pro=False, stats=False, residual=False, ac
             a.epi = BNSrc(sums_in.data_ptr(), float(M), None, None, gam.data_ptr(), bet.data_ptr(), 1e-5, sh)
             a.epi_sums = sums_out.data_ptr()
         a.ws, a.ws_elems = ws.data_ptr(), ws.numel()
-        fn = lambda: L.conv2d(C.byref(a), s)  # noqa: E731
+        if dgrad_epi:
+            sums_out.zero_()
+        fn = lambda: L.conv2d(C.byref(a), torch.cuda.current_stream().cuda_stream)  # noqa: E731
         nbytes = esz * (M * csi + cout * kp + M * cso * (1 + int(residual) + int(acc) + int(dgrad_epi)))
     us = bench(fn)
     flops = 2.0 * M * cout * ks * ks * cin
     return us, nbytes / us / 1e3, flops / us / 1e6
 
 
+CASES = [
+    # name, B, H, W, cin, cout, ks, flags
+    ("s1 1x1 32->32 plain", 64, 64, 64, 32, 32, 1, {}),
+    ("s1 1x1 32->32 pro", 64, 64, 64, 32, 32, 1, dict(pro=True)),
+    ("s1 1x1 32->32 pro+stats", 64, 64, 64, 32, 32, 1, dict(pro=True, stats=True)),
+    ("s1 1x1 32->32 pro+stats+res", 64, 64, 64, 32, 32, 1, dict(pro=True, stats=True, residual=True)),
+    ("s1 1x1 32->32 skip acc", 64, 64, 64, 32, 32, 1, dict(acc=True)),
+    ("s1 3x3 32->32 pro+stats", 64, 64, 64, 32, 32, 3, dict(pro=True, stats=True)),
+    ("s1 3x3 32->32 dgrad", 64, 64, 64, 32, 32, 3, dict(dgrad_epi=True)),
+    ("s1 3x3 7->32 in", 64, 64, 64, 7, 32, 3, dict(stats=True)),
+    ("s1 1x1 32->6 out", 64, 64, 64, 32, 6, 1, dict(pro=True)),
+    ("s2 1x1 64->64 pro+stats", 64, 32, 32, 64, 64, 1, dict(pro=True, stats=True)),
+    ("s2 3x3 64->64 pro+stats", 64, 32, 32, 64, 64, 3, dict(pro=True, stats=True)),
+    ("s3 3x3 128->128 pro+stats", 64, 16, 16, 128, 128, 3, dict(pro=True, stats=True)),
+    ("s4 3x3 256->256 pro+stats", 64, 8, 8, 256, 256, 3, dict(pro=True, stats=True)),
+    ("s5 3x3 512->512 pro+stats", 64, 4, 4, 512, 512, 3, dict(pro=True, stats=True)),
+    ("s5 1x1 512->512 pro+stats", 64, 4, 4, 512, 512, 1, dict(pro=True, stats=True)),
+    ("s5 3x3 512->512 dgrad", 64, 4, 4, 512, 512, 3, dict(dgrad_epi=True)),
+    ("s5 1x1 512->512 pro+stats+res", 64, 4, 4, 512, 512, 1, dict(pro=True, stats=True, residual=True)),
+    ("s5 1x1 512->96 out", 64, 4, 4, 512, 96, 1, dict(pro=True)),
+    ("s5 3x3 97->512 in", 64, 4, 4, 97, 512, 3, dict(stats=True)),
+    ("s4 1x1 256->256 pro+stats", 64, 8, 8, 256, 256, 1, dict(pro=True, stats=True)),
+    ("s4 3x3 256->256 dgrad", 64, 8, 8, 256, 256, 3, dict(dgrad_epi=True)),
+    ("s3 1x1 128->128 pro+stats", 64, 16, 16, 128, 128, 1, dict(pro=True, stats=True)),
+    ("s3 3x3 128->128 dgrad", 64, 16, 16, 128, 128, 3, dict(dgrad_epi=True)),
+    ("wgrad s1 1x1 32", 64, 64, 64, 32, 32, 1, dict(pro=True, wgrad=True)),
+    ("wgrad s1 3x3 32", 64, 64, 64, 32, 32, 3, dict(pro=True, wgrad=True)),
+    ("wgrad s2 3x3 64", 64, 32, 32, 64, 64, 3, dict(pro=True, wgrad=True)),
+    ("wgrad s3 3x3 128", 64, 16, 16, 128, 128, 3, dict(pro=True, wgrad=True)),
+    ("wgrad s5 3x3 512", 64, 4, 4, 512, 512, 3, dict(pro=True, wgrad=True)),
+    ("wgrad s5 1x1 512", 64, 4, 4, 512, 512, 1, dict(pro=True, wgrad=True)),
+]
+
+
 def main():
     torch.manual_seed(0)
-    cases = [
-        # name, B, H, W, cin, cout, ks, flags
-        ("s1 1x1 32->32 plain", 64, 64, 64, 32, 32, 1, {}),
-        ("s1 1x1 32->32 pro", 64, 64, 64, 32, 32, 1, dict(pro=True)),
-        ("s1 1x1 32->32 pro+stats", 64, 64, 64, 32, 32, 1, dict(pro=True, stats=True)),
-        ("s1 1x1 32->32 pro+stats+res", 64, 64, 64, 32, 32, 1, dict(pro=True, stats=True, residual=True)),
-        ("s1 1x1 32->32 skip acc", 64, 64, 64, 32, 32, 1, dict(acc=True)),
-        ("s1 3x3 32->32 pro+stats", 64, 64, 64, 32, 32, 3, dict(pro=True, stats=True)),
-        ("s1 3x3 32->32 dgrad", 64, 64, 64, 32, 32, 3, dict(dgrad_epi=True)),
-        ("s1 3x3 7->32 in", 64, 64, 64, 7, 32, 3, dict(stats=True)),
-        ("s1 1x1 32->6 out", 64, 64, 64, 32, 6, 1, dict(pro=True)),
-        ("s2 1x1 64->64 pro+stats", 64, 32, 32, 64, 64, 1, dict(pro=True, stats=True)),
-        ("s2 3x3 64->64 pro+stats", 64, 32, 32, 64, 64, 3, dict(pro=True, stats=True)),
-        ("s3 3x3 128->128 pro+stats", 64, 16, 16, 128, 128, 3, dict(pro=True, stats=True)),
-        ("s4 3x3 256->256 pro+stats", 64, 8, 8, 256, 256, 3, dict(pro=True, stats=True)),
-        ("s5 3x3 512->512 pro+stats", 64, 4, 4, 512, 512, 3, dict(pro=True, stats=True)),
-        ("s5 1x1 512->512 pro+stats", 64, 4, 4, 512, 512, 1, dict(pro=True, stats=True)),
-        ("wgrad s1 1x1 32", 64, 64, 64, 32, 32, 1, dict(pro=True, wgrad=True)),
-        ("wgrad s1 3x3 32", 64, 64, 64, 32, 32, 3, dict(pro=True, wgrad=True)),
-        ("wgrad s2 3x3 64", 64, 32, 32, 64, 64, 3, dict(pro=True, wgrad=True)),
-        ("wgrad s3 3x3 128", 64, 16, 16, 128, 128, 3, dict(pro=True, wgrad=True)),
-        ("wgrad s5 3x3 512", 64, 4, 4, 512, 512, 3, dict(pro=True, wgrad=True)),
-        ("wgrad s5 1x1 512", 64, 4, 4, 512, 512, 1, dict(pro=True, wgrad=True)),
-    ]
-    print("%-32s %9s %9s %9s" % ("case", "us", "GB/s", "TFLOP/s"))
-    for name, B, H, W, ci, co, ks, fl in cases:
-        us, gbs, tfs = conv_case(B, H, W, ci, co, ks, **fl)
-        print("%-32s %9.1f %9.1f %9.1f" % (name, us, gbs, tfs), flush=True)
+    variants = [0, 1, 2] if "--both" in sys.argv else [0]
+    only = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--case=")]
+    print("%-32s %3s %9s %9s %9s" % ("case", "var", "us", "GB/s", "TFLOP/s"))
+    for name, B, H, W, ci, co, ks, fl in CASES:
+        if only and not any(o in name for o in only):
+            continue
+        for v in variants:
+            _lib.lib().conv_set_variant(v)
+            us, gbs, tfs = conv_case(B, H, W, ci, co, ks, **fl)
+            print("%-32s %3d %9.1f %9.1f %9.1f" % (name, v, us, gbs, tfs), flush=True)
+    _lib.lib().conv_set_variant(0)
+
+
+
+
+
+def stamps(case_filter):
+    """Phase breakdown of the halo-tile conv (rnvp_conv_debug_stamps)."""
+    import numpy as np
+    L = _lib.lib()
+    buf = torch.zeros(8 * 65536, dtype=torch.int64, device="cuda")
+    for name, B, H, W, ci, co, ks, fl in CASES:
+        if case_filter not in name:
+            continue
+        L.conv_debug_stamps(buf.data_ptr())
+        buf.zero_()
+        conv_case(B, H, W, ci, co, ks, **fl)
+        torch.cuda.synchronize()
+        L.conv_debug_stamps(None)
+        st = buf.view(-1, 8).cpu().numpy().astype(np.float64)
+        st = st[st[:, 0] > 0]
+        t0 = st[:, 0].min()
+        ph = np.diff(st[:, :6], axis=1) * 10.0 / 1000.0   # us
+        clk = np.median((st[:, 7] - st[:, 6]) / np.maximum(st[:, 5] - st[:, 0], 1)) * 100.0   # MHz
+        print("%-30s wgs %d  start spread %.2f us  end %.2f us | tables %.2f staging %.2f loop %.2f red %.2f epi %.2f"
+              " | shader clock %.0f MHz"
+              % (name, len(st), (st[:, 0].max() - t0) / 100.0, (st[:, 5].max() - t0) / 100.0,
+                 *[float(np.median(ph[:, k])) for k in range(5)], clk))
 
 
 if __name__ == "__main__":
-    main()
+    st = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--stamps=")]
+    if st:
+        for f in st:
+            stamps(f)
+    else:
+        main()

@@ -28,26 +28,32 @@ int main() {
         for (int i = 0; i < 50; ++i) k_touch<<<1024, 256, 0, s>>>(p);
         for (int i = 0; i < 50; ++i) k_lds<<<1024, 256, 48 * 1024, s>>>(p);
     }
-    // same sequence captured in a graph
-    hipGraph_t g;
-    hipGraphExec_t ge;
-    hipStreamBeginCapture(s, hipStreamCaptureModeGlobal);
-    for (int i = 0; i < 50; ++i) k_empty<<<1, 64, 0, s>>>();
-    for (int i = 0; i < 50; ++i) k_touch<<<1024, 256, 0, s>>>(p);
-    for (int i = 0; i < 50; ++i) k_empty_big<<<1024, 256, 0, s>>>(b);
-    hipStreamEndCapture(s, &g);
-    hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    // per-kernel-type graphs: steady-state cost per dispatch inside a graph
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    for (int rep = 0; rep < 3; ++rep) {
-        hipEventRecord(e0, s);
-        hipGraphLaunch(ge, s);
-        hipEventRecord(e1, s);
-        hipEventSynchronize(e1);
-        float ms;
-        hipEventElapsedTime(&ms, e0, e1);
-        printf("graph of 150 kernels: %.1f us total, %.2f us/kernel\n", ms * 1e3, ms * 1e3 / 150);
+    for (int kind = 0; kind < 5; ++kind) {
+        hipGraph_t g;
+        hipGraphExec_t ge;
+        hipStreamBeginCapture(s, hipStreamCaptureModeGlobal);
+        for (int i = 0; i < 200; ++i) {
+            if (kind == 0) k_empty<<<1, 64, 0, s>>>();
+            if (kind == 1) k_empty<<<1024, 256, 0, s>>>();
+            if (kind == 2) k_empty_big<<<1024, 256, 0, s>>>(b);
+            if (kind == 3) k_touch<<<1024, 256, 0, s>>>(p);
+            if (kind == 4) k_lds<<<1024, 256, 48 * 1024, s>>>(p);
+        }
+        hipStreamEndCapture(s, &g);
+        hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+        for (int rep = 0; rep < 3; ++rep) {
+            hipEventRecord(e0, s);
+            hipGraphLaunch(ge, s);
+            hipEventRecord(e1, s);
+            hipEventSynchronize(e1);
+            float ms;
+            hipEventElapsedTime(&ms, e0, e1);
+            if (rep == 2) printf("graph kind %d: 200 kernels %.1f us, %.2f us/kernel\n", kind, ms * 1e3, ms * 1e3 / 200);
+        }
     }
     hipDeviceSynchronize();
     printf("done\n");

@@ -1,6 +1,6 @@
 """Summarise a rocprofv3 --kernel-trace CSV per training step.
 
-    python tools/trace_summary.py run_kernel_trace.csv [--by-shape] [--top N]
+    python tools/trace_summary.py run_kernel_trace.csv|run_results.db [--by-shape] [--top N]
 
 Steps are delimited by k_adam dispatches; the last complete step is reported
 (kernel name, grid, LDS) with count, total and mean duration, plus the step's
@@ -17,13 +17,24 @@ def short(name):
     return re.sub(r"\(.*", "", name)[:60]
 
 
+def load_rows(path):
+    """rocprofv3 kernel-trace CSV, or the rocpd SQLite database (ROCm 7 default output)"""
+    if not path.endswith(".db"):
+        return list(csv.DictReader(open(path)))
+    import sqlite3
+    c = sqlite3.connect(path)
+    q = ("select name, start, end, grid_x, grid_y, grid_z, lds_size from kernels")
+    return [dict(Kernel_Name=n, Start_Timestamp=s, End_Timestamp=e, Grid_Size_X=gx, Grid_Size_Y=gy,
+                 Grid_Size_Z=gz, LDS_Block_Size=lds) for n, s, e, gx, gy, gz, lds in c.execute(q)]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("csv")
     ap.add_argument("--by-shape", action="store_true")
     ap.add_argument("--top", type=int, default=40)
     a = ap.parse_args()
-    rows = list(csv.DictReader(open(a.csv)))
+    rows = load_rows(a.csv)
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     adam = [i for i, r in enumerate(rows) if "k_adam" in r["Kernel_Name"]]
     if len(adam) < 2:
