@@ -84,6 +84,29 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
+// Sum over the 16 lanes of a DPP row (lanes 16r .. 16r+15 = one MFMA column
+// group); every lane of the row gets the result.  row_ror butterfly on the
+// VALU (no LDS round trip: __shfl_xor lowers to ds_bpermute).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, false);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ __forceinline__ float row_sum16(float v) {
+    v += dpp_f<0x128>(v); v += dpp_f<0x124>(v); v += dpp_f<0x122>(v); v += dpp_f<0x121>(v);
+    return v;
+}
+__device__ __forceinline__ double row_sum16(double v) {
+    v += dpp_d<0x128>(v); v += dpp_d<0x124>(v); v += dpp_d<0x122>(v); v += dpp_d<0x121>(v);
+    return v;
+}
+
 // block-wide sum (blockDim.x multiple of 64, <= 1024); every thread gets the result
 template <typename F>
 __device__ __forceinline__ F block_sum(F v, F* red /* >= 16 entries of LDS */) {

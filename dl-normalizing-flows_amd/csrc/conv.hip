@@ -32,6 +32,7 @@ extern "C" int rnvp_stat_shards(long long M) {
 
 // selects the pre-v3 LDS-tiled split-K path for small pixel counts (A/B
 // microbenchmarks; set by rnvp_conv_set_variant)
+// (also the register-streaming kernel instead of the band kernel at the wide scales)
 static int rnvp_conv_legacy = 0;
 // phase timestamps of the halo kernel (diagnostic builds of a measurement:
 // rnvp_conv_debug_stamps), one row of 8 s_memrealtime values per workgroup
@@ -71,7 +72,7 @@ __device__ __forceinline__ double* shard_ptr(double* sums, int shards, int N) {
 // et: LDS epilogue table at channel n0 (scale | shift | mean | rstd, pitch).
 template <typename T>
 __device__ __forceinline__ void epi4(const rnvp_conv_args& a, long long o, const floatx4& acc, const float* bias,
-                                     bool epi_bn, const float* et, int pitch, float* s1, float* s2, int nvalid) {
+                                     bool epi_bn, const float* et, int pitch, double* s1, double* s2, int nvalid) {
     float v[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = acc[r] + bias[r];
@@ -100,7 +101,7 @@ __device__ __forceinline__ void epi4(const rnvp_conv_args& a, long long o, const
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             s1[r] += v[r];
-            s2[r] += v[r] * v[r];
+            s2[r] += (double)v[r] * v[r];
         }
     }
 #pragma unroll
@@ -125,7 +126,7 @@ __global__ __launch_bounds__(256) void k_conv(rnvp_conv_args a, int kt_per_split
 
     __shared__ u32x4 As[2][BM * 8];
     __shared__ u32x4 Bs[2][BN * 8];
-    __shared__ float red[WM * BN * 2];
+    __shared__ double red[WM * BN * 2];
     extern __shared__ double dsm[];   // tmp [2*max(cs,BN)] fp64 | bnp [2*cs] | etab [4*BN]
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -310,7 +311,7 @@ __global__ __launch_bounds__(256) void k_conv(rnvp_conv_args a, int kt_per_split
     {
         // ---- fused epilogue (4 channels of one pixel per lane) ----
         const bool want_sums = a.out_sums || (a.epi_relu_bn_bwd && a.epi_sums);
-        float s1[TN][4], s2[TN][4];
+        double s1[TN][4], s2[TN][4];
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -333,12 +334,7 @@ __global__ __launch_bounds__(256) void k_conv(rnvp_conv_args a, int kt_per_split
             for (int j = 0; j < TN; ++j)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    float u1 = s1[j][r], u2 = s2[j][r];
-#pragma unroll
-                    for (int o = 1; o < 16; o <<= 1) {
-                        u1 += __shfl_xor(u1, o, 64);
-                        u2 += __shfl_xor(u2, o, 64);
-                    }
+                    const double u1 = row_sum16(s1[j][r]), u2 = row_sum16(s2[j][r]);
                     if (li == 0) {
                         const int col = wn * WTN + j * 16 + 4 * g + r;
                         red[(wm * BN + col) * 2] = u1;
@@ -349,7 +345,7 @@ __global__ __launch_bounds__(256) void k_conv(rnvp_conv_args a, int kt_per_split
             for (int col = tid; col < BN; col += 256) {
                 const int n = n0 + col;
                 if (n >= N) continue;
-                float t1 = 0.f, t2 = 0.f;
+                double t1 = 0.0, t2 = 0.0;
 #pragma unroll
                 for (int w = 0; w < WM; ++w) {
                     t1 += red[(w * BN + col) * 2];
@@ -368,7 +364,7 @@ constexpr int MAX_SPLITS = 8;
 
 template <typename T>
 __global__ __launch_bounds__(256) void k_splitk_epi(rnvp_conv_args a, int splits, int shards) {
-    __shared__ float red[16][64][2];
+    __shared__ double red[16][64][2];
     __shared__ double tmp[128];
     __shared__ float etab[4 * 64];
     __shared__ float btab[64];
@@ -391,7 +387,7 @@ __global__ __launch_bounds__(256) void k_splitk_epi(rnvp_conv_args a, int splits
     if (epi_bn) block_bn_table(a.epi, N, n0, 64, etab, etab + 64, etab + 128, etab + 192, tmp);
     if (tid < 64) btab[tid] = (a.bias && n0 + tid < N) ? a.bias[n0 + tid] : 0.f;
     __syncthreads();
-    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+    double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
     if (live) epi4<T>(a, m * cso + n, acc, btab + col, epi_bn, etab + col, 64, s1, s2, N - n);
     const bool want_sums = a.out_sums || (epi_bn && a.epi_sums);
     if (want_sums) {
@@ -402,7 +398,7 @@ __global__ __launch_bounds__(256) void k_splitk_epi(rnvp_conv_args a, int splits
         }
         __syncthreads();
         if (tid < 64 && n0 + tid < N) {
-            float t1 = 0.f, t2 = 0.f;
+            double t1 = 0.0, t2 = 0.0;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 t1 += red[r][tid][0];
@@ -449,7 +445,7 @@ __global__ __launch_bounds__(256) void k_conv_stream(rnvp_conv_args a, int shard
     float* bnp = (float*)(dsm + 2 * ntmp);
     float* etab = bnp + 2 * cs;            // scale | shift | mean | rstd [NC each]
     float* btab = etab + 4 * NC;           // bias [NC]
-    float* red = btab + NC;                // [4 waves][NC][2]
+    double* red = (double*)(btab + NC);    // [4 waves][NC][2]
     T* Wl = (T*)(red + 4 * NC * 2);
 
     // pixel decode of this wave's tile (4 column tiles of 16 pixels); M < 2^31
@@ -508,7 +504,7 @@ __global__ __launch_bounds__(256) void k_conv_stream(rnvp_conv_args a, int shard
     __syncthreads();
 
     const int cso = a.cs_out;
-    float s1[NT][4], s2[NT][4];
+    double s1[NT][4], s2[NT][4];
 #pragma unroll
     for (int j = 0; j < NT; ++j)
 #pragma unroll
@@ -571,12 +567,7 @@ __global__ __launch_bounds__(256) void k_conv_stream(rnvp_conv_args a, int shard
         for (int j = 0; j < NT; ++j)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                float u1 = s1[j][r], u2 = s2[j][r];
-#pragma unroll
-                for (int o = 1; o < 16; o <<= 1) {
-                    u1 += __shfl_xor(u1, o, 64);
-                    u2 += __shfl_xor(u2, o, 64);
-                }
+                const double u1 = row_sum16(s1[j][r]), u2 = row_sum16(s2[j][r]);
                 if (li == 0) {
                     red[(wid * NC + j * 16 + 4 * g + r) * 2] = u1;
                     red[(wid * NC + j * 16 + 4 * g + r) * 2 + 1] = u2;
@@ -585,7 +576,7 @@ __global__ __launch_bounds__(256) void k_conv_stream(rnvp_conv_args a, int shard
         __syncthreads();
         double* sums = shard_ptr(epi_bn ? a.epi_sums : a.out_sums, shards, N);
         for (int n = tid; n < N; n += 256) {
-            float t1 = 0.f, t2 = 0.f;
+            double t1 = 0.0, t2 = 0.0;
 #pragma unroll
             for (int w = 0; w < 4; ++w) {
                 t1 += red[(w * NC + n) * 2];
@@ -603,7 +594,7 @@ size_t stream_lds_bytes(const rnvp_conv_args* a, int nt) {
     const int K = a->ks * a->ks * a->cs_in;
     const int kpl = ((K + KS - 1) / KS) * KS + CH;
     const int nc = 16 * nt, ntmp = a->cs_in > nc ? a->cs_in : nc;
-    return 16 * (size_t)ntmp + 8 * (size_t)a->cs_in + 16 * (size_t)nc + 4 * (size_t)nc + 32 * (size_t)nc +
+    return 16 * (size_t)ntmp + 8 * (size_t)a->cs_in + 16 * (size_t)nc + 4 * (size_t)nc + 64 * (size_t)nc +
            (size_t)nc * kpl * sizeof(T);
 }
 
@@ -700,7 +691,7 @@ struct DkSmem {
     float bnp[2 * DK_MAX_CS];                 // prologue scale | shift
     float etab[4 * BN];                       // epilogue scale | shift | mean | rstd
     float btab[BN];
-    float sred[4][BN][2];                     // per-wave BN-stat partials
+    double sred[4][BN][2];                    // per-wave BN-stat partials
     union {
         double tmp[2 * DK_MAX_CS];            // shard reduction (prologue)
         float red[4][BM][PITCH];              // partial tiles (end)
@@ -857,7 +848,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_dk(rnvp_conv_args a, int shards
     const int fi = wid % TM, fj0 = (wid / TM) * FR;
     const int m = m0 + fi * 16 + li;
     const int cso = a.cs_out;
-    float s1[FR][4], s2[FR][4];
+    double s1[FR][4], s2[FR][4];
 #pragma unroll
     for (int f = 0; f < FR; ++f)
 #pragma unroll
@@ -882,12 +873,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_dk(rnvp_conv_args a, int shards
         for (int f = 0; f < FR; ++f)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                float u1 = s1[f][r], u2 = s2[f][r];
-#pragma unroll
-                for (int o = 1; o < 16; o <<= 1) {
-                    u1 += __shfl_xor(u1, o, 64);
-                    u2 += __shfl_xor(u2, o, 64);
-                }
+                const double u1 = row_sum16(s1[f][r]), u2 = row_sum16(s2[f][r]);
                 if (li == 0) {
                     const int col = (fj0 + f) * 16 + 4 * g + r;
                     sm.sred[fi][col][0] = u1;
@@ -900,7 +886,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_dk(rnvp_conv_args a, int shards
         for (int col = tid; col < BN; col += 256) {
             const int n = n0 + col;
             if (n >= N) continue;
-            float t1 = 0.f, t2 = 0.f;
+            double t1 = 0.0, t2 = 0.0;
 #pragma unroll
             for (int w = 0; w < TM; ++w) {
                 t1 += sm.sred[w][col][0];
@@ -1032,7 +1018,7 @@ template <typename T, int BN>
 size_t halo_lds_bytes(int cs, int W, int ks) {
     constexpr int BM = 64, TM = BM / 16;
     const int pad = ks / 2, hal = pad * (W + 1), R = BM + 2 * hal;
-    const size_t head = 4 * (4 * BN + BN + 2 * TM * BN);
+    const size_t head = 4 * (4 * BN + BN) + 8 * (2 * TM * BN);
     const size_t zrow = (size_t)halo_pitch<T>(cs) * sizeof(T);
     size_t act = (size_t)R * halo_pitch<T>(cs) * sizeof(T);
     const size_t red = 4 * (size_t)BM * (BN + 4) * 4;
@@ -1074,7 +1060,7 @@ __global__ __launch_bounds__(256) void k_conv_halo(rnvp_conv_args a, int shards,
     const int pitch = halo_pitch<T>(cs);
     float* etab = (float*)lds;                 // scale | shift | mean | rstd [BN each]
     float* btab = etab + 4 * BN;
-    float* sred = btab + BN;                   // [TM][BN][2]
+    double* sred = (double*)(btab + BN);       // [TM][BN][2]
     T* zrow = (T*)(sred + TM * BN * 2);
     T* act = zrow + pitch;
     size_t act_bytes = (size_t)R * pitch * sizeof(T);
@@ -1248,7 +1234,7 @@ __global__ __launch_bounds__(256) void k_conv_halo(rnvp_conv_args a, int shards,
     const int fi = wid % TM, fj0 = (wid / TM) * FR;
     const int m = m0 + fi * 16 + li;
     const int cso = a.cs_out;
-    float s1[FR][4], s2[FR][4];
+    double s1[FR][4], s2[FR][4];
 #pragma unroll
     for (int f = 0; f < FR; ++f)
 #pragma unroll
@@ -1271,12 +1257,7 @@ __global__ __launch_bounds__(256) void k_conv_halo(rnvp_conv_args a, int shards,
         for (int f = 0; f < FR; ++f)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                float u1 = s1[f][r], u2 = s2[f][r];
-#pragma unroll
-                for (int o = 1; o < 16; o <<= 1) {
-                    u1 += __shfl_xor(u1, o, 64);
-                    u2 += __shfl_xor(u2, o, 64);
-                }
+                const double u1 = row_sum16(s1[f][r]), u2 = row_sum16(s2[f][r]);
                 if (li == 0) {
                     const int col = (fj0 + f) * 16 + 4 * g + r;
                     sred[(fi * BN + col) * 2] = u1;
@@ -1288,7 +1269,7 @@ __global__ __launch_bounds__(256) void k_conv_halo(rnvp_conv_args a, int shards,
         for (int col = tid; col < BN; col += 256) {
             const int n = n0 + col;
             if (n >= N) continue;
-            float t1 = 0.f, t2 = 0.f;
+            double t1 = 0.0, t2 = 0.0;
 #pragma unroll
             for (int w = 0; w < TM; ++w) {
                 t1 += sred[(w * BN + col) * 2];
@@ -1327,7 +1308,10 @@ int launch_halo(const rnvp_conv_args* a, hipStream_t s) {
 template <typename T>
 bool halo_ok(const rnvp_conv_args* a) {
     const long long M = (long long)a->B * a->H * a->W;
-    if (M > 16384 || a->cs_in < 64 || a->cs_in > DK_MAX_CS || a->n <= 16) return false;
+    // measured against the LDS-tiled kernel: the halo tile wins at M <= 1024
+    // (every shape) and for 3x3 at M <= 4096, loses above
+    if (M > 4096 || (M > 1024 && a->ks != 3)) return false;
+    if (a->cs_in < 64 || a->cs_in > DK_MAX_CS || a->n <= 16) return false;
     if (a->pro_bn_relu && a->pro.sums && a->pro.shards > 2) return false;
     if (a->epi_relu_bn_bwd && a->epi.sums && a->epi.shards > 2) return false;
     return halo_lds_bytes<T, 64>(a->cs_in, a->W, a->ks) <= 150 * 1024;
@@ -1342,9 +1326,285 @@ int dispatch_halo(const rnvp_conv_args* a, hipStream_t s) {
     return wide ? launch_halo<T, 64, 1>(a, s) : launch_halo<T, 32, 1>(a, s);
 }
 
+// ---------------------------------------------------------------------------
+// Band kernel for the wide scales (cs_in <= 64, N <= 64; M = 32k .. 262k
+// pixels).  A workgroup owns a band of BM = 256 consecutive pixels (whole
+// image rows at 64x64 / 32x32); the band plus its halo (pad*(W+1) pixels on
+// either side) is read from HBM once, BN+ReLU applied, into LDS, next to the
+// packed weights.  Each wave owns 64 pixels x all N channels and walks the
+// whole K from LDS: no split-K, no partial-tile reduction, and no per-tap
+// re-fetch of pixels (k_conv_stream re-reads every tap of every pixel from
+// L1/L2 with one k-step in flight).  Transposed product, epilogue as in
+// k_conv_stream (lane = 4 consecutive channels of one pixel).
+template <typename T>
+size_t band_lds_bytes(int cs, int n, int W, int ks) {
+    constexpr int CH = Mf<T>::CH, KS = 4 * CH, BM = 256;
+    const int nc = n <= 16 ? 16 : (n <= 32 ? 32 : 64);
+    const int K = ks * ks * cs;
+    const int kpl = ((K + KS - 1) / KS) * KS + CH;
+    const int R = BM + 2 * (ks / 2) * (W + 1);
+    const int ntmp = cs > nc ? cs : nc;
+    return 16 * (size_t)ntmp + 8 * (size_t)cs + 20 * (size_t)nc + 64 * (size_t)nc +
+           ((size_t)nc * kpl + (size_t)(R + 1) * (cs + CH)) * sizeof(T);
+}
+
+template <typename T, int NT, int KSZ, bool PRO>
+__global__ __launch_bounds__(256) void k_conv_band(rnvp_conv_args a, int shards) {
+    constexpr int CH = Mf<T>::CH, KS = 4 * CH;
+    constexpr int NC = 16 * NT;
+    constexpr int TM = 4, BM = 64 * TM;        // 4 waves x 64 pixels
+    constexpr int PAD = KSZ / 2;
+    constexpr int SB = 12;                     // staged 16-B chunks per thread per batch
+    extern __shared__ double dsm[];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, li = lane & 15;
+    const int M = a.B * a.H * a.W, W = a.W, H = a.H;
+    const int N = a.n, cs = a.cs_in;
+    const int K = KSZ * KSZ * cs;
+    const int nsteps = (K + KS - 1) / KS;
+    const int kpl = nsteps * KS + CH;          // weight row pitch (+16 B)
+    const bool epi_bn = a.epi_relu_bn_bwd != 0;
+    const int ntmp = cs > NC ? cs : NC;
+    const int hal = PAD * (W + 1), R = BM + 2 * hal;
+    const int pitch = cs + CH;                 // band row pitch (+16 B)
+
+    double* tmp = dsm;
+    float* bnp = (float*)(dsm + 2 * ntmp);     // scale | shift [cs each]
+    float* etab = bnp + 2 * cs;                // scale | shift | mean | rstd [NC each]
+    float* btab = etab + 4 * NC;               // bias [NC]
+    double* red = (double*)(btab + NC);        // [4 waves][NC][2]
+    T* Wl = (T*)(red + 8 * NC);                // [NC][kpl]
+    T* zrow = Wl + NC * kpl;                   // [pitch] zeros
+    T* act = zrow + pitch;                     // [R][pitch]
+
+    // consecutive bands (which share halo rows) on one XCD (bijective remap)
+    const int nb = gridDim.x, b = blockIdx.x;
+    const int q8 = nb / 8, r8 = nb % 8, xcd = b % 8;
+    const int m0 = ((xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8) * BM;
+
+    // ---- band + halo loads first: in flight under the table / weight prologue
+    const T* __restrict__ X = (const T*)a.x;
+    const int cpr = cs / CH;
+    const int total = R * cpr;
+    const float rcpr = 1.0f / (float)cpr;
+    u32x4 sv[SB];
+    auto stage_load = [&](int q0) {
+#pragma unroll
+        for (int u = 0; u < SB; ++u) {
+            const int q = q0 + u * 256 + tid;
+            const int r = fdiv_small(q, rcpr), c = q - r * cpr;
+            const int p = m0 - hal + r;
+            const bool ok = (q < total) & (p >= 0) & (p < M);
+            sv[u] = *(const u32x4*)(X + (ok ? (long long)p * cs + c * CH : 0));
+        }
+    };
+    auto stage_store = [&](int q0) {
+#pragma unroll
+        for (int u = 0; u < SB; ++u) {
+            const int q = q0 + u * 256 + tid;
+            if (q >= total) continue;
+            const int r = fdiv_small(q, rcpr), c = q - r * cpr;
+            const int p = m0 - hal + r;
+            u32x4 w = sv[u];
+            if (PRO) {
+                float f[CH];
+                unpack(w, f, T());
+                const int c0 = c * CH;
+#pragma unroll
+                for (int e = 0; e < CH; e += 4) {
+                    const floatx4 sc = *(const floatx4*)&bnp[c0 + e];
+                    const floatx4 sh = *(const floatx4*)&bnp[cs + c0 + e];
+                    f[e] = fmaxf(f[e] * sc.x + sh.x, 0.f);
+                    f[e + 1] = fmaxf(f[e + 1] * sc.y + sh.y, 0.f);
+                    f[e + 2] = fmaxf(f[e + 2] * sc.z + sh.z, 0.f);
+                    f[e + 3] = fmaxf(f[e + 3] * sc.w + sh.w, 0.f);
+                }
+                w = pack(f, T());
+            }
+            const uint32_t keep = (p >= 0 && p < M) ? ~0u : 0u;
+            *(u32x4*)(act + r * pitch + c * CH) = w & u32x4{keep, keep, keep, keep};
+        }
+    };
+    stage_load(0);
+
+    // ---- BN tables, packed weights (rows >= N and k >= K zero) and bias -> LDS
+    if (PRO) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + cs, nullptr, nullptr, tmp);
+    if (epi_bn) block_bn_table(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp);
+    {
+        const T* Wg = (const T*)a.w;
+        const int wcpr = kpl / CH, wtot = NC * wcpr, kv = nsteps * KS;
+        const float rw = 1.0f / (float)wcpr;
+        for (int q0 = 0; q0 < wtot; q0 += 4 * 256) {
+            u32x4 v[4];
+            unsigned okm = 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int q = q0 + u * 256 + tid;
+                const int r = fdiv_small(q, rw), c = q - r * wcpr;
+                const bool ok = (q < wtot) & (r < N) & (c * CH < kv);
+                v[u] = *(const u32x4*)(Wg + (ok ? (long long)r * a.kp + c * CH : 0));
+                okm |= (unsigned)ok << u;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int q = q0 + u * 256 + tid;
+                if (q < wtot) {
+                    const int r = fdiv_small(q, rw), c = q - r * wcpr;
+                    const uint32_t keep = ((okm >> u) & 1u) ? ~0u : 0u;
+                    *(u32x4*)(Wl + r * kpl + c * CH) = v[u] & u32x4{keep, keep, keep, keep};
+                }
+            }
+        }
+        for (int n = tid; n < NC; n += 256) btab[n] = (a.bias && n < N) ? a.bias[n] : 0.f;
+        for (int c = tid * CH; c < pitch; c += 256 * CH) *(u32x4*)(zrow + c) = u32x4{0u, 0u, 0u, 0u};
+    }
+    __syncthreads();
+
+    // ---- act(x) band -> LDS (transformed once) ----
+    stage_store(0);
+    for (int q0 = 256 * SB; q0 < total; q0 += 256 * SB) {
+        stage_load(q0);
+        stage_store(q0);
+    }
+    __syncthreads();
+
+    // ---- per-lane pixel state ----
+    int rowoff[TM];      // LDS element offset of the pixel's own band row
+    unsigned tvm[TM];    // bit tap set iff that tap of this output pixel is inside the image
+    const float rW = 1.0f / (float)W, rH = 1.0f / (float)H;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int lp = wid * 64 + i * 16 + li, m = m0 + lp;
+        rowoff[i] = (lp + hal) * pitch;
+        const int mm = m < M ? m : 0;
+        const int row = fdiv_small(mm, rW);
+        const int x = mm - row * W, y = row - fdiv_small(row, rH) * H;
+        unsigned bits = 0;
+#pragma unroll
+        for (int tp = 0; tp < KSZ * KSZ; ++tp) {
+            const int yy = y + tp / KSZ - PAD, xx = x + tp % KSZ - PAD;
+            bits |= (unsigned)((m < M) & (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W)) << tp;
+        }
+        tvm[i] = bits;
+    }
+
+    floatx4 acc[TM][NT];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    // lane's K position k = s*KS + g*CH -> (tap, ci); a 16-B chunk never
+    // straddles a tap (cs % CH == 0); KS / cs <= 4 wraps per step
+    int tap = 0, ci = g * CH;
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+        if (ci >= cs) { ci -= cs; ++tap; }
+    const T* wl = Wl + li * kpl + g * CH;
+    for (int st = 0; st < nsteps; ++st) {
+        const int ty = tap / KSZ;
+        const int toff = ((ty - PAD) * W + (tap - ty * KSZ - PAD)) * pitch + ci;
+        const int tsh = tap < KSZ * KSZ ? tap : 31;   // bit 31 of tvm is never set
+        u32x4 wv[NT], av[TM];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) wv[j] = *(const u32x4*)(wl + j * 16 * kpl + st * KS);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const bool ok = (tvm[i] >> tsh) & 1u;
+            av[i] = *(const u32x4*)(ok ? act + rowoff[i] + toff : zrow);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) Mf<T>::step(wv[j], av[i], acc[i][j]);
+        ci += KS;
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+            if (ci >= cs) { ci -= cs; ++tap; }
+    }
+
+    // ---- epilogue: lane owns channels j*16 + 4g .. +3 of its pixels ----
+    const int cso = a.cs_out;
+    double s1[NT][4], s2[NT][4];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.0;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int m = m0 + wid * 64 + i * 16 + li;
+        if (m >= M) continue;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const int n0 = j * 16 + 4 * g;
+            if (n0 >= cso) continue;
+            epi4<T>(a, (long long)m * cso + n0, acc[i][j], btab + n0, epi_bn, etab + n0, NC, s1[j], s2[j], N - n0);
+        }
+    }
+    const bool want_sums = a.out_sums || (epi_bn && a.epi_sums);
+    if (want_sums) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double u1 = row_sum16(s1[j][r]), u2 = row_sum16(s2[j][r]);
+                if (li == 0) {
+                    red[(wid * NC + j * 16 + 4 * g + r) * 2] = u1;
+                    red[(wid * NC + j * 16 + 4 * g + r) * 2 + 1] = u2;
+                }
+            }
+        __syncthreads();
+        double* sums = shard_ptr(epi_bn ? a.epi_sums : a.out_sums, shards, N);
+        for (int n = tid; n < N; n += 256) {
+            double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                t1 += red[(w * NC + n) * 2];
+                t2 += red[(w * NC + n) * 2 + 1];
+            }
+            atomicAdd(&sums[n], t1);
+            atomicAdd(&sums[N + n], t2);
+        }
+    }
+}
+
+template <typename T, int NT, int KSZ>
+int launch_band(const rnvp_conv_args* a, hipStream_t s) {
+    const long long M = (long long)a->B * a->H * a->W;
+    const unsigned grid = (unsigned)((M + 255) / 256);
+    const size_t shm = band_lds_bytes<T>(a->cs_in, a->n, a->W, KSZ);
+    const int sh = rnvp_stat_shards(M);
+    if (a->pro_bn_relu) k_conv_band<T, NT, KSZ, true><<<grid, 256, shm, s>>>(*a, sh);
+    else k_conv_band<T, NT, KSZ, false><<<grid, 256, shm, s>>>(*a, sh);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+// wide scales: few channels, many pixels (fp32 reciprocal pixel decode: M < 2^21)
+template <typename T>
+bool band_ok(const rnvp_conv_args* a) {
+    const long long M = (long long)a->B * a->H * a->W;
+    // 3x3 only: for 1x1 the streaming kernel (no halo to share) is faster
+    if (a->n > 64 || a->cs_in > 64 || a->ks != 3) return false;
+    if (M < 32768 || M >= (1ll << 21)) return false;
+    return band_lds_bytes<T>(a->cs_in, a->n, a->W, a->ks) <= 150 * 1024;
+}
+
+template <typename T>
+int dispatch_band(const rnvp_conv_args* a, hipStream_t s) {
+    if (a->ks == 3) {
+        if (a->n <= 16) return launch_band<T, 1, 3>(a, s);
+        if (a->n <= 32) return launch_band<T, 2, 3>(a, s);
+        return launch_band<T, 4, 3>(a, s);
+    }
+    if (a->n <= 16) return launch_band<T, 1, 1>(a, s);
+    if (a->n <= 32) return launch_band<T, 2, 1>(a, s);
+    return launch_band<T, 4, 1>(a, s);
+}
+
 template <typename T>
 int dispatch_conv(const rnvp_conv_args* a, hipStream_t s) {
     const long long M = (long long)a->B * a->H * a->W;
+    if (rnvp_conv_legacy == 0 && band_ok<T>(a)) return dispatch_band<T>(a, s);
     if (stream_ok<T>(a)) return dispatch_stream<T>(a, s);
     if (rnvp_conv_legacy == 0 && halo_ok<T>(a)) return dispatch_halo<T>(a, s);
     if (rnvp_conv_legacy == 2 && dk_ok<T>(a)) return dispatch_dk<T>(a, s);
@@ -1381,6 +1641,7 @@ __device__ __forceinline__ void wgrad_tile(const WgView& a, int co0, int k0, lon
     constexpr int CPR = 64 / CH;                      // chunks per 64-column row
     constexpr int ROWB = 64 * sizeof(T) + 16;         // padded row bytes
     constexpr int PER = STG * CPR / 256;              // chunks per thread per operand (2)
+    constexpr int D = 4;                              // stages of global loads in flight per thread
     __shared__ __attribute__((aligned(16))) char Ps[2][STG * ROWB];
     __shared__ __attribute__((aligned(16))) char Qs[2][STG * ROWB];
     __shared__ float dbs[64];
@@ -1390,6 +1651,7 @@ __device__ __forceinline__ void wgrad_tile(const WgView& a, int co0, int k0, lon
     const int wc = wid >> 1, wk = wid & 1;
     const int N = a.n, cs = a.cs_in, ks = a.ks, pad = ks >> 1;
     const int K = ks * ks * cs;
+    const int H = a.H, W = a.W;
     const T* __restrict__ X = (const T*)a.x;
     const T* __restrict__ DY = (const T*)a.dy;
     const bool do_bias = bias_out != nullptr;
@@ -1402,6 +1664,10 @@ __device__ __forceinline__ void wgrad_tile(const WgView& a, int co0, int k0, lon
     const int ptap = pk / cs, pci = pk - ptap * cs;
     const int pdy = ptap / ks - pad, pdx = ptap % ks - pad;
     const int pco = co0 + sc_ * CH;              // P column
+    const bool colp = pco < N, colq = pk < K;
+    const float rW = 1.0f / (float)W, rH = 1.0f / (float)H;   // pixel decode (M < 2^22, host-checked)
+    const int nst = mb < me ? (int)((me - mb + STG - 1) / STG) : 0;
+    const int mfirst = nst > 0 ? (int)mb : 0;
 
     floatx4 acc[2][2];
 #pragma unroll
@@ -1409,126 +1675,135 @@ __device__ __forceinline__ void wgrad_tile(const WgView& a, int co0, int k0, lon
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-    u32x4 rp[PER], rq[PER];
-    unsigned qmask = 0;
-    auto gload = [&](long long mt) {
-        qmask = 0;
+    // D-deep ring of register stages.  Loads are unconditional (clamped
+    // addresses) so none of them sits under a branch (which would make the
+    // compiler drain the queue); validity travels as bit masks applied when
+    // the stage is written to LDS.
+    u32x4 rp[D][PER], rq[D][PER];
+    unsigned pm[D], qm[D];
+    auto gload = [&](int u, long long mt) {
+        unsigned bp = 0, bq = 0;
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int r = (tid + i * 256) / CPR;
             const long long m = mt + r;
-            rp[i] = u32x4{0u, 0u, 0u, 0u};
-            rq[i] = u32x4{0u, 0u, 0u, 0u};
-            if (m < me) {
-                if (pco < N) rp[i] = *(const u32x4*)(DY + m * a.cs_dy + pco);
-                if (pk < K) {
-                    const int xx = (int)(m % a.W), yy = (int)((m / a.W) % a.H);
-                    const int y2 = yy + pdy, x2 = xx + pdx;
-                    if (y2 >= 0 && y2 < a.H && x2 >= 0 && x2 < a.W) {
-                        rq[i] = *(const u32x4*)(X + (m + (long long)pdy * a.W + pdx) * cs + pci);
-                        qmask |= 1u << i;
-                    }
-                }
-            }
+            const bool inm = m < me;
+            const int mi = inm ? (int)m : mfirst;
+            const int row = fdiv_small(mi, rW);
+            const int xx = mi - row * W, yy = row - fdiv_small(row, rH) * H;
+            const int y2 = yy + pdy, x2 = xx + pdx;
+            const bool okq = inm & colq & (y2 >= 0) & (y2 < H) & (x2 >= 0) & (x2 < W);
+            rp[u][i] = *(const u32x4*)(DY + (long long)mi * a.cs_dy + (colp ? pco : 0));
+            rq[u][i] = *(const u32x4*)(X + (okq ? ((long long)mi + pdy * W + pdx) * cs + pci : 0));
+            bp |= (unsigned)(inm & colp) << i;
+            bq |= (unsigned)okq << i;
         }
+        pm[u] = bp;
+        qm[u] = bq;
     };
-    auto lstore = [&](int buf) {
+    auto lstore = [&](int u, int buf) {
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int r = (tid + i * 256) / CPR;
-            u32x4 v = rq[i];
+            const uint32_t kp = ((pm[u] >> i) & 1u) ? ~0u : 0u;
+            const uint32_t kq = ((qm[u] >> i) & 1u) ? ~0u : 0u;
+            u32x4 v = rq[u][i];
             if (pro) {
-                if (qmask & (1u << i)) {
-                    float f[CH];
-                    unpack(v, f, T());
+                float f[CH];
+                unpack(v, f, T());
 #pragma unroll
-                    for (int j = 0; j < CH; ++j) f[j] = fmaxf(f[j] * bnp[pci + j] + bnp[cs + pci + j], 0.f);
-                    v = pack(f, T());
-                } else {
-                    v = u32x4{0u, 0u, 0u, 0u};
-                }
+                for (int j = 0; j < CH; ++j) f[j] = fmaxf(f[j] * bnp[pci + j] + bnp[cs + pci + j], 0.f);
+                v = pack(f, T());
             }
-            *(u32x4*)(Ps[buf] + r * ROWB + sc_ * 16) = rp[i];
-            *(u32x4*)(Qs[buf] + r * ROWB + sc_ * 16) = v;
+            *(u32x4*)(Ps[buf] + r * ROWB + sc_ * 16) = rp[u][i] & u32x4{kp, kp, kp, kp};
+            *(u32x4*)(Qs[buf] + r * ROWB + sc_ * 16) = v & u32x4{kq, kq, kq, kq};
         }
     };
 
-    if (mb < me) gload(mb);          // first stage in flight while the BN table settles
+    if (nst > 0) {   // the first D stages in flight while the BN table settles
+#pragma unroll
+        for (int u = 0; u < D; ++u) gload(u, mb + (long long)u * STG);
+    }
     if (pro) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + cs, nullptr, nullptr, dsm);
     __syncthreads();
-    if (mb < me) lstore(0);
+    if (nst > 0) lstore(0, 0);
     __syncthreads();
     const int g = lane >> 4, li = lane & 15;
-    int it = 0;
-    for (long long mt = mb; mt < me; mt += STG, ++it) {
-        const int cur = it & 1;
-        const bool more = mt + STG < me;
-        if (more) gload(mt + STG);
-        if (do_bias && tid < 64) {
-            float t = 0.f;
-            for (int r = 0; r < STG; ++r) t += ldv((const T*)(Ps[cur] + r * ROWB) + tid);
-            dbs[tid] += t;
-        }
-        if constexpr (sizeof(T) == 2) {
-            const int q = li >> 2, p = li & 3;
+    float bpart = 0.f;   // bias partial: column tid & 63, rows (tid >> 6) * STG/4 .. of every stage
+    for (int it0 = 0; it0 < nst; it0 += D) {
 #pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                u32x4 af[2], bfr[2];
+        for (int u = 0; u < D; ++u) {
+            const int it = it0 + u;
+            if (it >= nst) break;
+            const int cur = it & 1;
+            // ring slot u (stage it) is in LDS already: refill it with stage it + D
+            gload(u, mb + (long long)(it + D) * STG);
+            if (do_bias) {
+                const int c = tid & 63, r0 = (tid >> 6) * (STG / 4);
 #pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    const int c0 = wc * 32 + i * 16 + 4 * p;
-                    const char* base = Ps[cur] + (32 * s + 8 * g + q) * ROWB + c0 * 2;
-                    i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)base);
-                    i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)(base + 4 * ROWB));
-                    af[i].x = (uint32_t)(uint16_t)lo.x | ((uint32_t)(uint16_t)lo.y << 16);
-                    af[i].y = (uint32_t)(uint16_t)lo.z | ((uint32_t)(uint16_t)lo.w << 16);
-                    af[i].z = (uint32_t)(uint16_t)hi.x | ((uint32_t)(uint16_t)hi.y << 16);
-                    af[i].w = (uint32_t)(uint16_t)hi.z | ((uint32_t)(uint16_t)hi.w << 16);
-                }
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const int c0 = wk * 32 + j * 16 + 4 * p;
-                    const char* base = Qs[cur] + (32 * s + 8 * g + q) * ROWB + c0 * 2;
-                    i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)base);
-                    i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)(base + 4 * ROWB));
-                    bfr[j].x = (uint32_t)(uint16_t)lo.x | ((uint32_t)(uint16_t)lo.y << 16);
-                    bfr[j].y = (uint32_t)(uint16_t)lo.z | ((uint32_t)(uint16_t)lo.w << 16);
-                    bfr[j].z = (uint32_t)(uint16_t)hi.x | ((uint32_t)(uint16_t)hi.y << 16);
-                    bfr[j].w = (uint32_t)(uint16_t)hi.z | ((uint32_t)(uint16_t)hi.w << 16);
-                }
-#pragma unroll
-                for (int i = 0; i < 2; ++i)
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) Mf<bf16_t>::step(af[i], bfr[j], acc[i][j]);
+                for (int r = 0; r < STG / 4; ++r) bpart += ldv((const T*)(Ps[cur] + (r0 + r) * ROWB) + c);
             }
-        } else {
+            if constexpr (sizeof(T) == 2) {
+                const int q = li >> 2, p = li & 3;
 #pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                u32x4 af[2], bfr[2];
+                for (int s = 0; s < 2; ++s) {
+                    u32x4 af[2], bfr[2];
 #pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    const char* pcol = Ps[cur] + (16 * s + 4 * g) * ROWB + (wc * 32 + i * 16 + li) * 4;
-                    af[i].x = *(const uint32_t*)(pcol);
-                    af[i].y = *(const uint32_t*)(pcol + ROWB);
-                    af[i].z = *(const uint32_t*)(pcol + 2 * ROWB);
-                    af[i].w = *(const uint32_t*)(pcol + 3 * ROWB);
+                    for (int i = 0; i < 2; ++i) {
+                        const int c0 = wc * 32 + i * 16 + 4 * p;
+                        const char* base = Ps[cur] + (32 * s + 8 * g + q) * ROWB + c0 * 2;
+                        i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)base);
+                        i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)(base + 4 * ROWB));
+                        af[i].x = (uint32_t)(uint16_t)lo.x | ((uint32_t)(uint16_t)lo.y << 16);
+                        af[i].y = (uint32_t)(uint16_t)lo.z | ((uint32_t)(uint16_t)lo.w << 16);
+                        af[i].z = (uint32_t)(uint16_t)hi.x | ((uint32_t)(uint16_t)hi.y << 16);
+                        af[i].w = (uint32_t)(uint16_t)hi.z | ((uint32_t)(uint16_t)hi.w << 16);
+                    }
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const int c0 = wk * 32 + j * 16 + 4 * p;
+                        const char* base = Qs[cur] + (32 * s + 8 * g + q) * ROWB + c0 * 2;
+                        i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)base);
+                        i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)(base + 4 * ROWB));
+                        bfr[j].x = (uint32_t)(uint16_t)lo.x | ((uint32_t)(uint16_t)lo.y << 16);
+                        bfr[j].y = (uint32_t)(uint16_t)lo.z | ((uint32_t)(uint16_t)lo.w << 16);
+                        bfr[j].z = (uint32_t)(uint16_t)hi.x | ((uint32_t)(uint16_t)hi.y << 16);
+                        bfr[j].w = (uint32_t)(uint16_t)hi.z | ((uint32_t)(uint16_t)hi.w << 16);
+                    }
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) Mf<bf16_t>::step(af[i], bfr[j], acc[i][j]);
                 }
+            } else {
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const char* qcol = Qs[cur] + (16 * s + 4 * g) * ROWB + (wk * 32 + j * 16 + li) * 4;
-                    bfr[j].x = *(const uint32_t*)(qcol);
-                    bfr[j].y = *(const uint32_t*)(qcol + ROWB);
-                    bfr[j].z = *(const uint32_t*)(qcol + 2 * ROWB);
-                    bfr[j].w = *(const uint32_t*)(qcol + 3 * ROWB);
+                for (int s = 0; s < 2; ++s) {
+                    u32x4 af[2], bfr[2];
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        const char* pcol = Ps[cur] + (16 * s + 4 * g) * ROWB + (wc * 32 + i * 16 + li) * 4;
+                        af[i].x = *(const uint32_t*)(pcol);
+                        af[i].y = *(const uint32_t*)(pcol + ROWB);
+                        af[i].z = *(const uint32_t*)(pcol + 2 * ROWB);
+                        af[i].w = *(const uint32_t*)(pcol + 3 * ROWB);
+                    }
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const char* qcol = Qs[cur] + (16 * s + 4 * g) * ROWB + (wk * 32 + j * 16 + li) * 4;
+                        bfr[j].x = *(const uint32_t*)(qcol);
+                        bfr[j].y = *(const uint32_t*)(qcol + ROWB);
+                        bfr[j].z = *(const uint32_t*)(qcol + 2 * ROWB);
+                        bfr[j].w = *(const uint32_t*)(qcol + 3 * ROWB);
+                    }
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) Mf<float>::step(af[i], bfr[j], acc[i][j]);
                 }
-#pragma unroll
-                for (int i = 0; i < 2; ++i)
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) Mf<float>::step(af[i], bfr[j], acc[i][j]);
             }
+            if (it + 1 < nst) lstore((u + 1) % D, cur ^ 1);
+            __syncthreads();
         }
-        if (more) lstore(cur ^ 1);
-        __syncthreads();
     }
     // D rows = co, cols = k
 #pragma unroll
@@ -1545,6 +1820,8 @@ __device__ __forceinline__ void wgrad_tile(const WgView& a, int co0, int k0, lon
                     else *o = acc[i][j][r];
                 }
             }
+    if (do_bias) atomicAdd(&dbs[tid & 63], bpart);
+    __syncthreads();
     if (do_bias && tid < 64 && co0 + tid < N) {
         if (bias_atomic) atomicAdd(&bias_out[co0 + tid], dbs[tid]);
         else bias_out[co0 + tid] = dbs[tid];
@@ -1892,6 +2169,7 @@ extern "C" int rnvp_conv2d_wgrad(const rnvp_wgrad_args* a, void* stream) {
     if ((a->cs_in & 7) || (a->cs_dy & 7) || a->cs_in < a->cin || a->cs_dy < a->n) return RNVP_E_INVALID;
     if (a->kp < a->ks * a->ks * a->cs_in) return RNVP_E_INVALID;
     if (!al16(a->x) || !al16(a->dy)) return RNVP_E_INVALID;
+    if ((long long)a->B * a->H * a->W >= (1ll << 22)) return RNVP_E_UNSUPPORTED;
     if (a->B == 0) return RNVP_OK;
     hipStream_t s = (hipStream_t)stream;
     return a->dtype == RNVP_F32 ? launch_wgrad<float>(a, s) : launch_wgrad<bf16_t>(a, s);
@@ -1915,6 +2193,7 @@ extern "C" int rnvp_conv2d_wgrad_grouped(const rnvp_wgrad_group* gin, void* stre
     rnvp_wgrad_group g = *gin;
     const long long M = (long long)g.B * g.H * g.W;
     const int STG = g.dtype == RNVP_BF16 ? 64 : 32;
+    if (M >= (1ll << 22)) return RNVP_E_UNSUPPORTED;
     long long tasks = 0;
     int max_cs = 8;
     for (int c = 0; c < g.n_conv; ++c) {

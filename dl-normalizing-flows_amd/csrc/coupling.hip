@@ -79,6 +79,10 @@ __device__ __forceinline__ float seg_sum(float v, int seg) {
     for (int o = 1; o < seg; o <<= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+__device__ __forceinline__ double seg_sum(double v, int seg) {
+    for (int o = 1; o < seg; o <<= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
 
 template <typename T>
 __device__ __forceinline__ void tile_copy_in(const void* src, long long m0, int tp, int cs, T* lds) {
@@ -149,10 +153,10 @@ __global__ __launch_bounds__(256) void k_in_stats(rnvp_coupling_args a, int TP, 
         const int c = (g.kind == 0) ? cb : g.off_base + cb;
         float v = ok ? a.x[((long long)t.b * g.C + c) * g.HW + p] : 0.f;
         if (g.kind == 0 && !ckbd_m(g, p)) v = 0.f;
-        const float s1 = seg_sum(v, seg), s2 = seg_sum(v * v, seg);
+        const double s1 = seg_sum((double)v, seg), s2 = seg_sum((double)v * v, seg);
         if (ok && (lane & (seg - 1)) == 0) {
-            atomicAdd(&red[cb], (double)s1);
-            atomicAdd(&red[g.Cb + cb], (double)s2);
+            atomicAdd(&red[cb], s1);
+            atomicAdd(&red[g.Cb + cb], s2);
         }
     }
     __syncthreads();
@@ -244,10 +248,10 @@ __global__ __launch_bounds__(256) void k_out1(rnvp_coupling_args a, int TP, int 
             sl += lr;
         }
         if (ok) a.u[idx] = u;
-        const float s1 = seg_sum(u, seg), s2 = seg_sum(u * u, seg);
+        const double s1 = seg_sum((double)u, seg), s2 = seg_sum((double)u * u, seg);
         if (ok && (g.kind == 0 || chan_on) && (lane & (seg - 1)) == 0) {
-            atomicAdd(&red[cb], (double)s1);
-            atomicAdd(&red[g.Cb + cb], (double)s2);
+            atomicAdd(&red[cb], s1);
+            atomicAdd(&red[g.Cb + cb], s2);
         }
     }
     const float dl = block_sum(sl, redl);   // (barriers also publish red)
@@ -419,13 +423,11 @@ __global__ __launch_bounds__(256) void k_out_bwd_red(rnvp_coupling_args a, int T
             vB = gz * (a.u[idx] - tab[cb]) * tab[g.Cb + cb];
             vG = gl_at(a, idx, t.b);
         }
-        vA = seg_sum(vA, seg);
-        vB = seg_sum(vB, seg);
-        vG = seg_sum(vG, seg);
+        const double dA = seg_sum((double)vA, seg), dB = seg_sum((double)vB, seg), dG = seg_sum((double)vG, seg);
         if (ok && (lane & (seg - 1)) == 0) {
-            atomicAdd(&red[cb], (double)vA);
-            atomicAdd(&red[g.Cb + cb], (double)vB);
-            atomicAdd(&red[2 * g.Cb + cb], (double)vG);
+            atomicAdd(&red[cb], dA);
+            atomicAdd(&red[g.Cb + cb], dB);
+            atomicAdd(&red[2 * g.Cb + cb], dG);
         }
     }
     __syncthreads();
@@ -438,7 +440,7 @@ __global__ __launch_bounds__(256) void k_out_bwd_red(rnvp_coupling_args a, int T
 template <typename T>
 __global__ __launch_bounds__(256) void k_out_bwd_apply(rnvp_coupling_args a, int TP, int seg) {
     extern __shared__ double dsm[];
-    __shared__ float redl[16];
+    __shared__ double redl[16];
     const Geo g = geo(a);
     const Tile t = tile_of(g, TP);
     float* tab = (float*)dsm;                         // fm | rstd | kA | kB [Cb each]
@@ -461,7 +463,7 @@ __global__ __launch_bounds__(256) void k_out_bwd_apply(rnvp_coupling_args a, int
     for (int e = threadIdx.x; e < t.tp * a.cs_gst; e += blockDim.x) stv(&gs[e], 0.f);
     __syncthreads();
     const float sc = a.scale[0], ss = a.scale_shift[0];
-    float gsc = 0.f, gss = 0.f;
+    double gsc = 0.0, gss = 0.0;
     const int total = g.C * t.tp;
     for (int e = threadIdx.x; e < total; e += blockDim.x) {
         const int c = e / t.tp, pl = e - c * t.tp, p = t.p0 + pl;
@@ -492,14 +494,14 @@ __global__ __launch_bounds__(256) void k_out_bwd_apply(rnvp_coupling_args a, int
             const float glr = gu * a.x[idx] * ex + gl_at(a, idx, t.b);
             stv(&gs[pl * a.cs_gst + cb], gu);
             stv(&gs[pl * a.cs_gst + g.Cb + cb], glr * sc * (1.f - th * th));
-            gsc += glr * th;
+            gsc += (double)glr * th;
             gss += glr;
         } else {
             a.gx[idx] = gu;
         }
     }
-    const float dsc = block_sum(gsc, redl);   // (barriers also publish gs)
-    const float dss = block_sum(gss, redl);
+    const float dsc = (float)block_sum(gsc, redl);   // (barriers also publish gs)
+    const float dss = (float)block_sum(gss, redl);
     tile_copy_out<T>(gs, t.m0, t.tp, a.cs_gst, a.gst);
     if (threadIdx.x == 0 && (dsc != 0.f || dss != 0.f)) {
         atomicAdd(a.g_scale, dsc);
@@ -545,10 +547,10 @@ __global__ __launch_bounds__(256) void k_in_bwd_red(rnvp_coupling_args a, int TP
         const int cb = ok ? e / t.tp : 0, pl = ok ? e - cb * t.tp : 0;
         float gxa = 0.f, xh = 0.f;
         if (ok) in_bwd_vals<T>(a, g, t, gh, tab, cb, pl, gxa, xh);
-        const float s1 = seg_sum(gxa, seg), s2 = seg_sum(gxa * xh, seg);
+        const double s1 = seg_sum((double)gxa, seg), s2 = seg_sum((double)gxa * xh, seg);
         if (ok && (lane & (seg - 1)) == 0) {
-            atomicAdd(&red[cb], (double)s1);
-            atomicAdd(&red[g.Cb + cb], (double)s2);
+            atomicAdd(&red[cb], s1);
+            atomicAdd(&red[g.Cb + cb], s2);
         }
     }
     __syncthreads();

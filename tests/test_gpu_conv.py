@@ -1,5 +1,5 @@
 """Kernel-level parity of rnvp_conv2d (every kernel family it dispatches to:
-register-streaming, deep-K, LDS-tiled + split-K) against a float64 torch CPU
+band, register-streaming, halo tile, deep-K, LDS-tiled + split-K) against a float64 torch CPU
 restatement of the same fused op:
 
     y[m, n] = sum_k act(x)[m + tap(k), ci(k)] * w[n, k] + bias[n] (+ residual) (+ y)
@@ -160,6 +160,14 @@ CASES = [
     ("s2_3x3_stream", 4, 32, 32, 64, 64, 3, dict(pro=True, stats=True)),                  # streaming kernel
     ("s1_in_3x3_stream", 2, 64, 64, 7, 32, 3, dict(stats=True)),
     ("big_m_n128", 8, 64, 64, 64, 128, 3, dict(pro=True, stats=True)),                    # LDS-tiled kernel
+    # band kernel (M >= 32768, cs_in <= 64, N <= 64)
+    ("s2_3x3_band", 32, 32, 32, 64, 64, 3, dict(pro=True, stats=True)),
+    ("s1_3x3_band_dgrad", 8, 64, 64, 32, 32, 3, dict(dgrad=True, residual=True, acc=True, bias=False)),
+    ("s1_1x1_band_res", 8, 64, 64, 32, 32, 1, dict(pro=True, residual=True, stats=True)),
+    ("s1_in_band", 8, 64, 64, 7, 32, 3, dict(stats=True)),
+    ("s1_out_band", 8, 64, 64, 32, 6, 1, dict(pro=True)),
+    ("s2_1x1_band_odd", 32, 32, 32, 60, 40, 1, dict(pro=True, stats=True)),
+    ("band_ragged_m", 9, 61, 61, 24, 16, 3, dict(pro=True, stats=True)),                 # M % 256 != 0, odd W
 ]
 
 
@@ -189,3 +197,17 @@ def test_conv_variants_agree(case):
         b, _, _, _, _ = run_case(B, H, W, cin, cout, ks, "fp32", variant=v, **fl)
         assert rel(a, b) < 2e-6, v
         assert rel(b, ref) < 1e-5, v
+
+
+BAND = [c for c in CASES if "band" in c[0]]
+
+
+@pytest.mark.parametrize("case", BAND, ids=[c[0] for c in BAND])
+def test_band_matches_stream(case):
+    """band kernel (default at the wide scales) vs the register-streaming
+    kernel (variant 1), fp32"""
+    name, B, H, W, cin, cout, ks, fl = case
+    a, ref, _, _, _ = run_case(B, H, W, cin, cout, ks, "fp32", variant=0, **fl)
+    b, _, _, _, _ = run_case(B, H, W, cin, cout, ks, "fp32", variant=1, **fl)
+    assert rel(a, b) < 2e-6
+    assert rel(b, ref) < 1e-5
