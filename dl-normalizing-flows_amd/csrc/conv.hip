@@ -34,6 +34,8 @@ extern "C" int rnvp_stat_shards(long long M) {
 // microbenchmarks; set by rnvp_conv_set_variant)
 // (also the register-streaming kernel instead of the band kernel at the wide scales)
 static int rnvp_conv_legacy = 0;
+// pixels per wave of the streaming kernel / 16 (0: automatic; set by variant codes 11, 12, 14)
+static int rnvp_stream_tw = 0;
 // phase timestamps of the halo kernel (diagnostic builds of a measurement:
 // rnvp_conv_debug_stamps), one row of 8 s_memrealtime values per workgroup
 static unsigned long long* rnvp_conv_stamps = nullptr;
@@ -425,7 +427,7 @@ __global__ __launch_bounds__(256) void k_splitk_epi(rnvp_conv_args a, int splits
 // fragments are loaded before the current MFMAs, and the first tile's loads
 // are issued before the BN-table / weight prologue.
 
-template <typename T, int NT>
+template <typename T, int NT, int TW>
 __global__ __launch_bounds__(256) void k_conv_stream(rnvp_conv_args a, int shards) {
     constexpr int CH = Mf<T>::CH;
     constexpr int KS = 4 * CH;             // K per step call (bf16: one 16x16x32, f32: four 16x16x4)
@@ -449,13 +451,13 @@ __global__ __launch_bounds__(256) void k_conv_stream(rnvp_conv_args a, int shard
     T* Wl = (T*)(red + 4 * NC * 2);
 
     // pixel decode of this wave's tile (4 column tiles of 16 pixels); M < 2^31
-    const int ntiles = (int)((M + 63) / 64);
+    const int ntiles = (int)((M + 16 * TW - 1) / (16 * TW));
     const int tstride = gridDim.x * 4;
-    int mrow[4], yr[4], xr[4];
+    int mrow[TW], yr[TW], xr[TW];
     auto decode = [&](int t) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int m = t * 64 + i * 16 + li;
+        for (int i = 0; i < TW; ++i) {
+            const int m = t * (16 * TW) + i * 16 + li;
             mrow[i] = (t < ntiles && m < M) ? m : -1;
             const int mm = mrow[i] >= 0 ? m : 0;
             xr[i] = mm % a.W;
@@ -463,7 +465,7 @@ __global__ __launch_bounds__(256) void k_conv_stream(rnvp_conv_args a, int shard
         }
     };
     const T* __restrict__ X = (const T*)a.x;
-    u32x4 ra[4];
+    u32x4 ra[TW];
     unsigned msk = 0;
     int cur_ci = 0;
     auto load = [&](int s) {
@@ -473,7 +475,7 @@ __global__ __launch_bounds__(256) void k_conv_stream(rnvp_conv_args a, int shard
         cur_ci = ci;
         msk = 0;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < TW; ++i) {
             ra[i] = u32x4{0u, 0u, 0u, 0u};
             const int yy = yr[i] + dy, xx = xr[i] + dx;
             if (mrow[i] >= 0 && k < K && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) {
@@ -511,22 +513,22 @@ __global__ __launch_bounds__(256) void k_conv_stream(rnvp_conv_args a, int shard
         for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.f;
 
     for (; t < ntiles; t += tstride) {
-        floatx4 acc[4][NT];
+        floatx4 acc[TW][NT];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < TW; ++i)
 #pragma unroll
             for (int j = 0; j < NT; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
         for (int s = 0; s < nsteps; ++s) {
-            u32x4 av[4];
+            u32x4 av[TW];
             const int ci = cur_ci;
             const unsigned mk = msk;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) av[i] = ra[i];
+            for (int i = 0; i < TW; ++i) av[i] = ra[i];
             if (s + 1 < nsteps) load(s + 1);   // next k-step in flight under these MFMAs
             if (pro) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
+                for (int i = 0; i < TW; ++i) {
                     if (mk & (1u << i)) {
                         float f[CH];
                         unpack(av[i], f, T());
@@ -540,13 +542,13 @@ __global__ __launch_bounds__(256) void k_conv_stream(rnvp_conv_args a, int shard
 #pragma unroll
             for (int j = 0; j < NT; ++j) wv[j] = *(const u32x4*)(Wl + (j * 16 + li) * kpl + s * KS + g * CH);
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < TW; ++i)
 #pragma unroll
                 for (int j = 0; j < NT; ++j) Mf<T>::step(wv[j], av[i], acc[i][j]);
         }
         // epilogue: lane owns channels j*16 + 4g .. +3 of pixel t*64 + i*16 + li
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < TW; ++i) {
             const long long m = mrow[i];
             if (m < 0) continue;
 #pragma unroll
@@ -598,15 +600,27 @@ size_t stream_lds_bytes(const rnvp_conv_args* a, int nt) {
            (size_t)nc * kpl * sizeof(T);
 }
 
-template <typename T, int NT>
+template <typename T, int NT, int TW>
 int launch_stream(const rnvp_conv_args* a, hipStream_t s) {
     const long long M = (long long)a->B * a->H * a->W;
-    const long long ntiles = (M + 63) / 64;
+    const long long ntiles = (M + 16 * TW - 1) / (16 * TW);
     long long grid = (ntiles + 3) / 4;
-    if (grid > 1024) grid = 1024;
-    k_conv_stream<T, NT><<<(unsigned)grid, 256, stream_lds_bytes<T>(a, NT), s>>>(*a, rnvp_stat_shards(M));
+    if (grid > 2048) grid = 2048;
+    k_conv_stream<T, NT, TW><<<(unsigned)grid, 256, stream_lds_bytes<T>(a, NT), s>>>(*a, rnvp_stat_shards(M));
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
+}
+
+// pixels per wave (16 * TW), picked per pixel count from measurements
+// (rnvp_stream_tw overrides for A/B runs)
+template <typename T, int NT>
+int launch_stream_tw(const rnvp_conv_args* a, hipStream_t s) {
+    const long long M = (long long)a->B * a->H * a->W;
+    int tw = rnvp_stream_tw;
+    if (tw == 0) tw = M >= 4 * 64 * 1024 ? 4 : (M >= 32 * 1024 ? 2 : 1);   // measured: s1 4, s2 2
+    if (tw == 1) return launch_stream<T, NT, 1>(a, s);
+    if (tw == 2) return launch_stream<T, NT, 2>(a, s);
+    return launch_stream<T, NT, 4>(a, s);
 }
 
 // true when the streaming kernel handles this conv (N <= 64, weights fit LDS)
@@ -619,9 +633,9 @@ bool stream_ok(const rnvp_conv_args* a) {
 
 template <typename T>
 int dispatch_stream(const rnvp_conv_args* a, hipStream_t s) {
-    if (a->n <= 16) return launch_stream<T, 1>(a, s);
-    if (a->n <= 32) return launch_stream<T, 2>(a, s);
-    return launch_stream<T, 4>(a, s);
+    if (a->n <= 16) return launch_stream_tw<T, 1>(a, s);
+    if (a->n <= 32) return launch_stream_tw<T, 2>(a, s);
+    return launch_stream_tw<T, 4>(a, s);
 }
 
 template <typename T, int BM, int BN, int WM, int WN>
@@ -2157,6 +2171,12 @@ extern "C" int rnvp_conv_debug_stamps(unsigned long long* device_buf) {
 }
 
 extern "C" int rnvp_conv_set_variant(int legacy) {
+    if (legacy >= 10) {   // streaming-kernel tile override, default kernels otherwise
+        rnvp_stream_tw = legacy - 10;
+        rnvp_conv_legacy = 0;
+        return RNVP_OK;
+    }
+    rnvp_stream_tw = 0;
     rnvp_conv_legacy = legacy;
     return RNVP_OK;
 }

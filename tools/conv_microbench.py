@@ -148,6 +148,9 @@ CASES = [
 def main():
     torch.manual_seed(0)
     variants = [0, 1, 2] if "--both" in sys.argv else ([0, 1] if "--v01" in sys.argv else [0])
+    vs = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--variants=")]
+    if vs:
+        variants = [int(v) for v in vs[0].split(",")]
     only = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--case=")]
     print("%-32s %3s %9s %9s %9s" % ("case", "var", "us", "GB/s", "TFLOP/s"))
     for name, B, H, W, ci, co, ks, fl in CASES:
