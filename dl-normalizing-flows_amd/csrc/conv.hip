@@ -1946,10 +1946,16 @@ __global__ void k_bn_bwd(rnvp_bn_bwd_args a) {
     const T* X = (const T*)a.x;
     const T* R = (const T*)a.residual;
     T* DX = (T*)a.dx;
-    const long long nch = a.M * (cs / CH);
-    for (long long q = blockIdx.x * (long long)blockDim.x + threadIdx.x; q < nch; q += (long long)gridDim.x * blockDim.x) {
+    const int cpr = cs / CH;
+    const long long nch = a.M * cpr;
+    const long long q0 = blockIdx.x * (long long)blockDim.x + threadIdx.x, qs = (long long)gridDim.x * blockDim.x;
+    // the grid stride is a multiple of the chunks per pixel in practice: the
+    // channel chunk of a thread is then fixed (no 64-bit modulo per chunk)
+    const bool fixed = qs % cpr == 0;
+    int c0 = (int)(q0 % cpr) * CH;
+    for (long long q = q0; q < nch; q += qs) {
         const long long o = q * CH;
-        const int c0 = (int)(o % cs);
+        if (!fixed) c0 = (int)(q % cpr) * CH;
         float g[CH], x[CH], d[CH];
         unpack(*(const u32x4*)(G + o), g, T());
         unpack(*(const u32x4*)(X + o), x, T());
@@ -2024,12 +2030,13 @@ __global__ __launch_bounds__(256) void k_wn_rows(const rnvp_wn_desc* __restrict_
     const float scale = d.g ? d.g[co] / nrm : 1.f;
     if (threadIdx.x == 0 && d.norm) d.norm[co] = nrm;
     T* wf = (T*)d.wf + (long long)co * d.kp_f;
+    const float rcs = 1.0f / (float)d.cs_in;
     for (int k0 = threadIdx.x * CH; k0 < d.kp_f; k0 += blockDim.x * CH) {
         float w[CH];
+        const int tap = fdiv_small(k0, rcs), c0 = k0 - tap * d.cs_in;   // a chunk never straddles a tap
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
-            const int k = k0 + j;
-            const int tap = k / d.cs_in, ci = k - tap * d.cs_in;
+            const int ci = c0 + j;
             w[j] = 0.f;
             if (tap < kk && ci < d.cin) w[j] = scale * (in_lds ? rowbuf[ci * kk + tap] : v[ci * kk + tap]);
         }
@@ -2057,19 +2064,21 @@ __global__ __launch_bounds__(256) void k_wn_cols(const rnvp_wn_desc* __restrict_
         return sc * d.v[(long long)co * kr + ci * kk + tap];
     };
     if (in_lds) {
+        const float rkk = 1.0f / (float)kk;
         for (int q = threadIdx.x; q < n; q += blockDim.x) {
-            const int co = q / kk, tap = q - co * kk;
+            const int co = fdiv_small(q, rkk), tap = q - co * kk;
             sbuf[q] = wval(co, tap);
         }
         __syncthreads();
     }
     T* wd = (T*)d.wd + (long long)ci * d.kp_d;
+    const float rco = 1.0f / (float)d.cs_out;
     for (int k0 = threadIdx.x * CH; k0 < d.kp_d; k0 += blockDim.x * CH) {
         float w[CH];
+        const int tp = fdiv_small(k0, rco), c0 = k0 - tp * d.cs_out;    // cs_out % 8 == 0
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
-            const int k = k0 + j;
-            const int tp = k / d.cs_out, co = k - tp * d.cs_out;
+            const int co = c0 + j;
             w[j] = 0.f;
             if (tp < kk && co < d.cout) {
                 const int tap = kk - 1 - tp;
@@ -2104,8 +2113,9 @@ __global__ void k_wn_bwd(const rnvp_wn_desc* __restrict__ descs, int n_desc, flo
     };
     if (in_lds) {
         const int K = kk * d.cs_in;
+        const float rcs = 1.0f / (float)d.cs_in;
         for (int k = threadIdx.x; k < K; k += blockDim.x) {
-            const int tap = k / d.cs_in, ci = k - tap * d.cs_in;
+            const int tap = fdiv_small(k, rcs), ci = k - tap * d.cs_in;
             if (ci < d.cin) rowbuf[ci * kk + tap] = dw_at(k);
         }
         __syncthreads();
