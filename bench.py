@@ -51,6 +51,11 @@ def parse():
     p.add_argument("--cpu-batch", type=int, default=16)
     p.add_argument("--cpu-steps", type=int, default=2)
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--pmc-markers", default=None,
+                   help="write the instrumented step's launch families here and dispatch a marker before each "
+                        "launch (for rocprofv3 --pmc passes, tools/pmc_traffic.py)")
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+                   help="per-family PMC HBM bytes per launch (tools/pmc_traffic.py output) for roofline.traffic")
     return p.parse_args()
 
 
@@ -61,15 +66,20 @@ def synthetic_pixels(B, C, S, seed):
     return torch.from_numpy((k / 255.0).astype(np.float32))
 
 
-def kernel_roofline(trainer):
+def kernel_roofline(trainer, markers=None, traffic=None, config=None):
     """One instrumented eager step: HIP events around every engine launch
     (recorded on the launch stream).  Returns per-family totals and the
-    roofline object of the dominant (largest total time) family."""
+    roofline object of the dominant (largest total time) family.  `traffic`
+    (tools/pmc_traffic.py output of the same config) supplies the PMC HBM
+    bytes per launch."""
     from realnvp_hip import engine as E
     E.PROFILE = []
+    E.MARKERS = markers is not None
+    E.MARKER_FAMILIES = []
     torch.cuda.synchronize()
     trainer.step_eager()
     torch.cuda.synchronize()
+    E.MARKERS = False
     fam = {}
     for f, nb, fl, e0, e1 in E.PROFILE:
         ms = e0.elapsed_time(e1)
@@ -79,6 +89,9 @@ def kernel_roofline(trainer):
         d["flops"] += fl
         d["launches"] += 1
     E.PROFILE = None
+    if markers is not None:
+        json.dump(dict(config=config, families=E.MARKER_FAMILIES, n_params=int(trainer.param.numel()),
+                       alg_bytes={k: v["bytes"] / v["launches"] for k, v in fam.items()}), open(markers, "w"))
     dom = max(fam, key=lambda k: fam[k]["ms"])
     d = fam[dom]
     avg_ms = d["ms"] / d["launches"]
@@ -99,6 +112,12 @@ def kernel_roofline(trainer):
     roof.update(kernel=dom, launches_per_step=d["launches"], avg_launch_us=round(avg_ms * 1e3, 2),
                 alg_bytes_per_launch=int(bytes_per_launch), flops_per_launch=int(flops_per_launch),
                 traffic=None)
+    if traffic and os.path.exists(traffic):
+        t = json.load(open(traffic))
+        row = t.get("families", {}).get(dom)
+        if t.get("config") == config and row:
+            roof["traffic"] = row["traffic_per_launch"]
+            roof["traffic_source"] = "PMC 2*FETCH_SIZE+WRITE_SIZE, %s" % os.path.relpath(traffic, ROOT)
     families = {k: dict(ms=round(v["ms"], 3), launches=v["launches"],
                         gbs=round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1),
                         tflops=round(v["flops"] / max(v["ms"], 1e-9) / 1e9, 2)) for k, v in fam.items()}
@@ -198,7 +217,9 @@ def main():
     bpd = tr.bits_per_dim(mean_ll)
     imgs = world * args.batch * args.steps
     value = imgs / dt
-    roof, fams = kernel_roofline(tr)
+    cfg_key = dict(size=args.size, res_blocks=args.res_blocks, base_dim=args.base_dim, batch=args.batch,
+                   dtype=args.dtype)
+    roof, fams = kernel_roofline(tr, args.pmc_markers if rank == 0 else None, args.traffic, cfg_key)
     out = None
     if rank == 0:
         out = {

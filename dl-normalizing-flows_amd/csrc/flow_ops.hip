@@ -13,6 +13,17 @@ extern "C" const char* rnvp_status_string(int s) {
     return hipGetErrorString((hipError_t)s);
 }
 
+// Profiling marker: an empty one-lane dispatch.  bench.py brackets each engine
+// launch of its instrumented step with one so that per-dispatch PMC records
+// (rocprofv3 --pmc) can be attributed to kernel families (tools/pmc_traffic.py).
+__global__ void k_marker(int tag) { (void)tag; }
+
+extern "C" int rnvp_marker(int tag, void* stream) {
+    k_marker<<<1, 1, 0, (hipStream_t)stream>>>(tag);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
 // ---------------------------------------------------------------------------
 // index maps  (modules_realnvp.py:211-226, flow_realnvp.py:121-193)
 // ---------------------------------------------------------------------------

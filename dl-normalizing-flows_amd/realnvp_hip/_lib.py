@@ -105,6 +105,7 @@ class TensorRef(C.Structure):
 _SIGS = {
     "rnvp_version": (i32, []),
     "rnvp_status_string": (C.c_char_p, [i32]),
+    "rnvp_marker": (i32, [i32, vp]),
     "rnvp_checkerboard_mask": (i32, [vp, i32, i32, vp]),
     "rnvp_squeeze": (i32, [vp, vp, i32, i32, i32, i32, vp]),
     "rnvp_undo_squeeze": (i32, [vp, vp, i32, i32, i32, i32, vp]),

@@ -37,16 +37,26 @@ def stream_ptr():
 # list, every engine launch appends (family, algorithmic bytes, flops,
 # start event, end event), events recorded on the launch stream.
 PROFILE = None
+# When MARKERS is set (with PROFILE), an empty marker dispatch precedes and
+# follows every engine launch so a per-dispatch PMC trace can be split by family
+# (tools/pmc_traffic.py); MARKER_FAMILIES records the order.
+MARKERS = False
+MARKER_FAMILIES = []
 
 
 def _launch(family, nbytes, flops, fn, *args):
     if PROFILE is None:
         return fn(*args)
+    if MARKERS:
+        _lib.lib().marker(len(MARKER_FAMILIES), stream_ptr())
+        MARKER_FAMILIES.append(family)
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     e0.record()
     fn(*args)
     e1.record()
+    if MARKERS:
+        _lib.lib().marker(-1, stream_ptr())
     PROFILE.append((family, nbytes, flops, e0, e1))
 
 

@@ -34,6 +34,8 @@ enum { RNVP_OK = 0, RNVP_E_INVALID = -1, RNVP_E_UNSUPPORTED = -2 };
 /* ---- version / capabilities ------------------------------------------- */
 int rnvp_version(void);
 const char* rnvp_status_string(int status);
+/* empty one-lane dispatch: delimits engine launches in PMC traces (profiling only) */
+int rnvp_marker(int tag, void* stream);
 
 /* ---- index maps (bit-exact permutations) --------------------------------
  * replace AbstractCoupling.build_mask   modules_realnvp.py:211-226

@@ -112,18 +112,25 @@ def test_side_stream_overlap_matches_single_stream():
         model = make_model(32, 8, 1)
         tr = FlowTrainer(model, 4, dtype="fp32", overlap=overlap)
         tr.set_pixels(pixels(4, 3, 32, seed=5).to(DEV))
-        for _ in range(3):
+        tr.step()
+        torch.cuda.synchronize()
+        first = tr.grad.clone()
+        for _ in range(2):
             tr.step()
         torch.cuda.synchronize()
-        res.append((tr.param.clone(), tr.grad.clone(), tr.exp_avg.clone(), int(tr.step_t.item()), tr.lr))
-    (p0, g0, m0, s0, lr), (pb, gb, mb, _, _), (p1, g1, m1, s1, _) = res
+        res.append((tr.param.clone(), tr.grad.clone(), tr.exp_avg.clone(), int(tr.step_t.item()), tr.lr, first))
+    (p0, g0, m0, s0, lr, f0), (pb, gb, mb, _, _, fb), (p1, g1, m1, s1, _, f1) = res
     assert s0 == s1 == 3
-    # the atomics' run-to-run noise of the single-stream schedule itself,
-    # amplified by three Adam steps, sets the bar
+
     def d(a, b):
         return float((a - b).norm() / b.norm())
-    tol_g = max(1e-3, 4 * d(gb, g0))   # a race would be O(1)
-    tol_m = max(1e-3, 4 * d(mb, m0))
+    # step 1 sees identical parameters: only the atomics' summation order
+    # differs (a race would be O(1))
+    assert d(f1, f0) < max(1e-4, 8 * d(fb, f0)), (d(f1, f0), d(fb, f0))
+    # after three Adam steps the run-to-run noise is amplified by sign flips of
+    # near-zero gradients (measured 1.5e-4 .. 1.3e-3 between identical runs)
+    tol_g = max(1e-2, 8 * d(gb, g0))
+    tol_m = max(1e-2, 8 * d(mb, m0))
     assert d(g1, g0) < tol_g, (d(g1, g0), d(gb, g0))
     assert d(m1, m0) < tol_m, (d(m1, m0), d(mb, m0))
     assert float((p1 - p0).abs().max()) <= 3 * 2 * lr * 1.01
