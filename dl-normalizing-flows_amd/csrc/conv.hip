@@ -30,16 +30,6 @@ extern "C" int rnvp_stat_shards(long long M) {
     return r;
 }
 
-// selects the pre-v3 LDS-tiled split-K path for small pixel counts (A/B
-// microbenchmarks; set by rnvp_conv_set_variant)
-// (also the register-streaming kernel instead of the band kernel at the wide scales)
-static int rnvp_conv_legacy = 0;
-// pixels per wave of the streaming kernel / 16 (0: automatic; set by variant codes 11, 12, 14)
-static int rnvp_stream_tw = 0;
-// phase timestamps of the halo kernel (diagnostic builds of a measurement:
-// rnvp_conv_debug_stamps), one row of 8 s_memrealtime values per workgroup
-static unsigned long long* rnvp_conv_stamps = nullptr;
-
 namespace {
 
 template <typename T> struct Mf;
@@ -142,7 +132,6 @@ __global__ __launch_bounds__(256) void k_conv(rnvp_conv_args a, int kt_per_split
     const T* __restrict__ Wt = (const T*)a.w;
     const bool pro = a.pro_bn_relu != 0;
     const bool epi_bn = a.epi_relu_bn_bwd != 0;
-    const bool handoff = PARTIAL && a.tile_counters != nullptr;
 
     double* tmp = dsm;
     float* bnp = (float*)(dsm + 2 * max(cs, BN));   // prologue scale [cs] | shift [cs]
@@ -230,7 +219,7 @@ __global__ __launch_bounds__(256) void k_conv(rnvp_conv_args a, int kt_per_split
     // the first stage's loads are in flight while the BN tables are built
     if (kt0 < kt1) gload(kt0);
     if (pro) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + cs, nullptr, nullptr, tmp);
-    if (epi_bn && (!PARTIAL || handoff))
+    if (epi_bn && !PARTIAL)
         block_bn_table(a.epi, N, n0, BN, etab, etab + BN, etab + 2 * BN, etab + 3 * BN, tmp);
     for (int c = tid; c < BN; c += 256) btab[c] = (a.bias && n0 + c < N) ? a.bias[n0 + c] : 0.f;
     __syncthreads();   // bnp / etab / btab ready
@@ -271,46 +260,8 @@ __global__ __launch_bounds__(256) void k_conv(rnvp_conv_args a, int kt_per_split
                 if (n < cso) *(floatx4*)(ws + m * cso + n) = acc[i][j];
             }
         }
-        if (!handoff) return;
-        // In-launch hand-off: the tile's last split to arrive sums the other
-        // slabs and runs the epilogue (agent-scope release -> counter ->
-        // acquire; the counter is reset for the next launch).
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        int* flag = (int*)red;
-        if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            unsigned int* cnt = a.tile_counters + (blockIdx.y * gridDim.x + blockIdx.x);
-            const unsigned int old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int last = old == gridDim.z - 1;
-            if (last) {
-                __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            flag[0] = last;
-        }
-        __syncthreads();
-        const int last = flag[0];
-        __syncthreads();   // flag read by all before red is reused below
-        if (!last) return;
-        for (int z = 0; z < (int)gridDim.z; ++z) {
-            if (z == (int)blockIdx.z) continue;
-            const float* wz = a.ws + (long long)z * M * cso;
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                const long long m = m0 + wm * WTM + i * 16 + li;
-                if (m >= M) continue;
-#pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    const int n = n0 + wn * WTN + j * 16 + 4 * g;
-                    if (n < cso) acc[i][j] += *(const floatx4*)(wz + m * cso + n);
-                }
-            }
-        }
-    }
-    {
+        return;
+    } else {
         // ---- fused epilogue (4 channels of one pixel per lane) ----
         const bool want_sums = a.out_sums || (a.epi_relu_bn_bwd && a.epi_sums);
         double s1[TN][4], s2[TN][4];
@@ -612,12 +563,10 @@ int launch_stream(const rnvp_conv_args* a, hipStream_t s) {
 }
 
 // pixels per wave (16 * TW), picked per pixel count from measurements
-// (rnvp_stream_tw overrides for A/B runs)
 template <typename T, int NT>
 int launch_stream_tw(const rnvp_conv_args* a, hipStream_t s) {
     const long long M = (long long)a->B * a->H * a->W;
-    int tw = rnvp_stream_tw;
-    if (tw == 0) tw = M >= 4 * 64 * 1024 ? 4 : (M >= 32 * 1024 ? 2 : 1);   // measured: s1 4, s2 2
+    const int tw = M >= 4 * 64 * 1024 ? 4 : (M >= 32 * 1024 ? 2 : 1);   // measured: s1 4, s2 2
     if (tw == 1) return launch_stream<T, NT, 1>(a, s);
     if (tw == 2) return launch_stream<T, NT, 2>(a, s);
     return launch_stream<T, NT, 4>(a, s);
@@ -660,14 +609,7 @@ int launch_conv(const rnvp_conv_args* a, hipStream_t s) {
         const int kps = (nk + splits - 1) / splits;
         splits = (nk + kps - 1) / kps;
         dim3 g1((unsigned)gm, (unsigned)gn, (unsigned)splits);
-        if (a->tile_counters && gm * gn <= a->n_counters) {   // in-launch reduction
-            k_conv<T, BM, BN, WM, WN, true><<<g1, 256, shm, s>>>(*a, kps, shards);
-            RNVP_LAUNCH_CHECK();
-            return RNVP_OK;
-        }
-        rnvp_conv_args b = *a;
-        b.tile_counters = nullptr;
-        k_conv<T, BM, BN, WM, WN, true><<<g1, 256, shm, s>>>(b, kps, shards);
+        k_conv<T, BM, BN, WM, WN, true><<<g1, 256, shm, s>>>(*a, kps, shards);
         RNVP_LAUNCH_CHECK();
         dim3 g2((unsigned)((M + 15) / 16), (unsigned)((a->cs_out + 63) / 64));
         k_splitk_epi<T><<<g2, 256, 0, s>>>(*a, splits, shards);
@@ -681,265 +623,8 @@ int launch_conv(const rnvp_conv_args* a, hipStream_t s) {
 }
 
 
-// ---------------------------------------------------------------------------
-// deep-K conv for small pixel counts (scales 3-5: M = 1,024..16,384, K up to
-// 4,608): split K over the workgroup's waves instead of over workgroups
-// ---------------------------------------------------------------------------
-// Tile [BM pixels] x [64 channels] per workgroup; every wave computes the
-// whole tile over the k-steps s = wave, wave+4, ... (interleaved, so the four
-// waves read neighbouring bytes of the same pixel rows and weight rows at the
-// same time).  Operands go global -> registers in MFMA fragment layout (an A
-// fragment lane = one pixel's 16-byte channel chunk, a B fragment lane = one
-// weight row's chunk), DK k-steps in flight per wave, BN+ReLU applied in
-// registers; no LDS and no barrier in the main loop.  The four partial tiles
-// are summed through LDS and the fused epilogue (bias / residual / skip
-// accumulation / next-BN statistics, or the dgrad ReLU+BN-backward mask and
-// sums) runs in the same launch: no split-K workspace, no second kernel.
-// Blocks are mapped channel-tile-major so the blocks of one XCD (b % 8) share
-// a slice of the weight matrix in their L2.
-constexpr int DK_MAX_CS = 1024;      // prologue BN table capacity (channels)
-
-template <typename T, int BM>
-struct DkSmem {
-    static constexpr int BN = 64, PITCH = BN + 4;
-    float bnp[2 * DK_MAX_CS];                 // prologue scale | shift
-    float etab[4 * BN];                       // epilogue scale | shift | mean | rstd
-    float btab[BN];
-    double sred[4][BN][2];                    // per-wave BN-stat partials
-    union {
-        double tmp[2 * DK_MAX_CS];            // shard reduction (prologue)
-        float red[4][BM][PITCH];              // partial tiles (end)
-    } u;
-};
-
-template <typename T, int BM, int DK, bool PRO>
-__global__ __launch_bounds__(256, 2) void k_conv_dk(rnvp_conv_args a, int shards) {
-    constexpr int CH = Mf<T>::CH;
-    constexpr int KS = 4 * CH;                 // K per k-step (bf16 32, f32 16)
-    constexpr int BN = 64, TM = BM / 16, TN = BN / 16;
-    constexpr int PITCH = DkSmem<T, BM>::PITCH;
-    constexpr int FR = TM * TN / 4;            // epilogue fragments per wave
-    __shared__ DkSmem<T, BM> sm;
-
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, li = lane & 15;
-    const int M = a.B * a.H * a.W;
-    const int N = a.n, cs = a.cs_in, ks = a.ks, pad = ks >> 1;
-    const int K = ks * ks * cs;
-    const int nsteps = (K + KS - 1) / KS;
-    const int gm = (M + BM - 1) / BM, gn = (N + BN - 1) / BN;
-    // channel-tile-major, XCD-contiguous tile index (bijective remap)
-    const int nb = gridDim.x, b = blockIdx.x;
-    const int q8 = nb / 8, r8 = nb % 8, xcd = b % 8;
-    const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
-    const int nt = t / gm, mt = t - nt * gm;
-    const int m0 = mt * BM, n0 = nt * BN;
-    const T* __restrict__ X = (const T*)a.x;
-    const T* __restrict__ Wt = (const T*)a.w;
-    constexpr bool pro = PRO;
-    const bool epi_bn = a.epi_relu_bn_bwd != 0;
-
-    // A rows of this lane (fixed over K)
-    int am[TM], ay[TM], ax[TM];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-        const int m = m0 + i * 16 + li;
-        am[i] = m < M ? m : -1;
-        const int mm = m < M ? m : 0;
-        ax[i] = mm % a.W;
-        ay[i] = (mm / a.W) % a.H;
-    }
-    bool bok[TN];
-    const T* wrow[TN];   // this lane's weight rows (clamped in-bounds)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        bok[j] = n0 + j * 16 + li < N;
-        wrow[j] = Wt + (long long)(bok[j] ? n0 + j * 16 + li : 0) * a.kp;
-    }
-
-    // k-step ring
-    u32x4 ra[DK][TM], rb[DK][TN];
-    unsigned amask[DK];
-    int aci[DK];
-    const int my_steps = wid < nsteps ? (nsteps - wid + 3) / 4 : 0;
-    // Every load is unconditional (invalid lanes read a clamped, in-bounds
-    // address and are zeroed at use by a select): a load under a branch makes
-    // hipcc drain vmcnt(0) at each use, which would serialise the ring.  Steps
-    // past my_steps are "dead" (mask 0, MFMA on zeros), so the ring runs in
-    // whole groups of DK with no guard.
-    auto load = [&](int u, int it) {
-        const bool live = it < my_steps;
-        const int k = (wid + 4 * (live ? it : 0)) * KS + g * CH;
-        const int tap = k / cs, ci = k - tap * cs;
-        const int dy = tap / ks - pad, dx = tap % ks - pad;
-        aci[u] = ci;
-        unsigned mk = 0;
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            const int yy = ay[i] + dy, xx = ax[i] + dx;
-            // bitwise, not short-circuit: no control flow around the load
-            const bool ok = live & (am[i] >= 0) & (k < K) & (yy >= 0) & (yy < a.H) & (xx >= 0) & (xx < a.W);
-            const long long off = ok ? (long long)(am[i] + dy * a.W + dx) * cs + ci : 0;
-            ra[u][i] = *(const u32x4*)(X + off);
-            mk |= (ok ? 1u : 0u) << i;
-        }
-        amask[u] = mk;
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-            rb[u][j] = *(const u32x4*)(wrow[j] + k);
-    };
-    // the first DK k-steps are in flight while the tables are built
-#pragma unroll
-    for (int u = 0; u < DK; ++u) load(u, u);
-
-    if (pro) block_bn_table(a.pro, a.cin, 0, cs, sm.bnp, sm.bnp + cs, nullptr, nullptr, sm.u.tmp);
-    if (epi_bn) block_bn_table(a.epi, N, n0, BN, sm.etab, sm.etab + BN, sm.etab + 2 * BN, sm.etab + 3 * BN, sm.u.tmp);
-    for (int c = tid; c < BN; c += 256) sm.btab[c] = (a.bias && n0 + c < N) ? a.bias[n0 + c] : 0.f;
-    __syncthreads();
-
-    floatx4 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-    for (int it0 = 0; it0 < my_steps; it0 += DK) {
-#pragma unroll
-        for (int u = 0; u < DK; ++u) {
-            const int it = it0 + u;
-            u32x4 av[TM], bv[TN];
-#pragma unroll
-            for (int i = 0; i < TM; ++i) av[i] = ra[u][i];
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const uint32_t keep = bok[j] ? ~0u : 0u;
-                bv[j] = rb[u][j] & u32x4{keep, keep, keep, keep};
-            }
-            const unsigned mk = amask[u];
-            const int ci = aci[u];
-            load(u, it + DK);
-            if constexpr (pro) {
-                float sc[CH], sh[CH];
-#pragma unroll
-                for (int c = 0; c < CH; c += 4) {
-                    const floatx4 a4 = *(const floatx4*)&sm.bnp[ci + c];
-                    const floatx4 b4 = *(const floatx4*)&sm.bnp[cs + ci + c];
-                    sc[c] = a4.x; sc[c + 1] = a4.y; sc[c + 2] = a4.z; sc[c + 3] = a4.w;
-                    sh[c] = b4.x; sh[c + 1] = b4.y; sh[c + 2] = b4.z; sh[c + 3] = b4.w;
-                }
-#pragma unroll
-                for (int i = 0; i < TM; ++i) {
-                    float f[CH];
-                    unpack(av[i], f, T());
-#pragma unroll
-                    for (int c = 0; c < CH; ++c) f[c] = fmaxf(f[c] * sc[c] + sh[c], 0.f);
-                    // zero padding AFTER act, by an AND (a select here becomes a branch)
-                    const uint32_t keep = 0u - ((mk >> i) & 1u);
-                    av[i] = pack(f, T()) & u32x4{keep, keep, keep, keep};
-                }
-            } else {
-#pragma unroll
-                for (int i = 0; i < TM; ++i) {
-                    const uint32_t keep = 0u - ((mk >> i) & 1u);
-                    av[i] &= u32x4{keep, keep, keep, keep};
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j) Mf<T>::step(bv[j], av[i], acc[i][j]);
-        }
-    }
-
-    // ---- reduce the four partial tiles through LDS ----
-    __syncthreads();   // tables done with u.tmp (all waves past the prologue)
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) *(floatx4*)&sm.u.red[wid][i * 16 + li][j * 16 + 4 * g] = acc[i][j];
-    __syncthreads();
-
-    // this wave's epilogue fragments: row tile fi, column tiles fj0 .. fj0+FR-1
-    const int fi = wid % TM, fj0 = (wid / TM) * FR;
-    const int m = m0 + fi * 16 + li;
-    const int cso = a.cs_out;
-    double s1[FR][4], s2[FR][4];
-#pragma unroll
-    for (int f = 0; f < FR; ++f)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s1[f][r] = s2[f][r] = 0.f;
-    if (m < M) {
-#pragma unroll
-        for (int f = 0; f < FR; ++f) {
-            const int col = (fj0 + f) * 16 + 4 * g;
-            const int n = n0 + col;
-            if (n >= cso) continue;
-            floatx4 v = *(const floatx4*)&sm.u.red[0][fi * 16 + li][col];
-#pragma unroll
-            for (int w = 1; w < 4; ++w) v += *(const floatx4*)&sm.u.red[w][fi * 16 + li][col];
-            epi4<T>(a, (long long)m * cso + n, v, sm.btab + col, epi_bn, sm.etab + col, BN, s1[f], s2[f], N - n);
-        }
-    }
-    const bool want_sums = a.out_sums || (epi_bn && a.epi_sums);
-    if (want_sums) {
-        // reduce over the 16 pixels of the fragment, then over the waves that
-        // share a column tile (through LDS), one fp64 atomic per channel
-#pragma unroll
-        for (int f = 0; f < FR; ++f)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const double u1 = row_sum16(s1[f][r]), u2 = row_sum16(s2[f][r]);
-                if (li == 0) {
-                    const int col = (fj0 + f) * 16 + 4 * g + r;
-                    sm.sred[fi][col][0] = u1;
-                    sm.sred[fi][col][1] = u2;
-                }
-            }
-        __syncthreads();
-        double* sums = (epi_bn ? a.epi_sums : a.out_sums);
-        sums += (long long)(blockIdx.x % shards) * 2 * N;
-        for (int col = tid; col < BN; col += 256) {
-            const int n = n0 + col;
-            if (n >= N) continue;
-            double t1 = 0.0, t2 = 0.0;
-#pragma unroll
-            for (int w = 0; w < TM; ++w) {
-                t1 += sm.sred[w][col][0];
-                t2 += sm.sred[w][col][1];
-            }
-            atomicAdd(&sums[n], (double)t1);
-            atomicAdd(&sums[N + n], (double)t2);
-        }
-    }
-}
-
-template <typename T, int BM>
-int launch_dk(const rnvp_conv_args* a, hipStream_t s) {
-    const long long M = (long long)a->B * a->H * a->W;
-    const long long gm = (M + BM - 1) / BM, gn = (a->n + 63) / 64;
-    constexpr int DK = BM >= 64 ? 2 : 4;
-    if (a->pro_bn_relu)
-        k_conv_dk<T, BM, DK, true><<<(unsigned)(gm * gn), 256, 0, s>>>(*a, rnvp_stat_shards(M));
-    else
-        k_conv_dk<T, BM, DK, false><<<(unsigned)(gm * gn), 256, 0, s>>>(*a, rnvp_stat_shards(M));
-    RNVP_LAUNCH_CHECK();
-    return RNVP_OK;
-}
-
-// small pixel count, channel counts the prologue table holds
-template <typename T>
-bool dk_ok(const rnvp_conv_args* a) {
-    const long long M = (long long)a->B * a->H * a->W;
-    return M <= 16384 && a->cs_in <= DK_MAX_CS && a->n > 16;
-}
-
-template <typename T>
-int dispatch_dk(const rnvp_conv_args* a, hipStream_t s) {
-    const long long M = (long long)a->B * a->H * a->W;
-    const long long tiles64 = ((M + 63) / 64) * ((a->n + 63) / 64);
-    if (tiles64 >= 256) return launch_dk<T, 64>(a, s);
-    return launch_dk<T, 32>(a, s);
-}
-
+// prologue BN table capacity of the halo-tile kernel (channels)
+constexpr int DK_MAX_CS = 1024;
 
 // ---------------------------------------------------------------------------
 // halo-tile conv (deep scales): act(x) staged ONCE per workgroup in LDS
@@ -1028,6 +713,15 @@ __device__ __forceinline__ void tab_finish(const rnvp_bn_src& s, int C, int c0, 
 // >= 0.5 away from any multiple of d, far more than the rounding error.
 __device__ __forceinline__ int fdiv_small(int q, float r) { return (int)(((float)q + 0.5f) * r); }
 
+// floor(q / d) for 0 <= q < 2^31 with q / d < 2^22 (r = 1/d): the float
+// quotient is within 0.75 of the true one, one correction step each way.
+__device__ __forceinline__ int fdiv_exact(int q, int d, float r) {
+    int t = (int)((float)q * r);
+    t -= (t * d > q) ? 1 : 0;
+    t += ((t + 1) * d <= q) ? 1 : 0;
+    return t;
+}
+
 template <typename T, int BN>
 size_t halo_lds_bytes(int cs, int W, int ks) {
     constexpr int BM = 64, TM = BM / 16;
@@ -1042,10 +736,7 @@ size_t halo_lds_bytes(int cs, int W, int ks) {
 }
 
 template <typename T, int BN, int KSZ, bool PRO, int DK, bool UNI>
-__global__ __launch_bounds__(256) void k_conv_halo(rnvp_conv_args a, int shards, unsigned long long* stamps) {
-#define HALO_STAMP(i) do { if (stamps && threadIdx.x == 0) stamps[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-    HALO_STAMP(0);
-    if (stamps && threadIdx.x == 0) stamps[blockIdx.x * 8 + 6] = __builtin_amdgcn_s_memtime();
+__global__ __launch_bounds__(256) void k_conv_halo(rnvp_conv_args a, int shards) {
     constexpr int BM = 64;
     constexpr int CH = Mf<T>::CH, KS = 4 * CH;
     constexpr int TM = BM / 16, TN = BN / 16;
@@ -1138,7 +829,6 @@ __global__ __launch_bounds__(256) void k_conv_halo(rnvp_conv_args a, int shards,
     for (int c = tid; c < BN; c += 256) btab[c] = (a.bias && n0 + c < N) ? a.bias[n0 + c] : 0.f;
     for (int c = tid * CH; c < pitch; c += 256 * CH) *(u32x4*)(zrow + c) = u32x4{0u, 0u, 0u, 0u};
     __syncthreads();
-    HALO_STAMP(1);
 
     const T* wrow[TN];
 #pragma unroll
@@ -1165,7 +855,6 @@ __global__ __launch_bounds__(256) void k_conv_halo(rnvp_conv_args a, int shards,
         stage_store(q0);
     }
     __syncthreads();
-    HALO_STAMP(2);
 
     // ---- per-lane pixel state ----
     int rowoff[TM];      // LDS element offset of the pixel's own row
@@ -1235,10 +924,8 @@ __global__ __launch_bounds__(256) void k_conv_halo(rnvp_conv_args a, int shards,
         }
     }
 
-    HALO_STAMP(3);
     // ---- reduce the four partial tiles through LDS (aliases the act tile) ----
     __syncthreads();
-    HALO_STAMP(4);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1293,9 +980,6 @@ __global__ __launch_bounds__(256) void k_conv_halo(rnvp_conv_args a, int shards,
             atomicAdd(&sums[N + n], (double)t2);
         }
     }
-    HALO_STAMP(5);
-    if (stamps && threadIdx.x == 0) stamps[blockIdx.x * 8 + 7] = __builtin_amdgcn_s_memtime();
-#undef HALO_STAMP
 }
 
 template <typename T, int BN, int KSZ>
@@ -1308,11 +992,11 @@ int launch_halo(const rnvp_conv_args* a, hipStream_t s) {
     constexpr int DK = BN >= 64 ? 6 : 8;      // weight k-steps in flight per wave
     const unsigned grid = (unsigned)(gm * gn);
     if (a->pro_bn_relu) {
-        if (uni) k_conv_halo<T, BN, KSZ, true, DK, true><<<grid, 256, shm, s>>>(*a, sh, rnvp_conv_stamps);
-        else k_conv_halo<T, BN, KSZ, true, DK, false><<<grid, 256, shm, s>>>(*a, sh, rnvp_conv_stamps);
+        if (uni) k_conv_halo<T, BN, KSZ, true, DK, true><<<grid, 256, shm, s>>>(*a, sh);
+        else k_conv_halo<T, BN, KSZ, true, DK, false><<<grid, 256, shm, s>>>(*a, sh);
     } else {
-        if (uni) k_conv_halo<T, BN, KSZ, false, DK, true><<<grid, 256, shm, s>>>(*a, sh, rnvp_conv_stamps);
-        else k_conv_halo<T, BN, KSZ, false, DK, false><<<grid, 256, shm, s>>>(*a, sh, rnvp_conv_stamps);
+        if (uni) k_conv_halo<T, BN, KSZ, false, DK, true><<<grid, 256, shm, s>>>(*a, sh);
+        else k_conv_halo<T, BN, KSZ, false, DK, false><<<grid, 256, shm, s>>>(*a, sh);
     }
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
@@ -1618,10 +1302,10 @@ int dispatch_band(const rnvp_conv_args* a, hipStream_t s) {
 template <typename T>
 int dispatch_conv(const rnvp_conv_args* a, hipStream_t s) {
     const long long M = (long long)a->B * a->H * a->W;
-    if (rnvp_conv_legacy == 0 && band_ok<T>(a)) return dispatch_band<T>(a, s);
+    const bool tuned = a->variant == 0;
+    if (tuned && band_ok<T>(a)) return dispatch_band<T>(a, s);
     if (stream_ok<T>(a)) return dispatch_stream<T>(a, s);
-    if (rnvp_conv_legacy == 0 && halo_ok<T>(a)) return dispatch_halo<T>(a, s);
-    if (rnvp_conv_legacy == 2 && dk_ok<T>(a)) return dispatch_dk<T>(a, s);
+    if (tuned && halo_ok<T>(a)) return dispatch_halo<T>(a, s);
     // largest tile that still gives >= 512 workgroups (2 per CU); small grids
     // fall through to 64x64 tiles and split K
     if (a->n <= 16) return launch_conv<T, 128, 16, 4, 1>(a, s);
@@ -1679,7 +1363,7 @@ __device__ __forceinline__ void wgrad_tile(const WgView& a, int co0, int k0, lon
     const int pdy = ptap / ks - pad, pdx = ptap % ks - pad;
     const int pco = co0 + sc_ * CH;              // P column
     const bool colp = pco < N, colq = pk < K;
-    const float rW = 1.0f / (float)W, rH = 1.0f / (float)H;   // pixel decode (M < 2^22, host-checked)
+    const float rW = 1.0f / (float)W, rH = 1.0f / (float)H;   // pixel decode (M / W < 2^22, host-checked)
     const int nst = mb < me ? (int)((me - mb + STG - 1) / STG) : 0;
     const int mfirst = nst > 0 ? (int)mb : 0;
 
@@ -1703,8 +1387,8 @@ __device__ __forceinline__ void wgrad_tile(const WgView& a, int co0, int k0, lon
             const long long m = mt + r;
             const bool inm = m < me;
             const int mi = inm ? (int)m : mfirst;
-            const int row = fdiv_small(mi, rW);
-            const int xx = mi - row * W, yy = row - fdiv_small(row, rH) * H;
+            const int row = fdiv_exact(mi, W, rW);
+            const int xx = mi - row * W, yy = row - fdiv_exact(row, H, rH) * H;
             const int y2 = yy + pdy, x2 = xx + pdx;
             const bool okq = inm & colq & (y2 >= 0) & (y2 < H) & (x2 >= 0) & (x2 < W);
             rp[u][i] = *(const u32x4*)(DY + (long long)mi * a.cs_dy + (colp ? pco : 0));
@@ -1840,37 +1524,6 @@ __device__ __forceinline__ void wgrad_tile(const WgView& a, int co0, int k0, lon
         if (bias_atomic) atomicAdd(&bias_out[co0 + tid], dbs[tid]);
         else bias_out[co0 + tid] = dbs[tid];
     }
-}
-
-template <typename T>
-__global__ __launch_bounds__(256) void k_wgrad(rnvp_wgrad_args a, long long m_per_block) {
-    const long long M = (long long)a.B * a.H * a.W;
-    const long long mb = (long long)blockIdx.z * m_per_block;
-    const long long me = (mb + m_per_block < M) ? mb + m_per_block : M;
-    const WgView v{a.x, a.dy, a.pro, a.H, a.W, a.ks, a.cs_in, a.cin, a.cs_dy, a.n, a.kp, a.pro_bn_relu};
-    wgrad_tile<T>(v, blockIdx.x * 64, blockIdx.y * 64, mb, me, M, a.dw, true,
-                  (a.dbias && blockIdx.y == 0) ? a.dbias : nullptr, true);
-}
-
-template <typename T>
-int launch_wgrad(const rnvp_wgrad_args* a, hipStream_t s) {
-    constexpr int STG = (sizeof(T) == 2) ? 64 : 32;
-    const long long M = (long long)a->B * a->H * a->W;
-    const int K = a->ks * a->ks * a->cs_in;
-    const int tco = (a->n + 63) / 64, tk = (K + 63) / 64;
-    long long steps = (M + STG - 1) / STG;
-    // enough blocks to fill the chip, but at most 128 fp32 adders per dw word
-    long long z = (1024 + tco * tk - 1) / (tco * tk);
-    if (z > 128) z = 128;
-    if (z < 1) z = 1;
-    if (z > steps) z = steps;
-    long long mpb = ((steps + z - 1) / z) * STG;
-    z = (M + mpb - 1) / mpb;
-    dim3 grid((unsigned)tco, (unsigned)tk, (unsigned)z);
-    size_t shm = 24 * (size_t)a->cs_in;
-    k_wgrad<T><<<grid, 256, shm, s>>>(*a, mpb);
-    RNVP_LAUNCH_CHECK();
-    return RNVP_OK;
 }
 
 // grouped: block -> (conv, slab z, co tile, k tile).  Consecutive tasks (the
@@ -2162,6 +1815,7 @@ inline bool al16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
 
 extern "C" int rnvp_conv2d(const rnvp_conv_args* a, void* stream) {
     if (!a || !a->x || !a->w || !a->y) return RNVP_E_INVALID;
+    if (a->variant < 0 || a->variant > 1) return RNVP_E_INVALID;
     if (a->dtype != RNVP_F32 && a->dtype != RNVP_BF16) return RNVP_E_INVALID;
     if (a->ks != 1 && a->ks != 3) return RNVP_E_UNSUPPORTED;
     if (a->B < 0 || a->H <= 0 || a->W <= 0 || a->n <= 0 || a->cin <= 0) return RNVP_E_INVALID;
@@ -2173,36 +1827,6 @@ extern "C" int rnvp_conv2d(const rnvp_conv_args* a, void* stream) {
     if (a->B == 0) return RNVP_OK;
     hipStream_t s = (hipStream_t)stream;
     return a->dtype == RNVP_F32 ? dispatch_conv<float>(a, s) : dispatch_conv<bf16_t>(a, s);
-}
-
-extern "C" int rnvp_conv_debug_stamps(unsigned long long* device_buf) {
-    rnvp_conv_stamps = device_buf;
-    return RNVP_OK;
-}
-
-extern "C" int rnvp_conv_set_variant(int legacy) {
-    if (legacy >= 10) {   // streaming-kernel tile override, default kernels otherwise
-        rnvp_stream_tw = legacy - 10;
-        rnvp_conv_legacy = 0;
-        return RNVP_OK;
-    }
-    rnvp_stream_tw = 0;
-    rnvp_conv_legacy = legacy;
-    return RNVP_OK;
-}
-
-extern "C" int rnvp_conv2d_wgrad(const rnvp_wgrad_args* a, void* stream) {
-    if (!a || !a->x || !a->dy || !a->dw) return RNVP_E_INVALID;
-    if (a->dtype != RNVP_F32 && a->dtype != RNVP_BF16) return RNVP_E_INVALID;
-    if (a->ks != 1 && a->ks != 3) return RNVP_E_UNSUPPORTED;
-    if (a->B < 0 || a->H <= 0 || a->W <= 0 || a->n <= 0 || a->cin <= 0) return RNVP_E_INVALID;
-    if ((a->cs_in & 7) || (a->cs_dy & 7) || a->cs_in < a->cin || a->cs_dy < a->n) return RNVP_E_INVALID;
-    if (a->kp < a->ks * a->ks * a->cs_in) return RNVP_E_INVALID;
-    if (!al16(a->x) || !al16(a->dy)) return RNVP_E_INVALID;
-    if ((long long)a->B * a->H * a->W >= (1ll << 22)) return RNVP_E_UNSUPPORTED;
-    if (a->B == 0) return RNVP_OK;
-    hipStream_t s = (hipStream_t)stream;
-    return a->dtype == RNVP_F32 ? launch_wgrad<float>(a, s) : launch_wgrad<bf16_t>(a, s);
 }
 
 extern "C" int rnvp_wgrad_slabs(long long M) {
@@ -2223,7 +1847,7 @@ extern "C" int rnvp_conv2d_wgrad_grouped(const rnvp_wgrad_group* gin, void* stre
     rnvp_wgrad_group g = *gin;
     const long long M = (long long)g.B * g.H * g.W;
     const int STG = g.dtype == RNVP_BF16 ? 64 : 32;
-    if (M >= (1ll << 22)) return RNVP_E_UNSUPPORTED;
+    if (M >= (1ll << 31) || M / g.W >= (1ll << 22)) return RNVP_E_UNSUPPORTED;
     long long tasks = 0;
     int max_cs = 8;
     for (int c = 0; c < g.n_conv; ++c) {

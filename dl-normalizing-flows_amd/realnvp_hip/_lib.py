@@ -37,15 +37,7 @@ class ConvArgs(C.Structure):
                 ("pro_bn_relu", i32), ("pro", BNSrc),
                 ("out_sums", vp),
                 ("epi_relu_bn_bwd", i32), ("epi_x", vp), ("epi", BNSrc), ("epi_sums", vp),
-                ("ws", vp), ("ws_elems", i64), ("tile_counters", vp), ("n_counters", i32)]
-
-
-class WgradArgs(C.Structure):
-    _fields_ = [("dtype", i32), ("B", i32), ("H", i32), ("W", i32), ("ks", i32),
-                ("x", vp), ("cs_in", i32), ("cin", i32),
-                ("pro_bn_relu", i32), ("pro", BNSrc),
-                ("dy", vp), ("cs_dy", i32), ("n", i32),
-                ("dw", vp), ("kp", i32), ("dbias", vp)]
+                ("ws", vp), ("ws_elems", i64), ("variant", i32)]
 
 
 class BNBwdArgs(C.Structure):
@@ -118,9 +110,6 @@ _SIGS = {
     "rnvp_bn_running_update": (i32, [vp, i32, i32, f32, vp]),
     "rnvp_stat_shards": (i32, [i64]),
     "rnvp_conv2d": (i32, [C.POINTER(ConvArgs), vp]),
-    "rnvp_conv_set_variant": (i32, [i32]),
-    "rnvp_conv_debug_stamps": (i32, [vp]),
-    "rnvp_conv2d_wgrad": (i32, [C.POINTER(WgradArgs), vp]),
     "rnvp_wgrad_slabs": (i32, [i64]),
     "rnvp_wgrad_replicas": (i32, [i32]),
     "rnvp_conv2d_wgrad_grouped": (i32, [C.POINTER(WgradGroup), vp]),

@@ -120,21 +120,6 @@ def splitk_workspace(device, elems):
     return t
 
 
-_COUNTERS = {}
-N_COUNTERS = 1 << 16
-
-
-def tile_counters(device):
-    """Per-device zeroed uint32 hand-off counters of the in-launch split-K
-    reduction (every use leaves them zero)."""
-    key = str(device)
-    t = _COUNTERS.get(key)
-    if t is None:
-        t = torch.zeros(N_COUNTERS, dtype=torch.int32, device=device)
-        _COUNTERS[key] = t
-    return t
-
-
 def splitk_elems(M, nmax):
     return 8 * M * nmax if M <= 16384 else 0
 
@@ -320,7 +305,7 @@ class CouplingEngine:
         sc = dict(arena=ar, zero=zr, wn_table=torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(device),
                   wn_key=wsz["key"], wn_rows=wsz["rows"], n_wn=len(descs), shards=sh,
                   ws=splitk_workspace(device, wse) if wse else None, ws_elems=wse,
-                  wg=wg, wg_nz=nz, wg_nrep=nrep, wg_ws=wgws, counters=tile_counters(device))
+                  wg=wg, wg_nz=nz, wg_nrep=nrep, wg_ws=wgws)
         self._scratch[key] = sc
         return sc
 
@@ -487,8 +472,9 @@ class CouplingEngine:
         a.g_scale, a.g_scale_shift = gp("scale"), gp("scale_shift")
         L.coupling_out_bwd(C.byref(a), s)
 
-        grp = WgradGroup()
-        grp.dtype, grp.B, grp.H, grp.W = dt, B, H, W
+        # grouped weight gradients: one launch per WGRAD_GROUP_MAX convs (the
+        # group travels as a by-value kernel argument); R >= 6 nets have more
+        groups = []
         wg_bytes = wg_flops = 0.0
         wbase = sc["wg_ws"].data_ptr()
         for st in self.steps:
@@ -532,8 +518,11 @@ class CouplingEngine:
                 nb = esz * M * cs_in * (3 + int(bool(st.residual)) + int(st.accumulate))
                 _launch("bn_bwd", nb, 0.0, L.bn_bwd_apply, C.byref(c), s)
             else:
-                if grp.n_conv >= WGRAD_GROUP_MAX:
-                    raise RuntimeError("grouped wgrad: more than %d convs" % WGRAD_GROUP_MAX)
+                if not groups or groups[-1].n_conv >= WGRAD_GROUP_MAX:
+                    grp = WgradGroup()
+                    grp.dtype, grp.B, grp.H, grp.W = dt, B, H, W
+                    groups.append(grp)
+                grp = groups[-1]
                 c = grp.conv[grp.n_conv]
                 grp.n_conv += 1
                 ow, ob = sc["wg"][op.conv]
@@ -561,8 +550,9 @@ class CouplingEngine:
         # optimizer update).
         def weight_grads():
             ss = stream_ptr()
-            if grp.n_conv:
-                _launch("conv_wgrad", wg_bytes, wg_flops, L.conv2d_wgrad_grouped, C.byref(grp), ss)
+            for grp in groups:
+                _launch("conv_wgrad", wg_bytes / len(groups), wg_flops / len(groups), L.conv2d_wgrad_grouped,
+                        C.byref(grp), ss)
             L.weight_norm_bwd(sc["wn_table"].data_ptr(), sc["n_wn"], sc["wn_rows"], gbase, ss)
             if after is not None:
                 after()

@@ -72,8 +72,10 @@ def coupling_reverse(mod, x):
     _check_device(x, type(mod).__name__)
     if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in mod.parameters())):
         # sampling is a no-grad path in the reference loop (train.py:253-259);
-        # gradients through the inverse are not part of the engine.
-        pass
+        # the engine's inverse has no backward, so refuse rather than return
+        # outputs that silently carry no gradient.
+        raise RuntimeError("%s(reverse=True): the MI355X engine's inverse pass is not differentiable; run it under "
+                           "torch.no_grad() (as train.py:253-259 does)" % type(mod).__name__)
     with torch.no_grad():
         out, ldj = mod.engine().reverse(x.contiguous(), mod.training, mod.compute_dtype)
     return out, ldj

@@ -13,9 +13,13 @@ MI355X-specific structure:
   * every buffer is allocated once; the whole step is captured into a HIP
     graph and replayed (no per-kernel host cost);
   * data parallel: one process per GPU, batch slice per rank, gradient
-    arena all-reduced (average) over RCCL in buckets between the backward
-    graph and the optimizer graph.  BatchNorm statistics stay per rank
-    (= the reference's semantics for each 64-image shard).
+    arena averaged over RCCL in ~25 MB buckets that are issued on a
+    communication stream as soon as backward has finished them (the deep
+    scales, 86 % of the parameters, finish first), overlapping the
+    remaining backward; optionally reduced in bf16.  BatchNorm statistics
+    stay per rank (= the reference's semantics for each 64-image shard).
+  * optimizer state converts to / from torch.optim.Adam.state_dict() format
+    (train.py:139-154, 249-250 checkpoints).
 """
 import math
 
@@ -26,9 +30,34 @@ from . import _lib
 from .engine import stream_ptr
 
 
+def arena_blocks(model):
+    """(offset, numel) of each coupling's parameters in the flat arena
+    (named_parameters() order), couplings in forward order."""
+    offs = {}
+    off = 0
+    for n, p in model.named_parameters():
+        offs[n] = off
+        off += p.numel()
+    names = {id(m): n for n, m in model.named_modules()}
+    out = []
+    for mod in model.couplings():
+        pre = names[id(mod)] + "."
+        first = next(n for n, _ in mod.named_parameters())
+        out.append((offs[pre + first], sum(p.numel() for p in mod.parameters())))
+    return out
+
+
+def bucket_plan(model, bucket_elems, n_total):
+    """The trainer's all-reduce buckets for this model (dist.bucket_schedule
+    over the coupling blocks in backward order)."""
+    from .dist import bucket_schedule
+    return bucket_schedule(list(reversed(arena_blocks(model))), bucket_elems, n_total)
+
+
 class FlowTrainer:
     def __init__(self, model, batch_size, lr=5e-4, weight_decay=5e-5, betas=(0.9, 0.999), eps=1e-8,
-                 scale_reg=5e-5, dtype="bf16", seed=0, process_group=None, bucket_mb=64, overlap=False):
+                 scale_reg=5e-5, dtype="bf16", seed=0, process_group=None, bucket_mb=25, overlap=False,
+                 comm="overlap", reduce_dtype="fp32"):
         self.model = model
         self.dev = next(model.parameters()).device
         if self.dev.type != "cuda":
@@ -44,14 +73,24 @@ class FlowTrainer:
         self._build_plan()
         self.graph = None
         self.graph_opt = None
+        self.graph_input = None
         self.external_input = False
         self.bucket_elems = max(1, int(bucket_mb * 2 ** 20 // 4))
+        if comm not in ("overlap", "split"):
+            raise ValueError("comm must be 'overlap' or 'split'")
+        if reduce_dtype not in ("fp32", "bf16"):
+            raise ValueError("reduce_dtype must be 'fp32' or 'bf16'")
+        self.comm, self.reduce_dtype = comm, reduce_dtype
+        self.comm_stream = None
+        if self.pg is not None and comm == "overlap":
+            self.comm_stream = torch.cuda.Stream(device=self.dev)
         # side stream: weight gradients, weight-norm of the late couplings and
         # (single process) the per-coupling optimizer update run beside the
         # critical path (the forward/data-gradient chain)
         self.overlap = overlap
         self.side = torch.cuda.Stream(device=self.dev) if overlap else None
         self._build_adam_ranges()
+        self._build_buckets()
 
     # ----------------------------------------------------------------- arenas
     def _build_arenas(self):
@@ -177,6 +216,28 @@ class FlowTrainer:
         ends = offs[1:] + [self.n]
         self.adam_ranges = [(ru(o), (ru(e) if e < self.n else self.n)) for o, e in zip(offs, ends)]
 
+    def _build_buckets(self):
+        """All-reduce buckets in backward order (dist.bucket_schedule over the
+        couplings' gradient blocks); bucket k is issued right after coupling
+        bucket_after[k]'s backward has been scheduled."""
+        blocks = [st[6] for st in self.stages if st[0] == "coupling"]
+        base = self.grad.data_ptr()
+        spans = [((b.data_ptr() - base) // 4, b.numel()) for b in blocks]
+        if spans != arena_blocks(self.model):
+            raise RuntimeError("coupling gradient blocks do not follow the parameter arena")
+        self.buckets = bucket_plan(self.model, self.bucket_elems, self.n)
+        self.bucket_after = {}
+        for lo, hi, k in self.buckets:
+            self.bucket_after.setdefault(k, []).append((lo, hi))
+        self.reduce_buf = None
+        if self.pg is not None and self.reduce_dtype == "bf16":
+            self.reduce_buf = torch.empty(self.n, device=self.dev, dtype=torch.bfloat16)
+
+    def _reduce_bucket(self, lo, hi):
+        """Average grad[lo:hi) over the process group (on the current stream)."""
+        from .dist import average_slice
+        average_slice(self.grad, lo, hi, self.pg, self.reduce_buf)
+
     def _add_coupling(self, mod, x):
         eng = mod.engine()
         B, C, H, W = x.shape
@@ -254,7 +315,8 @@ class FlowTrainer:
         B = self.B
         gz = self._g(self.z)
         L.prior_logprob_bwd(self.z.data_ptr(), self.g_lp.data_ptr(), gz.data_ptr(), B, self.z[0].numel(), s)
-        ci = sum(1 for st in self.stages if st[0] == "coupling")
+        n_coupling = sum(1 for st in self.stages if st[0] == "coupling")
+        ci = n_coupling
         for st in reversed(self.stages):
             if st[0] == "coupling":
                 ci -= 1
@@ -264,6 +326,15 @@ class FlowTrainer:
                     lo, hi = self.adam_ranges[ci]
                     after = (lambda lo=lo, hi=hi: self._adam_range(lo, hi))
                 eng.backward(sv, self._g(z), None, self.g_lp, block, gx=self._g(x), side=self.side, after=after)
+                if self.comm_stream is not None:
+                    for lo, hi in self.bucket_after.get(n_coupling - 1 - ci, ()):
+                        # the bucket's weight gradients were written on the side
+                        # stream (overlap) or the current one
+                        ev = torch.cuda.Event()
+                        ev.record(self.side if self.side is not None else torch.cuda.current_stream())
+                        self.comm_stream.wait_event(ev)
+                        with torch.cuda.stream(self.comm_stream):
+                            self._reduce_bucket(lo, hi)
             elif st[0] == "squeeze":
                 _, a, b = st
                 L.undo_squeeze(self._g(b).data_ptr(), self._g(a).data_ptr(), *a.shape, s)
@@ -298,10 +369,12 @@ class FlowTrainer:
                              self.wd, self.mask.data_ptr(), self.reg, stream_ptr())
 
     def _allreduce(self):
-        if self.pg is None:
+        """Whole-arena bucketed average ("split" mode: between the captured
+        forward/backward graph and the optimizer graph)."""
+        if self.pg is None or self.comm_stream is not None:
             return
-        from .dist import allreduce_average
-        allreduce_average(self.grad, self.pg, self.bucket_elems)
+        for lo, hi, _ in self.buckets:
+            self._reduce_bucket(lo, hi)
 
     def _fwd_bwd(self):
         self.grad.zero_()
@@ -309,14 +382,45 @@ class FlowTrainer:
         self._backward()
         if self.side is not None:
             torch.cuda.current_stream().wait_stream(self.side)
+        if self.comm_stream is not None:
+            torch.cuda.current_stream().wait_stream(self.comm_stream)
 
     def step_eager(self):
         self._fwd_bwd()
         self._allreduce()
         self._optimizer()
 
-    def capture(self, warmup=2):
-        """Warm up eagerly on a side stream, then capture the step into HIP graphs."""
+    # --------------------------------------------------------------- graphs
+    def _snapshot(self):
+        bufs = {n: b.detach().clone() for n, b in self.model.named_buffers()}
+        return (self.param.clone(), self.exp_avg.clone(), self.exp_avg_sq.clone(), self.step_t.clone(),
+                self.ll_acc.clone(), bufs)
+
+    def _restore(self, snap):
+        p, m, v, t, ll, bufs = snap
+        with torch.no_grad():
+            self.param.copy_(p)
+            self.exp_avg.copy_(m)
+            self.exp_avg_sq.copy_(v)
+            self.step_t.copy_(t)
+            self.ll_acc.copy_(ll)
+            for n, b in self.model.named_buffers():
+                b.copy_(bufs[n])
+
+    def capture(self, warmup=2, restore=True):
+        """Warm up eagerly on a side stream, then capture the step into HIP
+        graphs.  The warm-up steps move the parameters, Adam moments, step
+        counter (and with it the dequantisation noise) and BN running stats;
+        with restore=True (default) all of that is put back afterwards, so
+        the first replay is the caller's first training step.  The input mode
+        (set_pixels: logit transform inside the graph, or set_input: an
+        already transformed batch) is fixed at capture.
+
+        Single process, and data parallel with comm="overlap": ONE graph
+        holds forward, backward, the bucketed all-reduces on the
+        communication stream and Adam.  comm="split": forward/backward graph,
+        eager all-reduce, optimizer graph."""
+        snap = self._snapshot() if restore else None
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -325,7 +429,9 @@ class FlowTrainer:
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        if self.pg is None:
+        self.graph_opt = None
+        self.graph_input = self.external_input
+        if self.pg is None or self.comm_stream is not None:
             with torch.cuda.graph(self.graph):
                 self._fwd_bwd()
                 self._optimizer()
@@ -336,6 +442,13 @@ class FlowTrainer:
             with torch.cuda.graph(self.graph_opt):
                 self._optimizer()
         torch.cuda.synchronize()
+        if snap is not None:
+            self._restore(snap)
+            torch.cuda.synchronize()
+        return warmup
+
+    def drop_graph(self):
+        self.graph = self.graph_opt = self.graph_input = None
 
     def step(self):
         if self.graph is None:
@@ -345,15 +458,90 @@ class FlowTrainer:
             self._allreduce()
             self.graph_opt.replay()
 
+    def _check_mode(self, external):
+        if self.graph is not None and self.graph_input != external:
+            raise RuntimeError("the captured step reads %s; call drop_graph() (or capture again) before feeding "
+                               "%s" % ("set_input() batches" if self.graph_input else "set_pixels() pixels",
+                                       "set_input() batches" if external else "set_pixels() pixels"))
+
     def set_pixels(self, pix):
+        """Raw pixels in [0, 1]; the step applies logit_transform on the device."""
+        self._check_mode(False)
         self.external_input = False
         self.pix.copy_(pix)
 
     def set_input(self, x, logdet):
         """Feed an already logit-transformed batch (parity tests)."""
+        self._check_mode(True)
         self.external_input = True
         self.xl.copy_(x)
         self.logdet.copy_(logdet)
+
+    # ------------------------------------------------------- checkpointing
+    def _param_list(self):
+        return list(self.model.named_parameters())
+
+    def optimizer_state_dict(self):
+        """The fused Adam's state as torch.optim.Adam(model.parameters(),
+        lr, betas, eps, weight_decay).state_dict() would hold it (the
+        reference's realnvp_state_optim.pt, train.py:250): per trainable
+        parameter index exp_avg / exp_avg_sq / step; frozen parameters (no
+        gradient, skipped by torch's Adam) carry no state."""
+        step = float(self.step_t.item())
+        state = {}
+        named = self._param_list()
+        for i, (n, p) in enumerate(named):
+            if not p.requires_grad or step == 0:
+                continue
+            off, k = self.offsets[n], p.numel()
+            state[i] = {"step": torch.tensor(step),
+                        "exp_avg": self.exp_avg[off:off + k].view_as(p).clone(),
+                        "exp_avg_sq": self.exp_avg_sq[off:off + k].view_as(p).clone()}
+        group = {"lr": self.lr, "betas": tuple(self.betas), "eps": self.eps, "weight_decay": self.wd,
+                 "amsgrad": False, "maximize": False, "foreach": None, "capturable": False,
+                 "differentiable": False, "fused": None, "decoupled_weight_decay": False,
+                 "params": list(range(len(named)))}
+        return {"state": state, "param_groups": [group]}
+
+    def load_optimizer_state_dict(self, sd):
+        """Inverse of optimizer_state_dict (accepts what torch.optim.Adam
+        saved for model.parameters(); train.py:149-154)."""
+        named = self._param_list()
+        groups = sd["param_groups"]
+        idx = [i for g in groups for i in g["params"]]
+        if len(idx) != len(named):
+            raise ValueError("optimizer state has %d parameters, the model %d" % (len(idx), len(named)))
+        g0 = groups[0]
+        if g0.get("amsgrad") or g0.get("maximize") or g0.get("decoupled_weight_decay"):
+            raise ValueError("only plain Adam with coupled weight decay is supported (train.py:134)")
+        steps = set()
+        with torch.no_grad():
+            self.exp_avg.zero_()
+            self.exp_avg_sq.zero_()
+            for pos, (n, p) in zip(idx, named):
+                st = sd["state"].get(pos)
+                if st is None:
+                    continue
+                off, k = self.offsets[n], p.numel()
+                self.exp_avg[off:off + k].copy_(st["exp_avg"].reshape(-1))
+                self.exp_avg_sq[off:off + k].copy_(st["exp_avg_sq"].reshape(-1))
+                steps.add(float(st["step"]))
+        if len(steps) > 1:
+            raise ValueError("per-parameter Adam step counts differ: %s" % sorted(steps))
+        self.step_t.fill_(int(steps.pop()) if steps else 0)
+        self.lr, self.betas, self.eps, self.wd = g0["lr"], tuple(g0["betas"]), g0["eps"], g0["weight_decay"]
+        if self.graph is not None:
+            self.drop_graph()    # lr / betas are baked into the captured launches
+
+    def state_dict(self):
+        """{'model': model.state_dict(), 'optimizer': torch-Adam-format state}
+        (the two files train.py:249-250 writes)."""
+        return {"model": self.model.state_dict(), "optimizer": self.optimizer_state_dict()}
+
+    def load_state_dict(self, sd):
+        with torch.no_grad():
+            self.model.load_state_dict(sd["model"])
+        self.load_optimizer_state_dict(sd["optimizer"])
 
     def reset_optimizer(self):
         self.exp_avg.zero_()

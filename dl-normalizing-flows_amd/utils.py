@@ -1,5 +1,6 @@
-"""Drop-in for the reference ``utils`` module (utils.py:33-93): the
-``Hyperparameters`` holder and ``logit_transform``.
+"""Drop-in for the reference ``utils`` module (utils.py:33-113): the
+``Hyperparameters`` holder, ``logit_transform`` and ``weights_init`` (the
+DCGAN initialiser train.py:37-41 imports next to them).
 
 logit_transform runs as one fused HIP kernel (dequantisation noise, affine
 squash to [0.05, 0.95], logit, per-sample log-det).  Differences from the
@@ -16,7 +17,7 @@ import torch
 from realnvp_hip import _lib
 from realnvp_hip.engine import stream_ptr
 
-__all__ = ["Hyperparameters", "logit_transform"]
+__all__ = ["Hyperparameters", "logit_transform", "weights_init"]
 
 
 class Hyperparameters():
@@ -63,3 +64,17 @@ def logit_transform(x, constraint=0.9, reverse=False, noise=None, seed=None):
     L.logit_fwd(x.data_ptr(), nptr, seed, 0, None, float(constraint), y.data_ptr(), logdet.data_ptr(), B, n,
                 stream_ptr())
     return y, logdet
+
+
+def weights_init(m):
+    """utils.py:98-113 (DCGAN initialiser, kept so train.py's import line
+    works unchanged): N(0, 0.02) conv weights, N(1, 0.02) / 0 BatchNorm
+    affine parameters.  Plain torch init on the module's own device (the
+    reference's trailing .cuda() calls return copies that are discarded)."""
+    import torch.nn as nn
+    classname = m.__class__.__name__
+    if classname.find("Conv") != -1:
+        nn.init.normal_(m.weight.data, 0.0, 0.02)
+    elif classname.find("BatchNorm") != -1:
+        nn.init.normal_(m.weight.data, 1.0, 0.02)
+        nn.init.constant_(m.bias.data, 0)

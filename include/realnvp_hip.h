@@ -107,7 +107,10 @@ int rnvp_bn_running_update(const rnvp_bn_running* descs_device, int n, int max_c
  * with rnvp_stat_shards(B*H*W) shards and must be zeroed by the caller.
  * Small grids split K over workgroups when a workspace is given
  * (ws: fp32, >= splits * M * n elements; the epilogue then runs in a second
- * kernel that reduces the splits). */
+ * kernel that reduces the splits).
+ * variant: 0 = automatic kernel choice per shape; 1 = the generic LDS-tiled
+ * implicit GEMM (+ split-K) wherever the streaming kernel does not apply
+ * (per call: used by the parity tests to cross-check the kernel families). */
 typedef struct rnvp_conv_args {
     int dtype;
     int B, H, W, ks;
@@ -121,35 +124,9 @@ typedef struct rnvp_conv_args {
     double* out_sums;
     int epi_relu_bn_bwd; const void* epi_x; rnvp_bn_src epi; double* epi_sums;
     float* ws; long long ws_elems;      /* split-K workspace (optional) */
-    unsigned int* tile_counters;        /* split-K hand-off counters, zero on entry and left
-                                           zero (optional: without them a separate reduce
-                                           launch runs the epilogue) */
-    int n_counters;
+    int variant;
 } rnvp_conv_args;
 int rnvp_conv2d(const rnvp_conv_args* a, void* stream);
-/* kernel family for small pixel counts: 0 = halo tile (default: the
- * workgroup's BN+ReLU'd input rows staged once in LDS, K split over its
- * waves, one launch), 1 = the LDS-tiled kernel with split-K over workgroups
- * (+ reduce launch), 2 = deep-K with register operands.  Process-wide; for
- * A/B measurements. */
-int rnvp_conv_set_variant(int legacy);
-/* diagnostics: when device_buf != NULL the halo-tile conv writes 8
- * s_memrealtime stamps (100 MHz) per workgroup at its phase boundaries
- * (start, tables, staging, K loop, reduction, end) to device_buf[wg*8 + i]. */
-int rnvp_conv_debug_stamps(unsigned long long* device_buf);
-
-/* weight gradient: dw[n, k] += sum_m dy[m, n] * act(x)[m + tap(k), ci(k)]
- * (fp32 atomics, dw must be zeroed by the caller), dbias[n] += sum_m dy[m, n]. */
-typedef struct rnvp_wgrad_args {
-    int dtype;
-    int B, H, W, ks;
-    const void* x; int cs_in; int cin;
-    int pro_bn_relu; rnvp_bn_src pro;
-    const void* dy; int cs_dy; int n;
-    float* dw; int kp;
-    float* dbias;
-} rnvp_wgrad_args;
-int rnvp_conv2d_wgrad(const rnvp_wgrad_args* a, void* stream);
 
 /* grouped weight gradient: the wgrads of every conv of one coupling's s/t
  * network in ONE launch (they are independent of each other once the

@@ -14,8 +14,14 @@ def _phase(name: str) -> float:
     return (zlib.crc32(name.encode()) % 10007) / 10007.0 * 6.283185307179586
 
 
+_DEVICE = None   # formula_state(..., device=d): evaluate the sinusoids there (big models)
+
+
 def _wave(name, shape, freq, amp, offset):
     n = int(np.prod(shape)) if len(shape) else 1
+    if _DEVICE is not None:
+        i = torch.arange(n, dtype=torch.float64, device=_DEVICE)
+        return (offset + amp * torch.sin(freq * i + _phase(name))).float().reshape(shape)
     i = np.arange(n, dtype=np.float64)
     v = offset + amp * np.sin(freq * i + _phase(name))
     return torch.from_numpy(v.astype(np.float32)).reshape(shape)
@@ -49,12 +55,21 @@ def formula_value(name: str, shape, trainable: bool) -> torch.Tensor:
     raise KeyError(name)
 
 
-def formula_state(module: torch.nn.Module):
-    """A full state dict for ``module`` (reference or engine: same keys)."""
+def formula_state(module: torch.nn.Module, device=None):
+    """A full state dict for ``module`` (reference or engine: same keys).
+    device: evaluate on that torch device (float64 sin, rounded to float32 --
+    equal to the numpy path up to the last float32 bit of a few elements;
+    used for the 0.9 B-parameter config-3 model)."""
+    global _DEVICE
     trainable = {n for n, p in module.named_parameters() if p.requires_grad}
     out = {}
-    for k, v in module.state_dict().items():
-        out[k] = formula_value(k, v.shape, k in trainable).to(v.dtype)
+    _DEVICE = device
+    try:
+        for k, v in module.state_dict().items():
+            t = formula_value(k, v.shape, k in trainable)
+            out[k] = (t.to(device) if device is not None else t).to(v.dtype)
+    finally:
+        _DEVICE = None
     return out
 
 

@@ -113,3 +113,17 @@ def test_backward_program_is_well_formed():
                     if s.gx:
                         written.add(s.gx)
                 assert "g:h0" in written
+
+
+def test_reference_train_py_import_line():
+    """train.py:37-41 imports these names from the drop-in modules unchanged."""
+    import torch.nn as nn
+    from flow_realnvp import RealNVP  # noqa: F401
+    from modules_realnvp import ChannelwiseAffineCoupling, CheckerboardAffineCoupling  # noqa: F401
+    from utils import Hyperparameters, logit_transform, weights_init  # noqa: F401
+    torch.manual_seed(0)
+    conv, bn = nn.Conv2d(3, 4, 3), nn.BatchNorm2d(4)
+    weights_init(conv)
+    weights_init(bn)
+    assert abs(float(conv.weight.std()) - 0.02) < 0.01
+    assert float(bn.bias.abs().max()) == 0.0 and abs(float(bn.weight.mean()) - 1.0) < 0.02

@@ -114,13 +114,10 @@ def run_case(B, H, W, cin, cout, ks, dtype, pro=False, residual=False, acc=False
         a.epi_relu_bn_bwd, a.epi_x, a.epi, a.epi_sums = 1, dex.data_ptr(), src, osums.data_ptr()
     ws = splitk_workspace(DEV, 8 * M * max(cso, csi) if M <= 16384 else 1)
     a.ws, a.ws_elems = ws.data_ptr(), ws.numel()
+    a.variant = variant
     L = _lib.lib()
-    L.conv_set_variant(variant)
-    try:
-        L.conv2d(C.byref(a), torch.cuda.current_stream().cuda_stream)
-        torch.cuda.synchronize()
-    finally:
-        L.conv_set_variant(0)
+    L.conv2d(C.byref(a), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
     full = dy.float().cpu()
     got = full.double()[:, :cout]
     assert torch.count_nonzero(full[:, cout:]) == 0, "channel padding must stay zero"
@@ -168,6 +165,21 @@ CASES = [
     ("s1_out_band", 8, 64, 64, 32, 6, 1, dict(pro=True)),
     ("s2_1x1_band_odd", 32, 32, 32, 60, 40, 1, dict(pro=True, stats=True)),
     ("band_ragged_m", 9, 61, 61, 24, 16, 3, dict(pro=True, stats=True)),                 # M % 256 != 0, odd W
+    # config 3's widest convs (mid 1024 at 2x2 / 4x4)
+    ("c3_1024_3x3_pro_stats", 16, 2, 2, 1024, 1024, 3, dict(pro=True, stats=True, bias=False)),
+    ("c3_1024_1x1_pro_res", 16, 4, 4, 1024, 1024, 1, dict(pro=True, residual=True, stats=True)),
+    ("c3_1024_3x3_dgrad", 16, 2, 2, 1024, 1024, 3, dict(dgrad=True, bias=False)),
+    ("c3_1024_out_1x1", 16, 2, 2, 1024, 192, 1, dict(pro=True)),
+    # config 1 at its benchmarked batch: scale-1 shapes, M = 64*64*64 = 262,144
+    ("c1_full_in_3x3", 64, 64, 64, 7, 32, 3, dict(stats=True)),
+    ("c1_full_3x3_pro_stats", 64, 64, 64, 32, 32, 3, dict(pro=True, stats=True, bias=False)),
+    ("c1_full_1x1_pro", 64, 64, 64, 32, 32, 1, dict(pro=True, stats=True, bias=False)),
+    ("c1_full_1x1_res", 64, 64, 64, 32, 32, 1, dict(pro=True, residual=True, stats=True)),
+    ("c1_full_skip_acc", 64, 64, 64, 32, 32, 1, dict(acc=True, stats=True)),
+    ("c1_full_out_1x1", 64, 64, 64, 32, 6, 1, dict(pro=True)),
+    ("c1_full_3x3_dgrad", 64, 64, 64, 32, 32, 3, dict(dgrad=True, residual=True, acc=True, bias=False)),
+    ("c1_full_1x1_dgrad", 64, 64, 64, 32, 32, 1, dict(dgrad=True, bias=False)),
+    ("c1_full_in_dgrad", 64, 64, 64, 32, 7, 3, dict(bias=False)),
 ]
 
 
@@ -183,20 +195,18 @@ def test_conv_vs_float64(case, dtype):
         assert rel(sums[1], s2) < 10 * tol, rel(sums[1], s2)
 
 
-DEEP = [c for c in CASES if c[0].startswith(("s5", "s4", "s3"))]
+DEEP = [c for c in CASES if c[0].startswith(("s5", "s4", "s3", "c3_"))]
 
 
 @pytest.mark.parametrize("case", DEEP, ids=[c[0] for c in DEEP])
 def test_conv_variants_agree(case):
     """the small-pixel-count kernel families (halo tile: default; LDS-tiled
-    split-K + reduce launch; deep-K register operands) give the same fp32
-    result"""
+    split-K + reduce launch: variant 1) give the same fp32 result"""
     name, B, H, W, cin, cout, ks, fl = case
     a, ref, _, _, _ = run_case(B, H, W, cin, cout, ks, "fp32", variant=0, **fl)
-    for v in (1, 2):    # LDS-tiled split-K; deep-K register operands
-        b, _, _, _, _ = run_case(B, H, W, cin, cout, ks, "fp32", variant=v, **fl)
-        assert rel(a, b) < 2e-6, v
-        assert rel(b, ref) < 1e-5, v
+    b, _, _, _, _ = run_case(B, H, W, cin, cout, ks, "fp32", variant=1, **fl)
+    assert rel(a, b) < 2e-6
+    assert rel(b, ref) < 1e-5
 
 
 BAND = [c for c in CASES if "band" in c[0]]

@@ -135,3 +135,148 @@ def test_side_stream_overlap_matches_single_stream():
     assert d(m1, m0) < tol_m, (d(m1, m0), d(mb, m0))
     assert float((p1 - p0).abs().max()) <= 3 * 2 * lr * 1.01
     assert d(p1, p0) < max(1e-3, 4 * d(pb, p0))
+
+
+# ---------------------------------------------------------------------------
+# data parallel path (process_group) on one GPU: world-size-1 RCCL group
+@pytest.fixture(scope="module")
+def nccl_world1():
+    import os
+    import socket
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    yield dist.group.WORLD
+    dist.destroy_process_group()
+
+
+def _one_step(model, pg=None, graph=False, **kw):
+    from realnvp_hip.trainer import FlowTrainer
+    tr = FlowTrainer(model, 4, dtype="fp32", process_group=pg, **kw)
+    tr.set_pixels(pixels(4, 3, 32, seed=5).to(DEV))
+    if graph:
+        tr.capture(warmup=1)
+    p0 = tr.param.clone()
+    tr.step()
+    torch.cuda.synchronize()
+    return tr, p0
+
+
+@pytest.mark.parametrize("graph", [False, True], ids=["eager", "hipgraph"])
+@pytest.mark.parametrize("comm", ["overlap", "split"])
+def test_process_group_step_matches_single_process(nccl_world1, comm, graph):
+    """The DP step (bucketed all-reduce on the communication stream during
+    backward, or between the captured graphs) with a world-size-1 RCCL group
+    equals the single-process step: same gradients (up to the replica
+    atomics' summation order), same Adam update, same step counter."""
+    ref, p0 = _one_step(make_model(32, 8, 1))
+    ref2, _ = _one_step(make_model(32, 8, 1))
+    tr, q0 = _one_step(make_model(32, 8, 1), pg=nccl_world1, graph=graph, comm=comm, bucket_mb=1)
+    assert len(tr.buckets) > 1
+    assert torch.equal(p0, q0)
+
+    def d(a, b):
+        return float((a - b).norm() / b.norm())
+    assert d(tr.grad, ref.grad) < max(1e-4, 8 * d(ref2.grad, ref.grad))
+    assert float((tr.param - ref.param).abs().max()) <= 2 * ref.lr * 1.01
+    assert d(tr.param, ref.param) < max(1e-5, 4 * d(ref2.param, ref.param))
+    assert int(tr.step_t.item()) == 1
+    np.testing.assert_allclose(tr.mean_logll(1), ref.mean_logll(1), rtol=1e-6)
+
+
+def test_process_group_bf16_reduction(nccl_world1):
+    ref, _ = _one_step(make_model(32, 8, 1))
+    tr, _ = _one_step(make_model(32, 8, 1), pg=nccl_world1, comm="overlap", reduce_dtype="bf16", bucket_mb=1)
+    assert float((tr.grad - ref.grad).norm() / ref.grad.norm()) < 4e-3
+
+
+# ---------------------------------------------------------------------------
+def _batch(s, B=4, size=32):
+    import utils
+    return utils.logit_transform(pixels(B, 3, size, seed=300 + s), noise=uniform_noise(B, 3, size, seed=400 + s))
+
+
+def _torch_step(model, opt, s):
+    x, ld = _batch(s)
+    opt.zero_grad()
+    lp, ws = model(x)
+    ll = (lp + ld).mean()
+    loss = -ll + 5e-5 * ws
+    loss.backward()
+    opt.step()
+    return float(ll)
+
+
+def _trainer_step(tr, s):
+    x, ld = _batch(s)
+    tr.set_input(x, ld)
+    tr.reset_metrics()
+    tr.step()
+    return tr.mean_logll(1)
+
+
+def test_optimizer_checkpoint_roundtrip_with_torch_adam():
+    """train.py:139-154, 249-250: the fused trainer's Adam state saved in
+    torch.optim.Adam format continues the same trajectory inside the
+    reference loop (torch Adam around the drop-in), and a torch Adam
+    checkpoint continues inside the fused trainer."""
+    from realnvp_hip.trainer import FlowTrainer
+    ma = make_model(32, 8, 1)
+    tr = FlowTrainer(ma, 4, dtype="fp32")
+    for s in range(2):
+        _trainer_step(tr, s)
+    sd = tr.state_dict()
+    st = sd["optimizer"]["state"]
+    assert len(st) == sum(1 for p in ma.parameters() if p.requires_grad)
+    assert all(float(v["step"]) == 2.0 for v in st.values())
+    # -> torch Adam around a fresh drop-in model
+    mb = make_model(32, 8, 1).train()
+    mb.load_state_dict(sd["model"])
+    opt = torch.optim.Adam(mb.parameters(), lr=5e-4, weight_decay=5e-5)
+    opt.load_state_dict(sd["optimizer"])
+    ll_t = _torch_step(mb, opt, 2)
+    ll_f = _trainer_step(tr, 2)
+    np.testing.assert_allclose(ll_f, ll_t, rtol=1e-5)
+    pa = torch.cat([p.detach().reshape(-1) for p in ma.parameters()])
+    pb = torch.cat([p.detach().reshape(-1) for p in mb.parameters()])
+    assert float((pa - pb).abs().max()) <= 2 * 5e-4 * 1.01
+    assert float((pa - pb).norm() / pb.norm()) < 1e-3
+    # <- torch Adam state into a fresh fused trainer, one more step each
+    _torch_step(mb, opt, 3)
+    mc = make_model(32, 8, 1)
+    tc = FlowTrainer(mc, 4, dtype="fp32")
+    tc.load_state_dict({"model": mb.state_dict(), "optimizer": opt.state_dict()})
+    assert int(tc.step_t.item()) == 4
+    ll_t = _torch_step(mb, opt, 4)
+    ll_f = _trainer_step(tc, 4)
+    np.testing.assert_allclose(ll_f, ll_t, rtol=1e-5)
+    pc = torch.cat([p.detach().reshape(-1) for p in mc.parameters()])
+    pb = torch.cat([p.detach().reshape(-1) for p in mb.parameters()])
+    assert float((pc - pb).abs().max()) <= 2 * 5e-4 * 1.01
+    assert float((pc - pb).norm() / pb.norm()) < 1e-3
+
+
+def test_capture_restores_state_and_fixes_input_mode():
+    """capture() leaves parameters, moments, step counter and BN buffers as
+    they were (ADVICE: warm-up steps used to train silently), and a graph
+    captured for set_pixels() refuses set_input() batches."""
+    from realnvp_hip.trainer import FlowTrainer
+    model = make_model(32, 8, 1)
+    tr = FlowTrainer(model, 4, dtype="fp32")
+    tr.set_pixels(pixels(4, 3, 32, seed=1).to(DEV))
+    p0, rv0 = tr.param.clone(), {n: b.clone() for n, b in model.named_buffers()}
+    assert tr.capture(warmup=2) == 2
+    assert torch.equal(tr.param, p0) and int(tr.step_t.item()) == 0
+    assert all(torch.equal(b, rv0[n]) for n, b in model.named_buffers())
+    x, ld = _batch(0)
+    with pytest.raises(RuntimeError):
+        tr.set_input(x, ld)
+    tr.drop_graph()
+    tr.set_input(x, ld)
+    tr.step()
+    assert int(tr.step_t.item()) == 1

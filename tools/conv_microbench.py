@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.join(ROOT, "dl-normalizing-flows_amd"))
 import torch  # noqa: E402
 
 from realnvp_hip import _lib  # noqa: E402
-from realnvp_hip._lib import BNSrc, ConvArgs, WgradArgs  # noqa: E402
+from realnvp_hip._lib import BNSrc, ConvArgs, WgradGroup  # noqa: E402
 from realnvp_hip.engine import splitk_workspace, stat_shards  # noqa: E402
 from realnvp_hip.net import chan_stride, round_up  # noqa: E402
 
@@ -49,7 +49,7 @@ def bench(fn, iters=20, reps=5):
 
 
 def conv_case(B, H, W, cin, cout, ks, pro=False, stats=False, residual=False, acc=False, dgrad_epi=False,
-              dtype="bf16", wgrad=False):
+              dtype="bf16", wgrad=False, variant=0):
     dev = "cuda"
     tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
     esz = 2 if dtype == "bf16" else 4
@@ -70,17 +70,20 @@ def conv_case(B, H, W, cin, cout, ks, pro=False, stats=False, residual=False, ac
     L = _lib.lib()
     s = torch.cuda.current_stream().cuda_stream
     if wgrad:
-        dw = torch.zeros(cout, kp, device=dev)
-        a = WgradArgs()
+        nz = int(L.wgrad_slabs(M))
+        nrep = int(L.wgrad_replicas(nz))
+        dw = torch.zeros(nrep, cout, kp, device=dev)
+        a = WgradGroup()
         a.dtype = 1 if dtype == "bf16" else 0
-        a.B, a.H, a.W, a.ks = B, H, W, ks
-        a.x, a.cs_in, a.cin = x.data_ptr(), csi, cin
+        a.B, a.H, a.W, a.n_conv = B, H, W, 1
+        c = a.conv[0]
+        c.x, c.cs_in, c.cin, c.ks = x.data_ptr(), csi, cin, ks
         if pro:
-            a.pro_bn_relu = 1
-            a.pro = BNSrc(sums_in.data_ptr(), float(M), None, None, gam.data_ptr(), bet.data_ptr(), 1e-5, sh)
-        a.dy, a.cs_dy, a.n = y.data_ptr(), cso, cout
-        a.dw, a.kp = dw.data_ptr(), kp
-        fn = lambda: L.conv2d_wgrad(C.byref(a), torch.cuda.current_stream().cuda_stream)  # noqa: E731
+            c.pro_bn_relu = 1
+            c.pro = BNSrc(sums_in.data_ptr(), float(M), None, None, gam.data_ptr(), bet.data_ptr(), 1e-5, sh)
+        c.dy, c.cs_dy, c.n = y.data_ptr(), cso, cout
+        c.ws, c.kp, c.nz, c.nrep = dw.data_ptr(), kp, nz, nrep
+        fn = lambda: L.conv2d_wgrad_grouped(C.byref(a), torch.cuda.current_stream().cuda_stream)  # noqa: E731
         nbytes = esz * M * (csi + cso) + 4 * cout * ks * ks * cin
     else:
         a = ConvArgs()
@@ -102,6 +105,7 @@ def conv_case(B, H, W, cin, cout, ks, pro=False, stats=False, residual=False, ac
             a.epi = BNSrc(sums_in.data_ptr(), float(M), None, None, gam.data_ptr(), bet.data_ptr(), 1e-5, sh)
             a.epi_sums = sums_out.data_ptr()
         a.ws, a.ws_elems = ws.data_ptr(), ws.numel()
+        a.variant = variant
         if dgrad_epi:
             sums_out.zero_()
         fn = lambda: L.conv2d(C.byref(a), torch.cuda.current_stream().cuda_stream)  # noqa: E731
@@ -147,53 +151,18 @@ CASES = [
 
 def main():
     torch.manual_seed(0)
-    variants = [0, 1, 2] if "--both" in sys.argv else ([0, 1] if "--v01" in sys.argv else [0])
-    vs = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--variants=")]
-    if vs:
-        variants = [int(v) for v in vs[0].split(",")]
+    variants = [0, 1] if "--v01" in sys.argv else [0]
     only = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--case=")]
     print("%-32s %3s %9s %9s %9s" % ("case", "var", "us", "GB/s", "TFLOP/s"))
     for name, B, H, W, ci, co, ks, fl in CASES:
         if only and not any(o in name for o in only):
             continue
         for v in variants:
-            _lib.lib().conv_set_variant(v)
-            us, gbs, tfs = conv_case(B, H, W, ci, co, ks, **fl)
+            if fl.get("wgrad") and v:
+                continue
+            us, gbs, tfs = conv_case(B, H, W, ci, co, ks, variant=v, **fl)
             print("%-32s %3d %9.1f %9.1f %9.1f" % (name, v, us, gbs, tfs), flush=True)
-    _lib.lib().conv_set_variant(0)
-
-
-
-
-
-def stamps(case_filter):
-    """Phase breakdown of the halo-tile conv (rnvp_conv_debug_stamps)."""
-    import numpy as np
-    L = _lib.lib()
-    buf = torch.zeros(8 * 65536, dtype=torch.int64, device="cuda")
-    for name, B, H, W, ci, co, ks, fl in CASES:
-        if case_filter not in name:
-            continue
-        L.conv_debug_stamps(buf.data_ptr())
-        buf.zero_()
-        conv_case(B, H, W, ci, co, ks, **fl)
-        torch.cuda.synchronize()
-        L.conv_debug_stamps(None)
-        st = buf.view(-1, 8).cpu().numpy().astype(np.float64)
-        st = st[st[:, 0] > 0]
-        t0 = st[:, 0].min()
-        ph = np.diff(st[:, :6], axis=1) * 10.0 / 1000.0   # us
-        clk = np.median((st[:, 7] - st[:, 6]) / np.maximum(st[:, 5] - st[:, 0], 1)) * 100.0   # MHz
-        print("%-30s wgs %d  start spread %.2f us  end %.2f us | tables %.2f staging %.2f loop %.2f red %.2f epi %.2f"
-              " | shader clock %.0f MHz"
-              % (name, len(st), (st[:, 0].max() - t0) / 100.0, (st[:, 5].max() - t0) / 100.0,
-                 *[float(np.median(ph[:, k])) for k in range(5)], clk))
 
 
 if __name__ == "__main__":
-    st = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--stamps=")]
-    if st:
-        for f in st:
-            stamps(f)
-    else:
-        main()
+    main()

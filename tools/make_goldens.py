@@ -121,14 +121,28 @@ COUPLING_CASES = [
 ]
 
 
+# deep nets (BASELINE config 3 / the reference CLI default R8 D64,
+# main.py:231-240): an R=8 coupling crosses the 24-conv grouped-wgrad chunk
+# (4R+3 = 35 convs); the mid-1024 channelwise coupling is c3's scale-4 shape
+# (C = 96 at 2x2), ~100 M parameters, so only per-tensor gradient norms and the
+# small tensors' full gradients are stored (weights come from formula_init).
+BIG_COUPLING_CASES = [
+    # name, kind, in_out, mid, size, cfg, hps kwargs, B, full gradients
+    ("ckbd_c3_m64_s32_r8_cfg1", "ckbd", 3, 64, 32, 1.0, dict(base_dim=64, res_blocks=8), 4, True),
+    ("chan_c96_m1024_s2_r8_cfg0", "chan", 96, 1024, 2, 0.0, dict(base_dim=64, res_blocks=8), 4, False),
+]
+
+
 def make_coupling(kind, cio, mid, size, cfg, hp):
     if kind == "ckbd":
         return modules_realnvp.CheckerboardAffineCoupling(cio, mid, size, cfg, hp)
     return modules_realnvp.ChannelwiseAffineCoupling(cio, mid, cfg, hp)
 
 
-def coupling_goldens():
-    for name, kind, cio, mid, size, cfg, hk, B in COUPLING_CASES:
+def coupling_goldens(cases=None):
+    cases = cases if cases is not None else [c + (True,) for c in COUPLING_CASES]
+    for name, kind, cio, mid, size, cfg, hk, B, full in cases:
+        t0 = time.time()
         hp = hps(**hk)
         mod = make_coupling(kind, cio, mid, size, cfg, hp)
         mod.load_state_dict(formula_state(mod))
@@ -142,9 +156,15 @@ def coupling_goldens():
         y, ldj = mod(xr)
         (y * gy + ldj * gl).sum().backward()
         d.update(train_y=f32(y), train_ldj=f32(ldj), grad_x=f32(xr.grad))
+        names, norms = [], []
         for n, p in mod.named_parameters():
             if p.grad is not None:
-                d["grad." + n] = f32(p.grad)
+                names.append(n)
+                norms.append(float(p.grad.double().norm()))
+                if full or p.numel() <= 4096:
+                    d["grad." + n] = f32(p.grad)
+        d["grad_names"] = np.array(names)
+        d["grad_norms"] = np.array(norms, dtype=np.float64)
         for k, v in mod.state_dict().items():
             if "running" in k or "num_batches" in k:
                 d["after_train." + k] = v.clone().numpy()
@@ -161,6 +181,7 @@ def coupling_goldens():
             xe, _ = mod(ye.clone(), reverse=True)
         d.update(eval_y=f32(ye), eval_ldj=f32(le), eval_rec=f32(xe))
         save("coupling_%s.npz" % name, d)
+        print(name, "took %.1fs" % (time.time() - t0))
 
 
 # ---------------------------------------------------------------------------
@@ -170,6 +191,65 @@ MODEL_CASES = [
     ("m32_d32_r2", 32, 32, 2, 4, 3),
     ("m64_d32_r4", 64, 32, 4, 2, 3),
 ]
+# BASELINE config 3 (32x32x3, R8, D64: 923.6 M parameters) at B=2, and config 1
+# at its full benchmarked batch B=64.  "lite" goldens keep the per-sample and
+# per-tensor outputs only (inputs are regenerated from the pixel / noise seeds).
+BIG_MODEL_CASES = [
+    ("m32_d64_r8", 32, 64, 8, 2, 0),
+    ("m64_d32_r4_b64", 64, 32, 4, 64, 0),
+]
+
+
+def model_inputs(B, size):
+    """the logit-transformed synthetic batch every model golden uses
+    (utils.py:44-72 with explicit noise)."""
+    pix = pixels(B, 3, size, seed=10)
+    noise = uniform_noise(B, 3, size, seed=11)
+    x = (pix * 255.0 + noise) / 256.0
+    x = ((x * 2.0 - 1.0) * 0.9 + 1.0) / 2.0
+    x_in = torch.log(x) - torch.log(1.0 - x)
+    pre = torch.tensor(np.log(0.9) - np.log(0.1))
+    logdet = (torch.nn.functional.softplus(x_in) + torch.nn.functional.softplus(-x_in)
+              - torch.nn.functional.softplus(-pre)).sum(dim=(1, 2, 3))
+    return pix, noise, x_in, logdet
+
+
+def lite_model_golden(name, size, bd, rb, B):
+    t0 = time.time()
+    prior = D.Normal(torch.tensor(0.0), torch.tensor(1.0), validate_args=False)
+    model = flow_realnvp.RealNVP(3, size, prior, hps(bd, rb))
+    model.load_state_dict(formula_state(model))
+    print(name, "built in %.1fs" % (time.time() - t0))
+    _, _, x_in, logdet = model_inputs(B, size)
+    d = dict(batch=np.array(B), logdet=f32(logdet))
+    model.train()
+    xr = x_in.clone().requires_grad_(True)
+    lp, ws = model(xr)
+    loss = -(lp + logdet).mean() + 5e-5 * ws
+    loss.backward()
+    d.update(train_logprob=f32(lp), weight_scale=f32(ws), loss=f32(loss),
+             grad_x_norm=np.array(float(xr.grad.double().norm())), grad_x_sum=np.array(float(xr.grad.double().sum())))
+    names, norms = [], []
+    for n, p in model.named_parameters():
+        if p.grad is not None:
+            names.append(n)
+            norms.append(float(p.grad.double().norm()))
+            if n.endswith("scale") or n.endswith("scale_shift"):
+                d["grad." + n] = f32(p.grad)
+    d["grad_names"] = np.array(names)
+    d["grad_norms"] = np.array(norms, dtype=np.float64)
+    for k, v in model.state_dict().items():
+        if "running" in k:
+            d["after_train." + k] = v.clone().numpy()
+    model.eval()
+    with torch.no_grad():
+        lpe, _ = model(x_in.clone())
+        ze, _ = model.f(x_in.clone())
+        xrec = model.g(ze.clone())
+    d.update(eval_logprob=f32(lpe),
+             eval_rec_err=np.array(float((xrec - x_in).abs().max() / x_in.abs().max())))
+    save("model_%s.npz" % name, d)
+    print(name, "took %.1fs" % (time.time() - t0))
 
 
 def model_goldens():
@@ -254,7 +334,7 @@ def model_goldens():
 
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
-    which = sys.argv[1:] or ["index", "logit", "coupling", "model"]
+    which = sys.argv[1:2] or ["index", "logit", "coupling", "model"]
     if "index" in which:
         index_maps()
     if "logit" in which:
@@ -263,6 +343,12 @@ if __name__ == "__main__":
         coupling_goldens()
     if "model" in which:
         model_goldens()
+    if "big_coupling" in which:
+        coupling_goldens(BIG_COUPLING_CASES)
+    if "big_model" in which:
+        for c in BIG_MODEL_CASES:
+            if not sys.argv[2:] or c[0] in sys.argv[2:]:
+                lite_model_golden(*c[:5])
 
 
 def init_golden():
