@@ -31,8 +31,16 @@ import torch  # noqa: E402
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA
 F32_PEAK_TFLOPS = 157.3        # f32 MFMA
-# algorithmic bytes / image / training step at config 1
-ALG_BYTES_PER_IMG = 292.33e6
+# BASELINE.json configs: shape, per-GPU batch, algorithmic
+# bytes / image / training step (10*A + 72*X + 40*P/B)
+CONFIGS = {
+    "c1": dict(size=64, res_blocks=4, base_dim=32, batch=64, n_scales=5, alg_bytes=292.33e6,
+               label="config 1: RealNVP 64x64x3, res-blocks 4, base-dim 32"),
+    "c3": dict(size=32, res_blocks=8, base_dim=64, batch=64, n_scales=5, alg_bytes=773.78e6,
+               label="config 3: RealNVP 32x32x3, res-blocks 8, base-dim 64 (923.6 M parameters)"),
+    "c4": dict(size=128, res_blocks=4, base_dim=64, batch=256, n_scales=6, alg_bytes=2014.07e6,
+               label="config 4: RealNVP 128x128x3, 6 scales, res-blocks 4, base-dim 64"),
+}
 
 
 def parse():
@@ -40,23 +48,35 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--batch", type=int, default=64, help="images per GPU")
-    p.add_argument("--size", type=int, default=64)
-    p.add_argument("--res-blocks", type=int, default=4)
-    p.add_argument("--base-dim", type=int, default=32)
+    p.add_argument("--config", default="c1", choices=sorted(CONFIGS), help="BASELINE.json config preset")
+    p.add_argument("--batch", type=int, default=None, help="images per GPU (default: the config's)")
+    p.add_argument("--size", type=int, default=None)
+    p.add_argument("--res-blocks", type=int, default=None)
+    p.add_argument("--base-dim", type=int, default=None)
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--overlap", action="store_true", help="side stream for weight gradients (HIP graphs serialise it today)")
+    p.add_argument("--comm", default="overlap", choices=["overlap", "split"], help="DP all-reduce schedule")
+    p.add_argument("--reduce-dtype", default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-batch", type=int, default=16)
-    p.add_argument("--cpu-steps", type=int, default=2)
+    p.add_argument("--no-secondary", action="store_true",
+                   help="skip the secondary measurements (fp32 parity mode, drop-in loop, sampling, config 3)")
+    p.add_argument("--cpu-batch", type=int, default=64)
+    p.add_argument("--cpu-steps", type=int, default=3)
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--pmc-markers", default=None,
                    help="write the instrumented step's launch families here and dispatch a marker before each "
                         "launch (for rocprofv3 --pmc passes, tools/pmc_traffic.py)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="per-family PMC HBM bytes per launch (tools/pmc_traffic.py output) for roofline.traffic")
-    return p.parse_args()
+    a = p.parse_args()
+    cfg = CONFIGS[a.config]
+    for k in ("batch", "size", "res_blocks", "base_dim"):
+        if getattr(a, k) is None:
+            setattr(a, k, cfg[k])
+    a.n_scales = cfg["n_scales"]
+    a.custom = any(a.__dict__[k] != cfg[k] for k in ("batch", "size", "res_blocks", "base_dim"))
+    return a
 
 
 def synthetic_pixels(B, C, S, seed):
@@ -134,7 +154,7 @@ def cpu_baseline(args):
     threads = len(os.sched_getaffinity(0))
     threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
     torch.set_num_threads(threads)
-    spec = O.FlowSpec(3, args.size, O.HP(args.base_dim, args.res_blocks))
+    spec = O.FlowSpec(3, args.size, O.HP(args.base_dim, args.res_blocks), n_scales=args.n_scales)
     e = O.flow_spec_entries(spec)
     S = O.build_state(e, formula_value)
     tr = O.OracleTrainer(S, spec, O.param_names(e), O.trainable_names(e))
@@ -161,6 +181,99 @@ def cpu_baseline(args):
                                                args.cpu_steps, dt, cpu_model))
 
 
+def build_model(size, res_blocks, base_dim, n_scales, dev, seed):
+    """random-init drop-in RealNVP, constructed on the device (no host copy of
+    the parameters)"""
+    import flow_realnvp
+    import utils
+    torch.manual_seed(seed)     # same initial weights on every rank
+    prior = torch.distributions.Normal(torch.tensor(0.0, device=dev), torch.tensor(1.0, device=dev),
+                                       validate_args=False)
+    hp = utils.Hyperparameters(base_dim, res_blocks, True, True, True, True)
+    with torch.device(dev):
+        return flow_realnvp.RealNVP(3, size, prior, hp, n_scales=n_scales)
+
+
+def timed(fn, steps, warmup, barrier=lambda: None):
+    for _ in range(warmup):
+        fn()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    barrier()
+    return time.perf_counter() - t0
+
+
+def secondary(args, dev):
+    """Single-GPU context numbers next to the headline line: the fp32 parity
+    mode of the same config, the drop-in loop train.py runs (model(x),
+    loss.backward(), torch.optim.Adam), graph-replayed generation, and
+    BASELINE config 3."""
+    import utils
+    from realnvp_hip.sampler import FlowSampler
+    from realnvp_hip.trainer import FlowTrainer
+    out = {}
+    B = args.batch
+    pix = synthetic_pixels(B, 3, args.size, seed=0).to(dev)
+
+    # fp32 parity mode (the north star's 1e-5 log-prob mode) of the same step
+    model = build_model(args.size, args.res_blocks, args.base_dim, args.n_scales, dev, args.seed)
+    tr = FlowTrainer(model, B, dtype="fp32", seed=1000)
+    tr.set_pixels(pix)
+    tr.capture(warmup=1)
+    dt = timed(tr.step, 5, 2)
+    out["fp32_parity_mode"] = dict(value=round(5 * B / dt, 2), unit="images/sec", ms_per_step=round(dt / 5 * 1e3, 3),
+                                   dtype="fp32", steps=5)
+    del tr
+
+    # the drop-in as train.py:176-200 drives it (eager autograd, torch Adam), fp32
+    model.train()
+    opt = torch.optim.Adam(model.parameters(), lr=5e-4, weight_decay=5e-5)
+    def loop_step():
+        x, ld = utils.logit_transform(pix)      # device noise, seed from torch's CPU generator
+        opt.zero_grad()
+        lp, ws = model(x)
+        loss = -(lp + ld).mean() + 5e-5 * ws
+        loss.backward()
+        opt.step()
+    dt = timed(loop_step, 3, 1)
+    out["drop_in_loop"] = dict(value=round(3 * B / dt, 2), unit="images/sec", ms_per_step=round(dt / 3 * 1e3, 3),
+                               dtype="fp32", steps=3,
+                               note="model(x) + loss.backward() + torch.optim.Adam, eager (train.py:176-200)")
+    del opt
+
+    # generation: RealNVP.sample(n) + logit_transform(reverse=True), eval mode (train.py:253-259)
+    model.eval()
+    for dtype in ("fp32", "bf16"):
+        with torch.no_grad():
+            smp = FlowSampler(model, B, dtype=dtype)
+            dt = timed(smp.sample, 10, 2)
+        out["sampling_" + dtype] = dict(value=round(10 * B / dt, 2), unit="images/sec",
+                                        ms_per_call=round(dt / 10 * 1e3, 3), n=B)
+        del smp
+    del model
+    torch.cuda.empty_cache()
+
+    # BASELINE config 3 (R8, D64, 923.6 M parameters), bf16, batch 64
+    c = CONFIGS["c3"]
+    model = build_model(c["size"], c["res_blocks"], c["base_dim"], c["n_scales"], dev, args.seed)
+    tr = FlowTrainer(model, c["batch"], dtype="bf16", seed=1000)
+    tr.set_pixels(synthetic_pixels(c["batch"], 3, c["size"], seed=0).to(dev))
+    tr.capture(warmup=1)
+    tr.reset_metrics()
+    dt = timed(tr.step, 5, 1)
+    v = 5 * c["batch"] / dt
+    out["config3"] = dict(workload=c["label"] + ", per-GPU batch %d, train step fwd+bwd+Adam" % c["batch"],
+                          value=round(v, 2), unit="images/sec", ms_per_step=round(dt / 5 * 1e3, 3), dtype="bf16",
+                          steps=5, step_roofline_frac=round(v * c["alg_bytes"] / (HBM_PEAK_GBS * 1e9), 5))
+    del tr, model
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -176,40 +289,27 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         pg = dist.group.WORLD
 
-    import flow_realnvp
-    import utils
+    from realnvp_hip.dist import max_over_ranks, mean_over_ranks, rank_seed
     from realnvp_hip.trainer import FlowTrainer
 
-    torch.manual_seed(args.seed)     # same initial weights on every rank
     dev = torch.device("cuda", local)
-    prior = torch.distributions.Normal(torch.tensor(0.0, device=dev), torch.tensor(1.0, device=dev),
-                                       validate_args=False)
-    hp = utils.Hyperparameters(args.base_dim, args.res_blocks, True, True, True, True)
-    model = flow_realnvp.RealNVP(3, args.size, prior, hp).to(dev)
-    from realnvp_hip.dist import max_over_ranks, mean_over_ranks, rank_seed
+    model = build_model(args.size, args.res_blocks, args.base_dim, args.n_scales, dev, args.seed)
     tr = FlowTrainer(model, args.batch, dtype=args.dtype, seed=rank_seed(1000, rank), process_group=pg,
-                     overlap=args.overlap)
+                     overlap=args.overlap, comm=args.comm, reduce_dtype=args.reduce_dtype)
     tr.set_pixels(synthetic_pixels(args.batch, 3, args.size, seed=rank_seed(0, rank)).to(dev))
 
     if not args.no_graph:
         tr.capture(warmup=2)
-    for _ in range(args.warmup):
-        tr.step()
-    tr.reset_metrics()
 
     def barrier():
         if pg is not None:
             import torch.distributed as dist
             dist.barrier()
 
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(args.warmup):
         tr.step()
-    torch.cuda.synchronize()
-    barrier()
-    dt = time.perf_counter() - t0
+    tr.reset_metrics()
+    dt = timed(tr.step, args.steps, 0, barrier)
     mean_ll = tr.mean_logll(args.steps)
     if pg is not None:
         dt = max_over_ranks(dt, dev, pg)
@@ -220,6 +320,11 @@ def main():
     cfg_key = dict(size=args.size, res_blocks=args.res_blocks, base_dim=args.base_dim, batch=args.batch,
                    dtype=args.dtype)
     roof, fams = kernel_roofline(tr, args.pmc_markers if rank == 0 else None, args.traffic, cfg_key)
+    alg_bytes = CONFIGS[args.config]["alg_bytes"]
+    label = CONFIGS[args.config]["label"]
+    if args.custom:
+        label = "custom: RealNVP %dx%dx3, res-blocks %d, base-dim %d" % (args.size, args.size, args.res_blocks,
+                                                                       args.base_dim)
     out = None
     if rank == 0:
         out = {
@@ -235,20 +340,26 @@ def main():
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic (uniform 8-bit pixels, device Philox dequantisation noise); random init",
-            "config": {"workload": "config 1: RealNVP %dx%dx3, res-blocks %d, base-dim %d, per-GPU batch %d, "
-                                   "train step fwd+bwd+Adam" % (args.size, args.size, args.res_blocks, args.base_dim,
-                                                                args.batch),
+            "config": {"workload": "%s, per-GPU batch %d, train step fwd+bwd+Adam" % (label, args.batch),
                        "global_batch": world * args.batch, "image_size": args.size, "res_blocks": args.res_blocks,
-                       "base_dim": args.base_dim, "parallelism": "dp%d" % world,
-                       "graph": not args.no_graph, "side_stream": args.overlap},
+                       "base_dim": args.base_dim, "n_scales": args.n_scales, "parallelism": "dp%d" % world,
+                       "graph": not args.no_graph, "side_stream": args.overlap,
+                       "allreduce": None if world == 1 else "%s, %s buckets of %d MB" % (
+                           args.comm, args.reduce_dtype, 25)},
             "bits_per_dim": round(bpd, 4),
-            "step_roofline_frac": round(value / world * ALG_BYTES_PER_IMG / (HBM_PEAK_GBS * 1e9), 5),
+            "step_roofline_frac": None if args.custom else round(value / world * alg_bytes / (HBM_PEAK_GBS * 1e9), 5),
             "roofline": roof,
             "kernel_families": fams,
             "cpu_baseline": None,
         }
-        if world == 1 and not args.no_cpu_baseline:
+    del tr, model
+    torch.cuda.empty_cache()
+    if rank == 0 and world == 1:
+        if not args.no_secondary:
+            out["secondary"] = secondary(args, dev)
+        if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0:
         print(json.dumps(out), flush=True)
     if pg is not None:
         import torch.distributed as dist

@@ -13,6 +13,7 @@ Parameter gradients go to a flat fp32 "grad block" laid out like the
 coupling's named_parameters() (frozen weight_g included, never written).
 """
 import ctypes as C
+import os
 from collections import OrderedDict
 
 import torch
@@ -27,6 +28,9 @@ COUPLING_SHARDS = 32      # RNVP_COUPLING_SHARDS (include/realnvp_hip.h)
 BN_MOMENTUM = 0.1
 
 DTYPES = {"fp32": (RNVP_F32, 4, torch.float32), "bf16": (RNVP_BF16, 2, torch.bfloat16)}
+# conv kernel family override for A/B diagnostics (rnvp_conv_args.variant):
+# 0 = per-shape tuned dispatch, 1 = generic LDS-tiled kernels only
+CONV_VARIANT = int(os.environ.get("RNVP_CONV_VARIANT", "0"))
 
 
 def stream_ptr():
@@ -358,6 +362,7 @@ class CouplingEngine:
             a.out_sums = ar.ptr("s:" + op.stats_bn) if (op.stats_bn and training) else None
             if sc["ws"] is not None:
                 a.ws, a.ws_elems = sc["ws"].data_ptr(), sc["ws_elems"]
+            a.variant = CONV_VARIANT
             esz = DTYPES[sv["dtype"]][1]
             nb = esz * (M * cs_in + spec.cout * kp_f + M * cs_out * (1 + int(bool(op.residual)) + int(op.accumulate)))
             _launch("conv_fwd", nb, 2.0 * M * spec.cout * spec.ks * spec.ks * spec.cin, L.conv2d, C.byref(a), s)
@@ -400,12 +405,15 @@ class CouplingEngine:
         return z, (ldj_full if full_ldj else ldj_sample), sv
 
     # ---------------------------------------------------------------- inverse
-    def reverse(self, x, training, dtype):
+    def reverse(self, x, training, dtype, saved=None, out=None, want_ldj=True, prepare=True):
+        """Inverse pass (modules_realnvp.py:284-291, 345-351).  saved / out:
+        persistent buffers (graph-captured sampling); prepare=False when the
+        packed weights are already current."""
         L = _lib.lib()
         B, Cc, H, W = x.shape
         s = stream_ptr()
-        ws = self.prepare_weights(dtype)
-        sv = self.alloc_saved(B, H, W, dtype, x.device, training)
+        ws = self.prepare_weights(dtype) if prepare else self.weights(dtype)
+        sv = saved if saved is not None else self.alloc_saved(B, H, W, dtype, x.device, training)
         ar = sv["arena"]
         T = self._tensors()
         if training:
@@ -418,11 +426,12 @@ class CouplingEngine:
         self._net_forward(T, sv, ws, training, s)
         if training and "bn_table" in sv:
             L.bn_running_update(sv["bn_table"].data_ptr(), sv["bn_n"], sv["bn_cmax"], BN_MOMENTUM, s)
-        out = torch.empty_like(x)
-        ldj = torch.empty_like(x)
+        if out is None:
+            out = torch.empty_like(x)
+        ldj = torch.empty_like(x) if want_ldj else None
         a.st = ar.ptr("st")
         a.z = out.data_ptr()
-        a.ldj_full = ldj.data_ptr()
+        a.ldj_full = ldj.data_ptr() if want_ldj else None
         L.coupling_reverse(C.byref(a), s)
         return out, ldj
 
@@ -498,6 +507,7 @@ class CouplingEngine:
                     c.epi_sums = sar.ptr("e:" + op.pro_bn)
                 if sc["ws"] is not None:
                     c.ws, c.ws_elems = sc["ws"].data_ptr(), sc["ws_elems"]
+                c.variant = CONV_VARIANT
                 esz = DTYPES[dtype][1]
                 nb = esz * (M * cs_out + spec.cin * kp_d + M * cs_in * (1 + int(bool(op.pro_bn)) + int(bool(
                     st.residual)) + int(st.accumulate)))

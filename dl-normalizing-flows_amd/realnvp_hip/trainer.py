@@ -30,6 +30,34 @@ from . import _lib
 from .engine import stream_ptr
 
 
+def wn_table(engines, dtype, dev):
+    """One weight-norm descriptor table over the convs of several couplings
+    (rnvp_weight_norm_fwd refreshes all their packed weight images in two
+    launches).  None when there are no convs."""
+    import ctypes as C
+    from ._lib import WNDesc
+    descs = []
+    row0 = col0 = 0
+    for eng in engines:
+        for d in eng.weights(dtype)["descs"]:
+            e = WNDesc()
+            C.memmove(C.addressof(e), C.addressof(d), C.sizeof(WNDesc))
+            e.row0, e.col0 = row0, col0
+            row0 += e.cout
+            col0 += e.cin
+            descs.append(e)
+    if not descs:
+        return None
+    tab = (WNDesc * len(descs))(*descs)
+    t = torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(dev)
+    return (t, len(descs), row0, col0)
+
+
+def wn_forward(table, dtype):
+    t, n, rows, cols = table
+    _lib.lib().weight_norm_fwd(t.data_ptr(), n, rows, cols, 1 if dtype == "bf16" else 0, stream_ptr())
+
+
 def arena_blocks(model):
     """(offset, numel) of each coupling's parameters in the flat arena
     (named_parameters() order), couplings in forward order."""
@@ -171,31 +199,13 @@ class FlowTrainer:
         table covers the early couplings (few parameters, needed at once), the
         second the late, deep couplings (most of the parameters), which the
         side stream prepares while the early couplings run."""
-        import ctypes as C
-        from ._lib import WNDesc
-        couplings = [st for st in self.stages if st[0] == "coupling"]
-        self.wn_split = min(len(couplings), max(1, len(couplings) * 3 // 7))
-        self.wn_tables = []
-        for part in (couplings[:self.wn_split], couplings[self.wn_split:]):
-            descs = []
-            row0 = col0 = 0
-            for st in part:
-                for d in st[2].weights(self.dtype)["descs"]:
-                    e = WNDesc()
-                    C.memmove(C.addressof(e), C.addressof(d), C.sizeof(WNDesc))
-                    e.row0, e.col0 = row0, col0
-                    row0 += e.cout
-                    col0 += e.cin
-                    descs.append(e)
-            if not descs:
-                continue
-            tab = (WNDesc * len(descs))(*descs)
-            t = torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(self.dev)
-            self.wn_tables.append((t, len(descs), row0, col0))
+        engines = [st[2] for st in self.stages if st[0] == "coupling"]
+        self.wn_split = min(len(engines), max(1, len(engines) * 3 // 7))
+        self.wn_tables = [t for t in (wn_table(engines[:self.wn_split], self.dtype, self.dev),
+                                      wn_table(engines[self.wn_split:], self.dtype, self.dev)) if t is not None]
 
     def _wn_fwd(self, table):
-        t, n, rows, cols = table
-        _lib.lib().weight_norm_fwd(t.data_ptr(), n, rows, cols, 1 if self.dtype == "bf16" else 0, stream_ptr())
+        wn_forward(table, self.dtype)
 
     def _build_adam_ranges(self):
         """Per-coupling optimizer ranges [ru4(off_i), ru4(off_next)) of the flat
