@@ -120,15 +120,11 @@ __device__ __forceinline__ F block_sum(F v, F* red /* >= 16 entries of LDS */) {
     return t;
 }
 
-// BatchNorm apply in centred form, bn(x) = (x - mean) * (gamma * rstd) + beta:
-// subtracting the mean first keeps channels whose mean is large against
-// their spread accurate (x * scale + (beta - mean * scale) cancels there).
-__device__ __forceinline__ float bn_apply(float x, float scale, float mean, float beta) {
-    return fmaf(x - mean, scale, beta);
-}
-
-// per-channel BN parameters: scale = gamma * rstd, beta (the affine bias),
-// mean (and rstd) such that bn(x) = bn_apply(x, scale, mean, beta)
+// per-channel BN affine (scale, shift) such that bn(x) = x*scale + shift:
+// the alpha/beta form ATen's batch_norm applies (the reference's own
+// arithmetic; a centred (x - mean)*scale + beta form was measured further
+// from the fp64 truth on the deep goldens, whose near-degenerate channels
+// make ReLU decisions rounding-sensitive)
 __device__ __forceinline__ void bn_affine(const rnvp_bn_src& s, int C, int c, float& scale, float& shift,
                                           float* mean_out = nullptr, float* rstd_out = nullptr) {
     double mean, var;
@@ -150,7 +146,7 @@ __device__ __forceinline__ void bn_affine(const rnvp_bn_src& s, int C, int c, fl
     float g = s.gamma ? s.gamma[c] : 1.f;
     float b = s.beta ? s.beta[c] : 0.f;
     scale = g * rstd;
-    shift = b;
+    shift = b - (float)mean * g * rstd;
     if (mean_out) *mean_out = (float)mean;
     if (rstd_out) *rstd_out = rstd;
 }
@@ -222,10 +218,9 @@ __device__ __forceinline__ void block_shard_sums(const double* sums, int C, int 
 }
 
 // BN table for channels [c0, c0+nc) from already-reduced sums tmp[0..nc) /
-// tmp[nc..2nc) (train) or the running stats (eval): scale = gamma * rstd and
-// shift = beta such that bn(x) = bn_apply(x, scale, mean, shift), plus mean /
-// rstd when requested.  Channels >= C (padding) get scale = shift = 0,
-// mean = 0, rstd = 1.
+// tmp[nc..2nc) (train) or the running stats (eval): scale/shift such that
+// bn(x) = x*scale + shift, plus mean / rstd when requested.  Channels >= C
+// (padding) get scale = shift = 0, mean = 0, rstd = 1.
 __device__ __forceinline__ void block_bn_finish(const rnvp_bn_src& s, int C, int c0, int nc, float* scale, float* shift,
                                                 float* mean_out, float* rstd_out, const double* tmp) {
     const int nv = max(0, min(nc, C - c0));
@@ -246,7 +241,7 @@ __device__ __forceinline__ void block_bn_finish(const rnvp_bn_src& s, int C, int
             const float g = s.gamma ? s.gamma[c] : 1.f;
             const float b = s.beta ? s.beta[c] : 0.f;
             sc = g * rstd;
-            sf = b;
+            sf = b - (float)mean * g * rstd;
             mo = (float)mean;
             ro = rstd;
         }

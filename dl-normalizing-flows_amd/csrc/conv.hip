@@ -61,7 +61,7 @@ __device__ __forceinline__ double* shard_ptr(double* sums, int shards, int N) {
 
 // 4-channel epilogue in the transposed layout: y = acc + bias (+ residual)
 // (+ y), or the dgrad ReLU/BN-backward form; BN statistics into s1/s2.
-// et: LDS epilogue table at channel n0 (scale | beta | mean | rstd, pitch).
+// et: LDS epilogue table at channel n0 (scale | shift | mean | rstd, pitch).
 template <typename T>
 __device__ __forceinline__ void epi4(const rnvp_conv_args& a, long long o, const floatx4& acc, const float* bias,
                                      bool epi_bn, const float* et, int pitch, double* s1, double* s2, int nvalid) {
@@ -85,7 +85,7 @@ __device__ __forceinline__ void epi4(const rnvp_conv_args& a, long long o, const
         ld4((const T*)a.epi_x + o, xv);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            if (bn_apply(xv[r], et[r], et[2 * pitch + r], et[pitch + r]) <= 0.f) v[r] = 0.f;
+            if (xv[r] * et[r] + et[pitch + r] <= 0.f) v[r] = 0.f;
             s1[r] += v[r];
             s2[r] += v[r] * (xv[r] - et[2 * pitch + r]) * et[3 * pitch + r];
         }
@@ -134,8 +134,8 @@ __global__ __launch_bounds__(256) void k_conv(rnvp_conv_args a, int kt_per_split
     const bool epi_bn = a.epi_relu_bn_bwd != 0;
 
     double* tmp = dsm;
-    float* bnp = (float*)(dsm + 2 * max(cs, BN));   // prologue scale | beta | mean [cs each]
-    float* etab = bnp + 3 * cs;                      // epilogue scale | beta | mean | rstd [BN each]
+    float* bnp = (float*)(dsm + 2 * max(cs, BN));   // prologue scale [cs] | shift [cs]
+    float* etab = bnp + 2 * cs;                      // epilogue scale | shift | mean | rstd [BN each]
     float* btab = etab + 4 * BN;                     // bias [BN]
 
     // per-thread A rows (fixed over K) and chunk column
@@ -201,8 +201,7 @@ __global__ __launch_bounds__(256) void k_conv(rnvp_conv_args a, int kt_per_split
                     float f[CH];
                     unpack(v, f, T());
 #pragma unroll
-                    for (int j = 0; j < CH; ++j)
-                        f[j] = fmaxf(bn_apply(f[j], bnp[aci + j], bnp[2 * cs + aci + j], bnp[cs + aci + j]), 0.f);
+                    for (int j = 0; j < CH; ++j) f[j] = fmaxf(f[j] * bnp[aci + j] + bnp[cs + aci + j], 0.f);
                     v = pack(f, T());
                 } else {
                     v = u32x4{0u, 0u, 0u, 0u};
@@ -219,7 +218,7 @@ __global__ __launch_bounds__(256) void k_conv(rnvp_conv_args a, int kt_per_split
 
     // the first stage's loads are in flight while the BN tables are built
     if (kt0 < kt1) gload(kt0);
-    if (pro) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + cs, bnp + 2 * cs, nullptr, tmp);
+    if (pro) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + cs, nullptr, nullptr, tmp);
     if (epi_bn && !PARTIAL)
         block_bn_table(a.epi, N, n0, BN, etab, etab + BN, etab + 2 * BN, etab + 3 * BN, tmp);
     for (int c = tid; c < BN; c += 256) btab[c] = (a.bias && n0 + c < N) ? a.bias[n0 + c] : 0.f;
@@ -397,7 +396,7 @@ __global__ __launch_bounds__(256) void k_conv_stream(rnvp_conv_args a, int shard
 
     double* tmp = dsm;
     float* bnp = (float*)(dsm + 2 * ntmp);
-    float* etab = bnp + 3 * cs;            // scale | beta | mean | rstd [NC each]
+    float* etab = bnp + 2 * cs;            // scale | shift | mean | rstd [NC each]
     float* btab = etab + 4 * NC;           // bias [NC]
     double* red = (double*)(btab + NC);    // [4 waves][NC][2]
     T* Wl = (T*)(red + 4 * NC * 2);
@@ -441,7 +440,7 @@ __global__ __launch_bounds__(256) void k_conv_stream(rnvp_conv_args a, int shard
     decode(t);
     load(0);
 
-    if (pro) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + cs, bnp + 2 * cs, nullptr, tmp);
+    if (pro) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + cs, nullptr, nullptr, tmp);
     if (epi_bn) block_bn_table(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp);
     // weights -> LDS (rows >= N and k >= K zero), bias -> LDS
     {
@@ -485,8 +484,7 @@ __global__ __launch_bounds__(256) void k_conv_stream(rnvp_conv_args a, int shard
                         float f[CH];
                         unpack(av[i], f, T());
 #pragma unroll
-                        for (int j = 0; j < CH; ++j)
-                            f[j] = fmaxf(bn_apply(f[j], bnp[ci + j], bnp[2 * cs + ci + j], bnp[cs + ci + j]), 0.f);
+                        for (int j = 0; j < CH; ++j) f[j] = fmaxf(f[j] * bnp[ci + j] + bnp[cs + ci + j], 0.f);
                         av[i] = pack(f, T());
                     }
                 }
@@ -549,7 +547,7 @@ size_t stream_lds_bytes(const rnvp_conv_args* a, int nt) {
     const int K = a->ks * a->ks * a->cs_in;
     const int kpl = ((K + KS - 1) / KS) * KS + CH;
     const int nc = 16 * nt, ntmp = a->cs_in > nc ? a->cs_in : nc;
-    return 16 * (size_t)ntmp + 12 * (size_t)a->cs_in + 16 * (size_t)nc + 4 * (size_t)nc + 64 * (size_t)nc +
+    return 16 * (size_t)ntmp + 8 * (size_t)a->cs_in + 16 * (size_t)nc + 4 * (size_t)nc + 64 * (size_t)nc +
            (size_t)nc * kpl * sizeof(T);
 }
 
@@ -599,7 +597,7 @@ int launch_conv(const rnvp_conv_args* a, hipStream_t s) {
     const long long grid = gm * gn;
     const int shards = rnvp_stat_shards(M);
     const int cs = a->cs_in;
-    const size_t shm = 16 * (size_t)(cs > BN ? cs : BN) + 12 * (size_t)cs + 20 * (size_t)BN;
+    const size_t shm = 16 * (size_t)(cs > BN ? cs : BN) + 8 * (size_t)cs + 20 * (size_t)BN;
     int splits = 1;
     if (a->ws && grid < 384 && nk >= 8) {
         splits = (int)((512 + grid - 1) / grid);
@@ -648,7 +646,7 @@ __host__ __device__ constexpr int halo_pitch(int cs) { return cs + Mf<T>::CH; }
 // BN table for channels [c0, c0+nc) of a source with <= 2 stat shards, in
 // registers (CPT channels per thread, no LDS atomics): tab_issue loads
 // (unconditional, clamped addresses, so the loads can stay in flight behind
-// later ones), tab_finish forms scale/beta (+ mean, rstd) into LDS.
+// later ones), tab_finish forms scale/shift (+ mean, rstd) into LDS.
 template <int CPT>
 struct BnTab {
     double a1[CPT], a2[CPT], b1[CPT], b2[CPT];
@@ -700,7 +698,7 @@ __device__ __forceinline__ void tab_finish(const rnvp_bn_src& s, int C, int c0, 
             }
             const float rstd = (float)(1.0 / sqrt(var + (double)s.eps));
             sc = t.gam[j] * rstd;
-            sf = t.bet[j];
+            sf = t.bet[j] - (float)mean * t.gam[j] * rstd;
             mo = (float)mean;
             ro = rstd;
         }
@@ -733,7 +731,7 @@ size_t halo_lds_bytes(int cs, int W, int ks) {
     size_t act = (size_t)R * halo_pitch<T>(cs) * sizeof(T);
     const size_t red = 4 * (size_t)BM * (BN + 4) * 4;
     if (red > act) act = red;
-    const size_t tail = 8 * 2 * (size_t)(cs > BN ? cs : BN) + 4 * 3 * (size_t)cs;
+    const size_t tail = 8 * 2 * (size_t)(cs > BN ? cs : BN) + 4 * 2 * (size_t)cs;
     return head + zrow + act + tail;
 }
 
@@ -765,7 +763,7 @@ __global__ __launch_bounds__(256) void k_conv_halo(rnvp_conv_args a, int shards)
     const int hal = PAD * (W + 1);
     const int R = BM + 2 * hal;
     const int pitch = halo_pitch<T>(cs);
-    float* etab = (float*)lds;                 // scale | beta | mean | rstd [BN each]
+    float* etab = (float*)lds;                 // scale | shift | mean | rstd [BN each]
     float* btab = etab + 4 * BN;
     double* sred = (double*)(btab + BN);       // [TM][BN][2]
     T* zrow = (T*)(sred + TM * BN * 2);
@@ -810,11 +808,10 @@ __global__ __launch_bounds__(256) void k_conv_halo(rnvp_conv_args a, int shards)
                 for (int e = 0; e < CH; e += 4) {
                     const floatx4 sc = *(const floatx4*)&bnp[c0 + e];
                     const floatx4 sh = *(const floatx4*)&bnp[cs + c0 + e];
-                    const floatx4 mu = *(const floatx4*)&bnp[2 * cs + c0 + e];
-                    f[e] = fmaxf(bn_apply(f[e], sc.x, mu.x, sh.x), 0.f);
-                    f[e + 1] = fmaxf(bn_apply(f[e + 1], sc.y, mu.y, sh.y), 0.f);
-                    f[e + 2] = fmaxf(bn_apply(f[e + 2], sc.z, mu.z, sh.z), 0.f);
-                    f[e + 3] = fmaxf(bn_apply(f[e + 3], sc.w, mu.w, sh.w), 0.f);
+                    f[e] = fmaxf(f[e] * sc.x + sh.x, 0.f);
+                    f[e + 1] = fmaxf(f[e + 1] * sc.y + sh.y, 0.f);
+                    f[e + 2] = fmaxf(f[e + 2] * sc.z + sh.z, 0.f);
+                    f[e + 3] = fmaxf(f[e + 3] * sc.w + sh.w, 0.f);
                 }
                 w = pack(f, T());
             }
@@ -827,7 +824,7 @@ __global__ __launch_bounds__(256) void k_conv_halo(rnvp_conv_args a, int shards)
     if (PRO) tab_issue(a.pro, a.cin, 0, cs, ptab);
     if (epi_bn) tab_issue(a.epi, N, n0, BN, etb);
     stage_load(0);
-    if (PRO) tab_finish(a.pro, a.cin, 0, cs, ptab, bnp, bnp + cs, bnp + 2 * cs, nullptr);
+    if (PRO) tab_finish(a.pro, a.cin, 0, cs, ptab, bnp, bnp + cs, nullptr, nullptr);
     if (epi_bn) tab_finish(a.epi, N, n0, BN, etb, etab, etab + BN, etab + 2 * BN, etab + 3 * BN);
     for (int c = tid; c < BN; c += 256) btab[c] = (a.bias && n0 + c < N) ? a.bias[n0 + c] : 0.f;
     for (int c = tid * CH; c < pitch; c += 256 * CH) *(u32x4*)(zrow + c) = u32x4{0u, 0u, 0u, 0u};
@@ -1045,7 +1042,7 @@ size_t band_lds_bytes(int cs, int n, int W, int ks) {
     const int kpl = ((K + KS - 1) / KS) * KS + CH;
     const int R = BM + 2 * (ks / 2) * (W + 1);
     const int ntmp = cs > nc ? cs : nc;
-    return 16 * (size_t)ntmp + 12 * (size_t)cs + 20 * (size_t)nc + 64 * (size_t)nc +
+    return 16 * (size_t)ntmp + 8 * (size_t)cs + 20 * (size_t)nc + 64 * (size_t)nc +
            ((size_t)nc * kpl + (size_t)(R + 1) * (cs + CH)) * sizeof(T);
 }
 
@@ -1069,8 +1066,8 @@ __global__ __launch_bounds__(256) void k_conv_band(rnvp_conv_args a, int shards)
     const int pitch = cs + CH;                 // band row pitch (+16 B)
 
     double* tmp = dsm;
-    float* bnp = (float*)(dsm + 2 * ntmp);     // scale | beta | mean [cs each]
-    float* etab = bnp + 3 * cs;                // scale | beta | mean | rstd [NC each]
+    float* bnp = (float*)(dsm + 2 * ntmp);     // scale | shift [cs each]
+    float* etab = bnp + 2 * cs;                // scale | shift | mean | rstd [NC each]
     float* btab = etab + 4 * NC;               // bias [NC]
     double* red = (double*)(btab + NC);        // [4 waves][NC][2]
     T* Wl = (T*)(red + 8 * NC);                // [NC][kpl]
@@ -1114,11 +1111,10 @@ __global__ __launch_bounds__(256) void k_conv_band(rnvp_conv_args a, int shards)
                 for (int e = 0; e < CH; e += 4) {
                     const floatx4 sc = *(const floatx4*)&bnp[c0 + e];
                     const floatx4 sh = *(const floatx4*)&bnp[cs + c0 + e];
-                    const floatx4 mu = *(const floatx4*)&bnp[2 * cs + c0 + e];
-                    f[e] = fmaxf(bn_apply(f[e], sc.x, mu.x, sh.x), 0.f);
-                    f[e + 1] = fmaxf(bn_apply(f[e + 1], sc.y, mu.y, sh.y), 0.f);
-                    f[e + 2] = fmaxf(bn_apply(f[e + 2], sc.z, mu.z, sh.z), 0.f);
-                    f[e + 3] = fmaxf(bn_apply(f[e + 3], sc.w, mu.w, sh.w), 0.f);
+                    f[e] = fmaxf(f[e] * sc.x + sh.x, 0.f);
+                    f[e + 1] = fmaxf(f[e + 1] * sc.y + sh.y, 0.f);
+                    f[e + 2] = fmaxf(f[e + 2] * sc.z + sh.z, 0.f);
+                    f[e + 3] = fmaxf(f[e + 3] * sc.w + sh.w, 0.f);
                 }
                 w = pack(f, T());
             }
@@ -1129,7 +1125,7 @@ __global__ __launch_bounds__(256) void k_conv_band(rnvp_conv_args a, int shards)
     stage_load(0);
 
     // ---- BN tables, packed weights (rows >= N and k >= K zero) and bias -> LDS
-    if (PRO) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + cs, bnp + 2 * cs, nullptr, tmp);
+    if (PRO) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + cs, nullptr, nullptr, tmp);
     if (epi_bn) block_bn_table(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp);
     {
         const T* Wg = (const T*)a.w;
@@ -1347,7 +1343,7 @@ __device__ __forceinline__ void wgrad_tile(const WgView& a, int co0, int k0, lon
     __shared__ __attribute__((aligned(16))) char Ps[2][STG * ROWB];
     __shared__ __attribute__((aligned(16))) char Qs[2][STG * ROWB];
     __shared__ float dbs[64];
-    extern __shared__ double dsm[];   // tmp [2*cs] fp64 | bnp scale | beta | mean [cs each]
+    extern __shared__ double dsm[];   // tmp [2*cs] fp64 | bnp scale [cs] | shift [cs]
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wc = wid >> 1, wk = wid & 1;
@@ -1414,8 +1410,7 @@ __device__ __forceinline__ void wgrad_tile(const WgView& a, int co0, int k0, lon
                 float f[CH];
                 unpack(v, f, T());
 #pragma unroll
-                for (int j = 0; j < CH; ++j)
-                    f[j] = fmaxf(bn_apply(f[j], bnp[pci + j], bnp[2 * cs + pci + j], bnp[cs + pci + j]), 0.f);
+                for (int j = 0; j < CH; ++j) f[j] = fmaxf(f[j] * bnp[pci + j] + bnp[cs + pci + j], 0.f);
                 v = pack(f, T());
             }
             *(u32x4*)(Ps[buf] + r * ROWB + sc_ * 16) = rp[u][i] & u32x4{kp, kp, kp, kp};
@@ -1427,7 +1422,7 @@ __device__ __forceinline__ void wgrad_tile(const WgView& a, int co0, int k0, lon
 #pragma unroll
         for (int u = 0; u < D; ++u) gload(u, mb + (long long)u * STG);
     }
-    if (pro) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + cs, bnp + 2 * cs, nullptr, dsm);
+    if (pro) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + cs, nullptr, nullptr, dsm);
     __syncthreads();
     if (nst > 0) lstore(0, 0);
     __syncthreads();
@@ -1873,7 +1868,7 @@ extern "C" int rnvp_conv2d_wgrad_grouped(const rnvp_wgrad_group* gin, void* stre
     }
     if (tasks <= 0 || tasks > (1ll << 30)) return RNVP_E_INVALID;
     hipStream_t s = (hipStream_t)stream;
-    const size_t shm = 28 * (size_t)max_cs;
+    const size_t shm = 24 * (size_t)max_cs;
     if (g.dtype == RNVP_F32) k_wgrad_grouped<float><<<(unsigned)tasks, 256, shm, s>>>(g);
     else k_wgrad_grouped<bf16_t><<<(unsigned)tasks, 256, shm, s>>>(g);
     RNVP_LAUNCH_CHECK();

@@ -116,7 +116,7 @@ __device__ __forceinline__ double csum(const double* sums, int width, int i) {
     return t;
 }
 
-// per-channel in_bn table of the in part: scale, beta, mean, rstd [Cb each]
+// per-channel in_bn table of the in part: scale, shift, mean, rstd [Cb each]
 __device__ __forceinline__ void in_bn_table(const rnvp_coupling_args& a, const Geo& g, float* t) {
     for (int cb = threadIdx.x; cb < g.Cb; cb += blockDim.x) {
         rnvp_bn_src s;
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(256) void k_in_apply(rnvp_coupling_args a, int TP, 
         const int c = (g.kind == 0) ? cb : g.off_base + cb;
         float v = a.x[((long long)t.b * g.C + c) * g.HW + p];
         if (g.kind == 0 && !ckbd_m(g, p)) v = 0.f;
-        const float xa = bn_apply(v, tab[cb], tab[2 * g.Cb + cb], tab[g.Cb + cb]);
+        const float xa = v * tab[cb] + tab[g.Cb + cb];
         stv(&h[pl * cs + cb], fmaxf(xa, 0.f));
         stv(&h[pl * cs + g.Cb + cb], fmaxf(-xa, 0.f));
     }
@@ -520,7 +520,7 @@ __device__ __forceinline__ void in_bwd_vals(const rnvp_coupling_args& a, const G
     const int p = t.p0 + pl;
     float v = a.x[((long long)t.b * g.C + c) * g.HW + p];
     if (g.kind == 0 && !ckbd_m(g, p)) v = 0.f;
-    const float xa = bn_apply(v, tab[cb], tab[2 * g.Cb + cb], tab[g.Cb + cb]);
+    const float xa = v * tab[cb] + tab[g.Cb + cb];
     const float g1 = ldv(&gh[pl * a.cs_gh0 + cb]);
     const float g2 = ldv(&gh[pl * a.cs_gh0 + g.Cb + cb]);
     gxa = (xa > 0.f ? g1 : 0.f) - (xa < 0.f ? g2 : 0.f);

@@ -17,14 +17,32 @@ def _phase(name: str) -> float:
 _DEVICE = None   # formula_state(..., device=d): evaluate the sinusoids there (big models)
 
 
+_CHIRP = 0.0     # formula_state(..., style="chirp"): quadratic phase term
+
+
 def _wave(name, shape, freq, amp, offset):
+    """offset + amp * sin(freq*i + phase(name) [+ c*i^2]).  The plain wave makes
+    every conv weight matrix rank 2 (sin(a*i + b) separates over the row and
+    column index), so some channels are near-degenerate and ReLU decisions
+    become rounding-sensitive; the chirp term (style="chirp") couples the
+    indices and gives full-rank weights (the deep R=8 coupling goldens)."""
     n = int(np.prod(shape)) if len(shape) else 1
     if _DEVICE is not None:
         i = torch.arange(n, dtype=torch.float64, device=_DEVICE)
-        return (offset + amp * torch.sin(freq * i + _phase(name))).float().reshape(shape)
+        return (offset + amp * torch.sin(freq * i + _phase(name) + _CHIRP * i * i)).float().reshape(shape)
     i = np.arange(n, dtype=np.float64)
-    v = offset + amp * np.sin(freq * i + _phase(name))
+    v = offset + amp * np.sin(freq * i + _phase(name) + _CHIRP * i * i)
     return torch.from_numpy(v.astype(np.float32)).reshape(shape)
+
+
+def chirp_value(name, shape, trainable):
+    """formula_value with full-rank (chirped) weights"""
+    global _CHIRP
+    _CHIRP = 2.3e-4
+    try:
+        return formula_value(name, shape, trainable)
+    finally:
+        _CHIRP = 0.0
 
 
 def formula_value(name: str, shape, trainable: bool) -> torch.Tensor:
@@ -55,18 +73,19 @@ def formula_value(name: str, shape, trainable: bool) -> torch.Tensor:
     raise KeyError(name)
 
 
-def formula_state(module: torch.nn.Module, device=None):
+def formula_state(module: torch.nn.Module, device=None, style="wave"):
     """A full state dict for ``module`` (reference or engine: same keys).
     device: evaluate on that torch device (float64 sin, rounded to float32 --
     equal to the numpy path up to the last float32 bit of a few elements;
     used for the 0.9 B-parameter config-3 model)."""
     global _DEVICE
     trainable = {n for n, p in module.named_parameters() if p.requires_grad}
+    value = chirp_value if style == "chirp" else formula_value
     out = {}
     _DEVICE = device
     try:
         for k, v in module.state_dict().items():
-            t = formula_value(k, v.shape, k in trainable)
+            t = value(k, v.shape, k in trainable)
             out[k] = (t.to(device) if device is not None else t).to(v.dtype)
     finally:
         _DEVICE = None

@@ -100,10 +100,10 @@ def run_case(B, H, W, cin, cout, ks, dtype, pro=False, residual=False, acc=False
         src, k1, gam, bet, mean, rstd = bn_src(x, cin)
         keep.append(k1)
         a.pro_bn_relu, a.pro = 1, src
-        # the kernels form fp32 scale = gamma*rstd and mean, apply
-        # (x - mean) * scale + beta, then round act to the operand type
+        # the kernels form fp32 scale/shift, then round act to the operand type
         scale = (gam * rstd).float().double()
-        act = rnd(torch.relu((x - mean.float().double()) * scale + bet))
+        shift = (bet - mean.float().double() * gam * rstd).float().double()
+        act = rnd(torch.relu(x * scale + shift))
     sh = stat_shards(M)
     osums = torch.zeros(sh, 2, cout, dtype=torch.float64, device=DEV)
     if stats and not dgrad:
@@ -133,7 +133,8 @@ def run_case(B, H, W, cin, cout, ks, dtype, pro=False, residual=False, acc=False
     s1 = s2 = None
     if dgrad:
         escale = (egam * erstd).float().double()
-        ref = ref * (((ex - emean.float().double()) * escale + ebet) > 0)
+        eshift = (ebet - emean.float().double() * egam * erstd).float().double()
+        ref = ref * ((ex * escale + eshift) > 0)
         xhat = (ex - emean.float().double()) * erstd
         s1, s2 = ref.sum(0), (ref * xhat).sum(0)
     elif stats:

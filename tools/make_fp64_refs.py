@@ -24,21 +24,21 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import realnvp_oracle as O  # noqa: E402
-from formula_init import formula_value, pixels, uniform_noise  # noqa: E402
+from formula_init import chirp_value, formula_value, pixels, uniform_noise  # noqa: E402
 
 OUT = os.path.join(ROOT, "tests", "golden")
 torch.set_num_threads(8)
 
 
-def f64_state(entries):
-    return {k: (v.double() if v.is_floating_point() else v) for k, v in O.build_state(entries, formula_value).items()}
+def f64_state(entries, value=formula_value):
+    return {k: (v.double() if v.is_floating_point() else v) for k, v in O.build_state(entries, value).items()}
 
 
 def coupling(name, kind, cio, mid, hk):
     g = np.load(os.path.join(OUT, "coupling_%s.npz" % name))
     hp = O.HP(**hk)
     entries = O.coupling_spec("", kind, cio, mid, hp)
-    S = f64_state(entries)
+    S = f64_state(entries, chirp_value if "_r8_" in name else formula_value)
     train = O.trainable_names(entries)
     for n in train:
         S[n].requires_grad_(True)

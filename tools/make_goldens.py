@@ -122,7 +122,8 @@ COUPLING_CASES = [
 
 
 # deep nets (BASELINE config 3 / the reference CLI default R8 D64,
-# main.py:231-240): an R=8 coupling crosses the 24-conv grouped-wgrad chunk
+# main.py:231-240), with full-rank chirped formula weights
+# (tests/formula_init.py:chirp_value): an R=8 coupling crosses the 24-conv grouped-wgrad chunk
 # (4R+3 = 35 convs); the mid-1024 channelwise coupling is c3's scale-4 shape
 # (C = 96 at 2x2), ~100 M parameters, so only per-tensor gradient norms and the
 # small tensors' full gradients are stored (weights come from formula_init).
@@ -145,7 +146,7 @@ def coupling_goldens(cases=None):
         t0 = time.time()
         hp = hps(**hk)
         mod = make_coupling(kind, cio, mid, size, cfg, hp)
-        mod.load_state_dict(formula_state(mod))
+        mod.load_state_dict(formula_state(mod, style="chirp" if "_r8_" in name else "wave"))
         g = torch.Generator().manual_seed(zlib.crc32(name.encode()) % 1000)
         x = torch.randn(B, cio, size, size, generator=g)
         gy = torch.randn(B, cio, size, size, generator=g)
