@@ -20,8 +20,10 @@
 // MFMA: bf16 -> v_mfma_f32_16x16x32_bf16 (fp32 accumulate);
 //       f32  -> v_mfma_f32_16x16x4_f32 (exact fp32, parity mode).
 #include <math.h>
+#include <stdlib.h>
 
 #include "common.h"
+#include "conv_common.h"
 
 extern "C" int rnvp_stat_shards(long long M) {
     long long s = M / 8192;
@@ -31,76 +33,6 @@ extern "C" int rnvp_stat_shards(long long M) {
 }
 
 namespace {
-
-template <typename T> struct Mf;
-template <> struct Mf<bf16_t> {
-    static constexpr int CH = 8;
-    __device__ static __forceinline__ void step(const u32x4& a, const u32x4& b, floatx4& c) {
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
-    }
-};
-template <> struct Mf<float> {
-    static constexpr int CH = 4;
-    // lane group g supplies k = 4g + s at sub-step s (same mapping for A and B)
-    __device__ static __forceinline__ void step(const u32x4& a, const u32x4& b, floatx4& c) {
-        c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), c, 0, 0, 0);
-    }
-};
-
-// [row][8 chunks of 16 B]; XOR swizzle spreads the 16 rows one ds_read_b128
-// lane group reads over all 64 banks (rows r, r+1 differ in bank half, r>>1
-// picks the chunk).
-__device__ __forceinline__ int sw8(int row, int c) { return row * 8 + (c ^ ((row >> 1) & 7)); }
-
-__device__ __forceinline__ double* shard_ptr(double* sums, int shards, int N) {
-    return sums ? sums + (long long)(blockIdx.x % shards) * 2 * N : nullptr;
-}
-
-// 4-channel epilogue in the transposed layout: y = acc + bias (+ residual)
-// (+ y), or the dgrad ReLU/BN-backward form; BN statistics into s1/s2.
-// et: LDS epilogue table at channel n0 (scale | shift | mean | rstd, pitch).
-template <typename T>
-__device__ __forceinline__ void epi4(const rnvp_conv_args& a, long long o, const floatx4& acc, const float* bias,
-                                     bool epi_bn, const float* et, int pitch, double* s1, double* s2, int nvalid) {
-    float v[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = acc[r] + bias[r];
-    if (a.residual) {
-        float t[4];
-        ld4((const T*)a.residual + o, t);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += t[r];
-    }
-    if (a.accumulate) {
-        float t[4];
-        ld4((const T*)a.y + o, t);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += t[r];
-    }
-    if (epi_bn) {
-        float xv[4];
-        ld4((const T*)a.epi_x + o, xv);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            if (xv[r] * et[r] + et[pitch + r] <= 0.f) v[r] = 0.f;
-            s1[r] += v[r];
-            s2[r] += v[r] * (xv[r] - et[2 * pitch + r]) * et[3 * pitch + r];
-        }
-    } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            s1[r] += v[r];
-            s2[r] += (double)v[r] * v[r];
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-        if (r >= nvalid) v[r] = 0.f;
-    st4((T*)a.y + o, v);
-}
 
 // ---------------------------------------------------------------------------
 // forward / data-gradient conv
@@ -556,7 +488,8 @@ int launch_stream(const rnvp_conv_args* a, hipStream_t s) {
     const long long M = (long long)a->B * a->H * a->W;
     const long long ntiles = (M + 16 * TW - 1) / (16 * TW);
     long long grid = (ntiles + 3) / 4;
-    if (grid > 2048) grid = 2048;
+    static const long long cap = [] { const char* e = getenv("RNVP_STREAM_GRID"); return e ? atoll(e) : 2048ll; }();
+    if (grid > cap) grid = cap;
     k_conv_stream<T, NT, TW><<<(unsigned)grid, 256, stream_lds_bytes<T>(a, NT), s>>>(*a, rnvp_stat_shards(M));
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
@@ -639,88 +572,6 @@ constexpr int DK_MAX_CS = 1024;
 // memory (register ring, DK k-steps ahead; every load unconditional).  The
 // four waves split K (interleaved k-steps) and their partial tiles are summed
 // through LDS for the fused epilogue, as in k_conv_dk.
-template <typename T>
-__host__ __device__ constexpr int halo_pitch(int cs) { return cs + Mf<T>::CH; }
-
-
-// BN table for channels [c0, c0+nc) of a source with <= 2 stat shards, in
-// registers (CPT channels per thread, no LDS atomics): tab_issue loads
-// (unconditional, clamped addresses, so the loads can stay in flight behind
-// later ones), tab_finish forms scale/shift (+ mean, rstd) into LDS.
-template <int CPT>
-struct BnTab {
-    double a1[CPT], a2[CPT], b1[CPT], b2[CPT];
-    float gam[CPT], bet[CPT];
-};
-
-template <int CPT>
-__device__ __forceinline__ void tab_issue(const rnvp_bn_src& s, int C, int c0, int nc, BnTab<CPT>& t) {
-#pragma unroll
-    for (int j = 0; j < CPT; ++j) {
-        const int c = threadIdx.x + 256 * j;
-        const int cc = (c < nc && c0 + c < C) ? c0 + c : 0;
-        if (s.sums) {
-            t.a1[j] = s.sums[cc];
-            t.a2[j] = s.sums[C + cc];
-            const int h1 = s.shards > 1 ? 1 : 0;
-            t.b1[j] = s.sums[(long long)h1 * 2 * C + cc];
-            t.b2[j] = s.sums[(long long)h1 * 2 * C + C + cc];
-        } else {
-            t.a1[j] = s.mean[cc];
-            t.a2[j] = s.var[cc];
-            t.b1[j] = t.b2[j] = 0.0;
-        }
-        t.gam[j] = s.gamma ? s.gamma[cc] : 1.f;
-        t.bet[j] = s.beta ? s.beta[cc] : 0.f;
-    }
-}
-
-template <int CPT>
-__device__ __forceinline__ void tab_finish(const rnvp_bn_src& s, int C, int c0, int nc, const BnTab<CPT>& t,
-                                           float* scale, float* shift, float* mean_out, float* rstd_out) {
-    const double inv = s.sums ? 1.0 / s.count : 0.0;
-#pragma unroll
-    for (int j = 0; j < CPT; ++j) {
-        const int c = threadIdx.x + 256 * j;
-        if (c >= nc) continue;
-        float sc = 0.f, sf = 0.f, mo = 0.f, ro = 1.f;
-        if (c0 + c < C) {
-            double mean, var;
-            if (s.sums) {
-                const double s1 = t.a1[j] + (s.shards > 1 ? t.b1[j] : 0.0);
-                const double s2 = t.a2[j] + (s.shards > 1 ? t.b2[j] : 0.0);
-                mean = s1 * inv;
-                var = s2 * inv - mean * mean;
-                if (var < 0) var = 0;
-            } else {
-                mean = t.a1[j];
-                var = t.a2[j];
-            }
-            const float rstd = (float)(1.0 / sqrt(var + (double)s.eps));
-            sc = t.gam[j] * rstd;
-            sf = t.bet[j] - (float)mean * t.gam[j] * rstd;
-            mo = (float)mean;
-            ro = rstd;
-        }
-        scale[c] = sc;
-        shift[c] = sf;
-        if (mean_out) mean_out[c] = mo;
-        if (rstd_out) rstd_out[c] = ro;
-    }
-}
-
-// floor(q / d) for 0 <= q < 2^22 from a float reciprocal r = 1/d: q + 0.5 is
-// >= 0.5 away from any multiple of d, far more than the rounding error.
-__device__ __forceinline__ int fdiv_small(int q, float r) { return (int)(((float)q + 0.5f) * r); }
-
-// floor(q / d) for 0 <= q < 2^31 with q / d < 2^22 (r = 1/d): the float
-// quotient is within 0.75 of the true one, one correction step each way.
-__device__ __forceinline__ int fdiv_exact(int q, int d, float r) {
-    int t = (int)((float)q * r);
-    t -= (t * d > q) ? 1 : 0;
-    t += ((t + 1) * d <= q) ? 1 : 0;
-    return t;
-}
 
 template <typename T, int BN>
 size_t halo_lds_bytes(int cs, int W, int ks) {
@@ -1302,7 +1153,13 @@ int dispatch_band(const rnvp_conv_args* a, hipStream_t s) {
 template <typename T>
 int dispatch_conv(const rnvp_conv_args* a, hipStream_t s) {
     const long long M = (long long)a->B * a->H * a->W;
-    const bool tuned = a->variant == 0;
+    // forced deep-scale configuration (A/B and parity tests): no fallback
+    if (a->variant >= RNVP_VARIANT_DEEP0) return rnvp_deep_launch(a, s, a->variant - RNVP_VARIANT_DEEP0);
+    if (a->variant == RNVP_VARIANT_DEEP) {
+        const int r = rnvp_deep_launch(a, s, rnvp_deep_auto_cfg(a));
+        if (r != RNVP_E_UNSUPPORTED) return r;
+    }
+    const bool tuned = a->variant != 1;
     if (tuned && band_ok<T>(a)) return dispatch_band<T>(a, s);
     if (stream_ok<T>(a)) return dispatch_stream<T>(a, s);
     if (tuned && halo_ok<T>(a)) return dispatch_halo<T>(a, s);
@@ -1815,7 +1672,9 @@ inline bool al16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
 
 extern "C" int rnvp_conv2d(const rnvp_conv_args* a, void* stream) {
     if (!a || !a->x || !a->w || !a->y) return RNVP_E_INVALID;
-    if (a->variant < 0 || a->variant > 1) return RNVP_E_INVALID;
+    if (a->variant < 0 || (a->variant > RNVP_VARIANT_DEEP && a->variant < RNVP_VARIANT_DEEP0) ||
+        a->variant >= RNVP_VARIANT_DEEP0 + RNVP_DEEP_CFGS)
+        return RNVP_E_INVALID;
     if (a->dtype != RNVP_F32 && a->dtype != RNVP_BF16) return RNVP_E_INVALID;
     if (a->ks != 1 && a->ks != 3) return RNVP_E_UNSUPPORTED;
     if (a->B < 0 || a->H <= 0 || a->W <= 0 || a->n <= 0 || a->cin <= 0) return RNVP_E_INVALID;

@@ -1,0 +1,222 @@
+// Device helpers shared by the conv kernel translation units (conv.hip,
+// conv_deep.hip): MFMA step per operand type, LDS swizzle, BN-statistics
+// shards, the fused 4-channel epilogue, register BN tables, fast division.
+// Included inside each file's anonymous namespace.
+#pragma once
+#include <math.h>
+
+#include "common.h"
+
+namespace {
+
+template <typename T> struct Mf;
+template <> struct Mf<bf16_t> {
+    static constexpr int CH = 8;
+    __device__ static __forceinline__ void step(const u32x4& a, const u32x4& b, floatx4& c) {
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+    }
+};
+template <> struct Mf<float> {
+    static constexpr int CH = 4;
+    // lane group g supplies k = 4g + s at sub-step s (same mapping for A and B)
+    __device__ static __forceinline__ void step(const u32x4& a, const u32x4& b, floatx4& c) {
+        c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), c, 0, 0, 0);
+    }
+};
+
+// [row][8 chunks of 16 B]; XOR swizzle spreads the 16 rows one ds_read_b128
+// lane group reads over all 64 banks (rows r, r+1 differ in bank half, r>>1
+// picks the chunk).
+__device__ __forceinline__ int sw8(int row, int c) { return row * 8 + (c ^ ((row >> 1) & 7)); }
+
+__device__ __forceinline__ double* shard_ptr(double* sums, int shards, int N) {
+    return sums ? sums + (long long)(blockIdx.x % shards) * 2 * N : nullptr;
+}
+
+// 4-channel epilogue in the transposed layout: y = acc + bias (+ residual)
+// (+ y), or the dgrad ReLU/BN-backward form; BN statistics into s1/s2.
+// et: LDS epilogue table at channel n0 (scale | shift | mean | rstd, pitch).
+template <typename T>
+__device__ __forceinline__ void epi4(const rnvp_conv_args& a, long long o, const floatx4& acc, const float* bias,
+                                     bool epi_bn, const float* et, int pitch, double* s1, double* s2, int nvalid) {
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = acc[r] + bias[r];
+    if (a.residual) {
+        float t[4];
+        ld4((const T*)a.residual + o, t);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += t[r];
+    }
+    if (a.accumulate) {
+        float t[4];
+        ld4((const T*)a.y + o, t);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += t[r];
+    }
+    if (epi_bn) {
+        float xv[4];
+        ld4((const T*)a.epi_x + o, xv);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            if (xv[r] * et[r] + et[pitch + r] <= 0.f) v[r] = 0.f;
+            s1[r] += v[r];
+            s2[r] += v[r] * (xv[r] - et[2 * pitch + r]) * et[3 * pitch + r];
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            s1[r] += v[r];
+            s2[r] += (double)v[r] * v[r];
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        if (r >= nvalid) v[r] = 0.f;
+    st4((T*)a.y + o, v);
+}
+
+// the epilogue operands of one 4-channel element (residual, previous y for
+// the skip accumulation, the dgrad epilogue's pre-BN x), loaded at kernel
+// start so the epilogue waits on no global round trip
+struct EpiPre {
+    float r[4], y[4], x[4];
+};
+
+template <typename T>
+__device__ __forceinline__ void epi_prefetch(const rnvp_conv_args& a, long long o, bool live, EpiPre& p) {
+    const long long oo = live ? o : 0;
+    if (a.residual) ld4((const T*)a.residual + oo, p.r);
+    if (a.accumulate) ld4((const T*)a.y + oo, p.y);
+    if (a.epi_relu_bn_bwd) ld4((const T*)a.epi_x + oo, p.x);
+}
+
+// epi4 over prefetched operands
+template <typename T>
+__device__ __forceinline__ void epi4p(const rnvp_conv_args& a, long long o, const floatx4& acc, const float* bias,
+                                      bool epi_bn, const float* et, int pitch, double* s1, double* s2, int nvalid,
+                                      const EpiPre& p) {
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = acc[r] + bias[r];
+    if (a.residual) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += p.r[r];
+    }
+    if (a.accumulate) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += p.y[r];
+    }
+    if (epi_bn) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            if (p.x[r] * et[r] + et[pitch + r] <= 0.f) v[r] = 0.f;
+            s1[r] += v[r];
+            s2[r] += v[r] * (p.x[r] - et[2 * pitch + r]) * et[3 * pitch + r];
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            s1[r] += v[r];
+            s2[r] += (double)v[r] * v[r];
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        if (r >= nvalid) v[r] = 0.f;
+    st4((T*)a.y + o, v);
+}
+
+template <typename T>
+__host__ __device__ constexpr int halo_pitch(int cs) { return cs + Mf<T>::CH; }
+
+
+// BN table for channels [c0, c0+nc) of a source with <= 2 stat shards, in
+// registers (CPT channels per thread of NT, no LDS atomics): tab_issue loads
+// (unconditional, clamped addresses, so the loads can stay in flight behind
+// later ones), tab_finish forms scale/shift (+ mean, rstd) into LDS.
+template <int CPT>
+struct BnTab {
+    double a1[CPT], a2[CPT], b1[CPT], b2[CPT];
+    float gam[CPT], bet[CPT];
+};
+
+template <int CPT, int NT = 256>
+__device__ __forceinline__ void tab_issue(const rnvp_bn_src& s, int C, int c0, int nc, BnTab<CPT>& t) {
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+        const int c = threadIdx.x + NT * j;
+        const int cc = (c < nc && c0 + c < C) ? c0 + c : 0;
+        if (s.sums) {
+            t.a1[j] = s.sums[cc];
+            t.a2[j] = s.sums[C + cc];
+            const int h1 = s.shards > 1 ? 1 : 0;
+            t.b1[j] = s.sums[(long long)h1 * 2 * C + cc];
+            t.b2[j] = s.sums[(long long)h1 * 2 * C + C + cc];
+        } else {
+            t.a1[j] = s.mean[cc];
+            t.a2[j] = s.var[cc];
+            t.b1[j] = t.b2[j] = 0.0;
+        }
+        t.gam[j] = s.gamma ? s.gamma[cc] : 1.f;
+        t.bet[j] = s.beta ? s.beta[cc] : 0.f;
+    }
+}
+
+template <int CPT, int NT = 256>
+__device__ __forceinline__ void tab_finish(const rnvp_bn_src& s, int C, int c0, int nc, const BnTab<CPT>& t,
+                                           float* scale, float* shift, float* mean_out, float* rstd_out) {
+    const double inv = s.sums ? 1.0 / s.count : 0.0;
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+        const int c = threadIdx.x + NT * j;
+        if (c >= nc) continue;
+        float sc = 0.f, sf = 0.f, mo = 0.f, ro = 1.f;
+        if (c0 + c < C) {
+            double mean, var;
+            if (s.sums) {
+                const double s1 = t.a1[j] + (s.shards > 1 ? t.b1[j] : 0.0);
+                const double s2 = t.a2[j] + (s.shards > 1 ? t.b2[j] : 0.0);
+                mean = s1 * inv;
+                var = s2 * inv - mean * mean;
+                if (var < 0) var = 0;
+            } else {
+                mean = t.a1[j];
+                var = t.a2[j];
+            }
+            const float rstd = (float)(1.0 / sqrt(var + (double)s.eps));
+            sc = t.gam[j] * rstd;
+            sf = t.bet[j] - (float)mean * t.gam[j] * rstd;
+            mo = (float)mean;
+            ro = rstd;
+        }
+        scale[c] = sc;
+        shift[c] = sf;
+        if (mean_out) mean_out[c] = mo;
+        if (rstd_out) rstd_out[c] = ro;
+    }
+}
+
+// floor(q / d) for 0 <= q < 2^22 from a float reciprocal r = 1/d: q + 0.5 is
+// >= 0.5 away from any multiple of d, far more than the rounding error.
+__device__ __forceinline__ int fdiv_small(int q, float r) { return (int)(((float)q + 0.5f) * r); }
+
+// floor(q / d) for 0 <= q < 2^31 with q / d < 2^22 (r = 1/d): the float
+// quotient is within 0.75 of the true one, one correction step each way.
+__device__ __forceinline__ int fdiv_exact(int q, int d, float r) {
+    int t = (int)((float)q * r);
+    t -= (t * d > q) ? 1 : 0;
+    t += ((t + 1) * d <= q) ? 1 : 0;
+    return t;
+}
+
+}  // namespace
+
+// deep-scale conv family (conv_deep.hip): number of configurations and the
+// launcher of configuration cfg (RNVP_E_UNSUPPORTED when it does not apply)
+constexpr int RNVP_DEEP_CFGS = 4;
+int rnvp_deep_launch(const rnvp_conv_args* a, hipStream_t s, int cfg);
+int rnvp_deep_auto_cfg(const rnvp_conv_args* a);

@@ -109,8 +109,13 @@ int rnvp_bn_running_update(const rnvp_bn_running* descs_device, int n, int max_c
  * (ws: fp32, >= splits * M * n elements; the epilogue then runs in a second
  * kernel that reduces the splits).
  * variant: 0 = automatic kernel choice per shape; 1 = the generic LDS-tiled
- * implicit GEMM (+ split-K) wherever the streaming kernel does not apply
+ * implicit GEMM (+ split-K) wherever the streaming kernel does not apply;
+ * RNVP_VARIANT_DEEP = the deep-scale family (LDS activation tile + weight
+ * ring) with its automatic configuration where it applies;
+ * RNVP_VARIANT_DEEP0 + c = that family's configuration c, no fallback
  * (per call: used by the parity tests to cross-check the kernel families). */
+#define RNVP_VARIANT_DEEP 2
+#define RNVP_VARIANT_DEEP0 16
 typedef struct rnvp_conv_args {
     int dtype;
     int B, H, W, ks;

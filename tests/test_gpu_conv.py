@@ -221,3 +221,35 @@ def test_band_matches_stream(case):
     b, _, _, _, _ = run_case(B, H, W, cin, cout, ks, "fp32", variant=1, **fl)
     assert rel(a, b) < 2e-6
     assert rel(b, ref) < 1e-5
+
+
+# deep-scale family (conv_deep.hip): every configuration against the float64
+# restatement, both dtypes; configurations that do not apply to a shape
+# (channel stride not a multiple of the k-step, LDS too small) are skipped
+DEEP_FAMILY = DEEP + [
+    ("s3_1x1_pro_stats", 64, 16, 16, 128, 128, 1, dict(pro=True, stats=True)),
+    ("s3_3x3_dgrad_res", 16, 16, 16, 128, 128, 3, dict(dgrad=True, residual=True, bias=False)),
+    ("s4_1x1_skip_acc", 16, 8, 8, 256, 256, 1, dict(acc=True, stats=True)),
+    ("s4_3x3_ragged_m", 3, 7, 9, 256, 200, 3, dict(pro=True, stats=True)),                # M % 64 != 0, N % 64 != 0
+    ("s2_1x1_64", 8, 32, 32, 64, 64, 1, dict(pro=True, residual=True, stats=True)),
+]
+DEEP_CFGS = 4
+VARIANT_DEEP0 = 16
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("cfg", range(DEEP_CFGS))
+@pytest.mark.parametrize("case", DEEP_FAMILY, ids=[c[0] for c in DEEP_FAMILY])
+def test_deep_family_vs_float64(case, cfg, dtype):
+    name, B, H, W, cin, cout, ks, fl = case
+    try:
+        got, ref, sums, s1, s2 = run_case(B, H, W, cin, cout, ks, dtype, variant=VARIANT_DEEP0 + cfg, **fl)
+    except RuntimeError as e:
+        if "unsupported" in str(e):
+            pytest.skip("configuration %d does not apply" % cfg)
+        raise
+    tol = 1e-5 if dtype == "fp32" else 4e-3
+    assert rel(got, ref) < tol, rel(got, ref)
+    if s1 is not None:
+        assert rel(sums[0], s1) < 10 * tol, rel(sums[0], s1)
+        assert rel(sums[1], s2) < 10 * tol, rel(sums[1], s2)

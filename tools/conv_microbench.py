@@ -140,6 +140,14 @@ CASES = [
     ("s4 3x3 256->256 dgrad", 64, 8, 8, 256, 256, 3, dict(dgrad_epi=True)),
     ("s3 1x1 128->128 pro+stats", 64, 16, 16, 128, 128, 1, dict(pro=True, stats=True)),
     ("s3 3x3 128->128 dgrad", 64, 16, 16, 128, 128, 3, dict(dgrad_epi=True)),
+    ("s3 1x1 128->128 pro+stats+res", 64, 16, 16, 128, 128, 1, dict(pro=True, stats=True, residual=True)),
+    ("s3 1x1 128->128 skip acc", 64, 16, 16, 128, 128, 1, dict(acc=True, stats=True)),
+    ("s3 1x1 128->128 dgrad", 64, 16, 16, 128, 128, 1, dict(dgrad_epi=True)),
+    ("s4 1x1 256->256 dgrad", 64, 8, 8, 256, 256, 1, dict(dgrad_epi=True)),
+    ("s4 1x1 256->256 skip acc", 64, 8, 8, 256, 256, 1, dict(acc=True, stats=True)),
+    ("s5 1x1 512->512 dgrad", 64, 4, 4, 512, 512, 1, dict(dgrad_epi=True)),
+    ("s5 1x1 512->512 skip acc", 64, 4, 4, 512, 512, 1, dict(acc=True, stats=True)),
+    ("s2c 1x1 64->64 pro+stats", 64, 32, 32, 64, 64, 1, dict(pro=True, stats=True)),
     ("wgrad s1 1x1 32", 64, 64, 64, 32, 32, 1, dict(pro=True, wgrad=True)),
     ("wgrad s1 3x3 32", 64, 64, 64, 32, 32, 3, dict(pro=True, wgrad=True)),
     ("wgrad s2 3x3 64", 64, 32, 32, 64, 64, 3, dict(pro=True, wgrad=True)),
@@ -152,6 +160,8 @@ CASES = [
 def main():
     torch.manual_seed(0)
     variants = [0, 1] if "--v01" in sys.argv else [0]
+    if "--deep" in sys.argv:   # the deep-scale family's configurations (RNVP_VARIANT_DEEP0 + c)
+        variants = [0] + [16 + c for c in range(4)]
     only = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--case=")]
     print("%-32s %3s %9s %9s %9s" % ("case", "var", "us", "GB/s", "TFLOP/s"))
     for name, B, H, W, ci, co, ks, fl in CASES:
@@ -160,7 +170,10 @@ def main():
         for v in variants:
             if fl.get("wgrad") and v:
                 continue
-            us, gbs, tfs = conv_case(B, H, W, ci, co, ks, variant=v, **fl)
+            try:
+                us, gbs, tfs = conv_case(B, H, W, ci, co, ks, variant=v, **fl)
+            except RuntimeError:
+                continue   # configuration does not apply to this shape
             print("%-32s %3d %9.1f %9.1f %9.1f" % (name, v, us, gbs, tfs), flush=True)
 
 
