@@ -431,13 +431,15 @@ int launch_cfg(const rnvp_conv_args* a, hipStream_t s, int cfg) {
 
 }  // namespace
 
+// measured (tools/conv_microbench.py --deep, profiles/r2_deep_microbench.txt):
+// the deep family beats the other families at M <= 1024 (every shape:
+// whole-tile-per-wave, K / 4) and for the 3x3 at M <= 4096 (64-channel
+// tiles); elsewhere -1 (the caller's other families)
 int rnvp_deep_auto_cfg(const rnvp_conv_args* a) {
     const long long M = (long long)a->B * a->H * a->W;
-    const long long gm = (M + DEEP_BM - 1) / DEEP_BM;
-    const bool wide = gm * ((a->n + 63) / 64) >= 256;   // 64-channel tiles still fill the chip
-    const int K = a->ks * a->ks * a->cs_in;
-    if (K <= 256) return wide ? 2 : 3;
-    return wide ? 1 : 0;
+    if (M <= 1024) return 0;
+    if (M <= 4096 && a->ks == 3) return 1;
+    return -1;
 }
 
 int rnvp_deep_launch(const rnvp_conv_args* a, hipStream_t s, int cfg) {

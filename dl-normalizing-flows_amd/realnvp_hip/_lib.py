@@ -51,7 +51,7 @@ class WNDesc(C.Structure):
     _fields_ = [("v", vp), ("g", vp), ("wf", vp), ("wd", vp), ("norm", vp),
                 ("dw", vp), ("dv_off", i64), ("dg_off", i64),
                 ("cout", i32), ("cin", i32), ("ks", i32), ("cs_in", i32), ("kp_f", i32),
-                ("cs_out", i32), ("kp_d", i32), ("row0", i32), ("col0", i32),
+                ("cs_out", i32), ("kp_d", i32), ("row0", i32), ("tile0", i32),
                 ("nz", i32), ("dbp", vp), ("db_off", i64), ("zero_after", i32)]
 
 
@@ -115,6 +115,7 @@ _SIGS = {
     "rnvp_conv2d_wgrad_grouped": (i32, [C.POINTER(WgradGroup), vp]),
     "rnvp_bn_bwd_apply": (i32, [C.POINTER(BNBwdArgs), vp]),
     "rnvp_weight_norm_fwd": (i32, [vp, i32, i32, i32, i32, vp]),
+    "rnvp_weight_norm_tiles": (i32, [i32, i32]),
     "rnvp_weight_norm_bwd": (i32, [vp, i32, i32, vp, vp]),
     "rnvp_coupling_in_fwd": (i32, [C.POINTER(CouplingArgs), vp]),
     "rnvp_coupling_out_fwd": (i32, [C.POINTER(CouplingArgs), vp]),
@@ -141,7 +142,8 @@ class _Lib:
             fn = getattr(self.dll, name)
             fn.restype = res
             fn.argtypes = args
-            raw = name in ("rnvp_version", "rnvp_stat_shards", "rnvp_wgrad_slabs", "rnvp_wgrad_replicas") or res is not i32
+            raw = name in ("rnvp_version", "rnvp_stat_shards", "rnvp_wgrad_slabs", "rnvp_wgrad_replicas",
+                           "rnvp_weight_norm_tiles") or res is not i32
             setattr(self, name[len("rnvp_"):], fn if raw else self._wrap(name, fn))
 
     def _wrap(self, name, fn):

@@ -110,6 +110,11 @@ def stat_shards(M):
     return int(_lib.lib().stat_shards(int(M)))
 
 
+def wn_tiles(cout, cin):
+    """pack tiles of one conv in rnvp_weight_norm_fwd (rnvp_weight_norm_tiles)"""
+    return int(_lib.lib().weight_norm_tiles(int(cout), int(cin)))
+
+
 _SPLITK_WS = {}
 
 
@@ -187,7 +192,7 @@ class CouplingEngine:
             ar.add("norm:" + name, spec.cout * 4)
         ar.alloc(dev, zero=True)   # zero padding of the packed images, once
         descs = []
-        row0 = col0 = 0
+        row0 = tile0 = 0
         for name, spec in self.P.convs.items():
             cs_in, cs_out, kp_f, kp_d = geo[name]
             vn, gn, _ = self._conv_names(spec)
@@ -201,19 +206,19 @@ class CouplingEngine:
             d.cout, d.cin, d.ks, d.cs_in, d.kp_f, d.cs_out, d.kp_d, d.row0 = (
                 spec.cout, spec.cin, spec.ks, cs_in, kp_f, cs_out, kp_d, row0)
             d.nz = 1
-            d.col0 = col0
+            d.tile0 = tile0
             row0 += spec.cout
-            col0 += spec.cin
+            tile0 += wn_tiles(spec.cout, spec.cin)
             descs.append(d)
         table = (WNDesc * len(descs))(*descs)
         dtab = torch.frombuffer(bytearray(bytes(table)), dtype=torch.uint8).to(dev)
-        ws = dict(key=key, arena=ar, geo=geo, descs=descs, table=dtab, rows=row0, cols=col0, dtype=dtype)
+        ws = dict(key=key, arena=ar, geo=geo, descs=descs, table=dtab, rows=row0, tiles=tile0, dtype=dtype)
         self._weights[dtype] = ws
         return ws
 
     def prepare_weights(self, dtype):
         ws = self.weights(dtype)
-        _lib.lib().weight_norm_fwd(ws["table"].data_ptr(), len(ws["descs"]), ws["rows"], ws["cols"],
+        _lib.lib().weight_norm_fwd(ws["table"].data_ptr(), len(ws["descs"]), ws["rows"], ws["tiles"],
                                    DTYPES[dtype][0], stream_ptr())
         return ws
 

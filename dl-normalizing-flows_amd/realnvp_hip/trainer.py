@@ -33,29 +33,30 @@ from .engine import stream_ptr
 def wn_table(engines, dtype, dev):
     """One weight-norm descriptor table over the convs of several couplings
     (rnvp_weight_norm_fwd refreshes all their packed weight images in two
-    launches).  None when there are no convs."""
+    launches: row norms, then both images on tiles).  None when there are no convs."""
     import ctypes as C
     from ._lib import WNDesc
+    from .engine import wn_tiles
     descs = []
-    row0 = col0 = 0
+    row0 = tile0 = 0
     for eng in engines:
         for d in eng.weights(dtype)["descs"]:
             e = WNDesc()
             C.memmove(C.addressof(e), C.addressof(d), C.sizeof(WNDesc))
-            e.row0, e.col0 = row0, col0
+            e.row0, e.tile0 = row0, tile0
             row0 += e.cout
-            col0 += e.cin
+            tile0 += wn_tiles(e.cout, e.cin)
             descs.append(e)
     if not descs:
         return None
     tab = (WNDesc * len(descs))(*descs)
     t = torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(dev)
-    return (t, len(descs), row0, col0)
+    return (t, len(descs), row0, tile0)
 
 
 def wn_forward(table, dtype):
-    t, n, rows, cols = table
-    _lib.lib().weight_norm_fwd(t.data_ptr(), n, rows, cols, 1 if dtype == "bf16" else 0, stream_ptr())
+    t, n, rows, tiles = table
+    _lib.lib().weight_norm_fwd(t.data_ptr(), n, rows, tiles, 1 if dtype == "bf16" else 0, stream_ptr())
 
 
 def arena_blocks(model):

@@ -191,15 +191,18 @@ typedef struct rnvp_wn_desc {
     long long dv_off; long long dg_off;
     int cout, cin, ks, cs_in, kp_f, cs_out, kp_d;
     int row0;                          /* first global row (prefix sum of cout) */
-    int col0;                          /* first global wd row (prefix sum of cin) */
+    int tile0;                         /* first pack tile (prefix sum of rnvp_weight_norm_tiles) */
     int nz;                            /* dw partial slabs (>= 1) */
     float* dbp;                        /* bias partials [nz][cout] or NULL */
     long long db_off;                  /* bias gradient offset (elements) */
     int zero_after;                    /* re-zero dw / dbp after use (atomic accumulation) */
 } rnvp_wn_desc;
-/* fwd: one launch over the rows (norm + wf) and one over the wd rows
- * (total_cols = sum of cin), for any number of convs (a whole model). */
-int rnvp_weight_norm_fwd(const rnvp_wn_desc* descs_device, int n_desc, int total_rows, int total_cols, int dtype,
+/* fwd, for any number of convs (a whole model): one launch computes every
+ * row norm, one writes both packed images on [32 co] x [32 ci] tiles
+ * (total_tiles = sum over the convs of rnvp_weight_norm_tiles(cout, cin)).
+ * The images' padding must be zero on entry (it is never written). */
+int rnvp_weight_norm_tiles(int cout, int cin);
+int rnvp_weight_norm_fwd(const rnvp_wn_desc* descs_device, int n_desc, int total_rows, int total_tiles, int dtype,
                          void* stream);
 int rnvp_weight_norm_bwd(const rnvp_wn_desc* descs_device, int n_desc, int total_rows, float* grad_base, void* stream);
 
