@@ -1190,21 +1190,22 @@ struct WgView {
     int H, W, ks, cs_in, cin, cs_dy, n, kp, pro_bn_relu;
 };
 
-// one [64 co] x [64 k] tile over pixels [mb, me): result to out[co*kp + k]
+// one [TC co] x [TC k] tile (TC = 64 or 128) over pixels [mb, me): result to out[co*kp + k]
 // (fp32 atomics or plain stores) and, when bias_out, the bias sums of the
 // tile's co columns to bias_out[co] (atomic or plain).
-template <typename T>
+template <typename T, int TC>
 __device__ __forceinline__ void wgrad_tile(const WgView& a, int co0, int k0, long long mb, long long me,
                                            long long M, float* out, bool atomic, float* bias_out, bool bias_atomic) {
     constexpr int CH = Mf<T>::CH;
     constexpr int STG = (sizeof(T) == 2) ? 64 : 32;   // pixels per stage (two MFMA K-steps)
-    constexpr int CPR = 64 / CH;                      // chunks per 64-column row
-    constexpr int ROWB = 64 * sizeof(T) + 16;         // padded row bytes
-    constexpr int PER = STG * CPR / 256;              // chunks per thread per operand (2)
-    constexpr int D = 4;                              // stages of global loads in flight per thread
+    constexpr int CPR = TC / CH;                      // chunks per TC-column row
+    constexpr int ROWB = TC * sizeof(T) + 16;         // padded row bytes
+    constexpr int PER = STG * CPR / 256;              // chunks per thread per operand (2 / 4)
+    constexpr int D = TC == 64 ? 4 : 2;               // stages of global loads in flight per thread
+    constexpr int WT = TC / 2, FT = WT / 16;          // per-wave tile (2 x 2 waves), its 16x16 fragments
     __shared__ __attribute__((aligned(16))) char Ps[2][STG * ROWB];
     __shared__ __attribute__((aligned(16))) char Qs[2][STG * ROWB];
-    __shared__ float dbs[64];
+    __shared__ float dbs[TC];
     extern __shared__ double dsm[];   // tmp [2*cs] fp64 | bnp scale [cs] | shift [cs]
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1218,7 +1219,7 @@ __device__ __forceinline__ void wgrad_tile(const WgView& a, int co0, int k0, lon
     const bool pro = a.pro_bn_relu != 0;
 
     float* bnp = (float*)(dsm + 2 * cs);
-    if (tid < 64) dbs[tid] = 0.f;
+    if (tid < TC) dbs[tid] = 0.f;
     const int sc_ = tid % CPR;
     const int pk = k0 + sc_ * CH;                // Q column
     const int ptap = pk / cs, pci = pk - ptap * cs;
@@ -1229,11 +1230,11 @@ __device__ __forceinline__ void wgrad_tile(const WgView& a, int co0, int k0, lon
     const int nst = mb < me ? (int)((me - mb + STG - 1) / STG) : 0;
     const int mfirst = nst > 0 ? (int)mb : 0;
 
-    floatx4 acc[2][2];
+    floatx4 acc[FT][FT];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < FT; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < FT; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
     // D-deep ring of register stages.  Loads are unconditional (clamped
     // addresses) so none of them sits under a branch (which would make the
@@ -1289,7 +1290,7 @@ __device__ __forceinline__ void wgrad_tile(const WgView& a, int co0, int k0, lon
     if (nst > 0) lstore(0, 0);
     __syncthreads();
     const int g = lane >> 4, li = lane & 15;
-    float bpart = 0.f;   // bias partial: column tid & 63, rows (tid >> 6) * STG/4 .. of every stage
+    float bpart = 0.f;   // bias partial: column tid % TC, rows (tid / TC) * STG*TC/256 .. of every stage
     for (int it0 = 0; it0 < nst; it0 += D) {
 #pragma unroll
         for (int u = 0; u < D; ++u) {
@@ -1299,18 +1300,19 @@ __device__ __forceinline__ void wgrad_tile(const WgView& a, int co0, int k0, lon
             // ring slot u (stage it) is in LDS already: refill it with stage it + D
             gload(u, mb + (long long)(it + D) * STG);
             if (do_bias) {
-                const int c = tid & 63, r0 = (tid >> 6) * (STG / 4);
+                constexpr int RB = STG * TC / 256;
+                const int c = tid % TC, r0 = (tid / TC) * RB;
 #pragma unroll
-                for (int r = 0; r < STG / 4; ++r) bpart += ldv((const T*)(Ps[cur] + (r0 + r) * ROWB) + c);
+                for (int r = 0; r < RB; ++r) bpart += ldv((const T*)(Ps[cur] + (r0 + r) * ROWB) + c);
             }
             if constexpr (sizeof(T) == 2) {
                 const int q = li >> 2, p = li & 3;
 #pragma unroll
                 for (int s = 0; s < 2; ++s) {
-                    u32x4 af[2], bfr[2];
+                    u32x4 af[FT], bfr[FT];
 #pragma unroll
-                    for (int i = 0; i < 2; ++i) {
-                        const int c0 = wc * 32 + i * 16 + 4 * p;
+                    for (int i = 0; i < FT; ++i) {
+                        const int c0 = wc * WT + i * 16 + 4 * p;
                         const char* base = Ps[cur] + (32 * s + 8 * g + q) * ROWB + c0 * 2;
                         i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)base);
                         i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)(base + 4 * ROWB));
@@ -1320,8 +1322,8 @@ __device__ __forceinline__ void wgrad_tile(const WgView& a, int co0, int k0, lon
                         af[i].w = (uint32_t)(uint16_t)hi.z | ((uint32_t)(uint16_t)hi.w << 16);
                     }
 #pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        const int c0 = wk * 32 + j * 16 + 4 * p;
+                    for (int j = 0; j < FT; ++j) {
+                        const int c0 = wk * WT + j * 16 + 4 * p;
                         const char* base = Qs[cur] + (32 * s + 8 * g + q) * ROWB + c0 * 2;
                         i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)base);
                         i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)(base + 4 * ROWB));
@@ -1331,34 +1333,34 @@ __device__ __forceinline__ void wgrad_tile(const WgView& a, int co0, int k0, lon
                         bfr[j].w = (uint32_t)(uint16_t)hi.z | ((uint32_t)(uint16_t)hi.w << 16);
                     }
 #pragma unroll
-                    for (int i = 0; i < 2; ++i)
+                    for (int i = 0; i < FT; ++i)
 #pragma unroll
-                        for (int j = 0; j < 2; ++j) Mf<bf16_t>::step(af[i], bfr[j], acc[i][j]);
+                        for (int j = 0; j < FT; ++j) Mf<bf16_t>::step(af[i], bfr[j], acc[i][j]);
                 }
             } else {
 #pragma unroll
                 for (int s = 0; s < 2; ++s) {
-                    u32x4 af[2], bfr[2];
+                    u32x4 af[FT], bfr[FT];
 #pragma unroll
-                    for (int i = 0; i < 2; ++i) {
-                        const char* pcol = Ps[cur] + (16 * s + 4 * g) * ROWB + (wc * 32 + i * 16 + li) * 4;
+                    for (int i = 0; i < FT; ++i) {
+                        const char* pcol = Ps[cur] + (16 * s + 4 * g) * ROWB + (wc * WT + i * 16 + li) * 4;
                         af[i].x = *(const uint32_t*)(pcol);
                         af[i].y = *(const uint32_t*)(pcol + ROWB);
                         af[i].z = *(const uint32_t*)(pcol + 2 * ROWB);
                         af[i].w = *(const uint32_t*)(pcol + 3 * ROWB);
                     }
 #pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        const char* qcol = Qs[cur] + (16 * s + 4 * g) * ROWB + (wk * 32 + j * 16 + li) * 4;
+                    for (int j = 0; j < FT; ++j) {
+                        const char* qcol = Qs[cur] + (16 * s + 4 * g) * ROWB + (wk * WT + j * 16 + li) * 4;
                         bfr[j].x = *(const uint32_t*)(qcol);
                         bfr[j].y = *(const uint32_t*)(qcol + ROWB);
                         bfr[j].z = *(const uint32_t*)(qcol + 2 * ROWB);
                         bfr[j].w = *(const uint32_t*)(qcol + 3 * ROWB);
                     }
 #pragma unroll
-                    for (int i = 0; i < 2; ++i)
+                    for (int i = 0; i < FT; ++i)
 #pragma unroll
-                        for (int j = 0; j < 2; ++j) Mf<float>::step(af[i], bfr[j], acc[i][j]);
+                        for (int j = 0; j < FT; ++j) Mf<float>::step(af[i], bfr[j], acc[i][j]);
                 }
             }
             if (it + 1 < nst) lstore((u + 1) % D, cur ^ 1);
@@ -1367,22 +1369,22 @@ __device__ __forceinline__ void wgrad_tile(const WgView& a, int co0, int k0, lon
     }
     // D rows = co, cols = k
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < FT; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < FT; ++j)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int co = co0 + wc * 32 + i * 16 + (lane >> 4) * 4 + r;
-                const int k = k0 + wk * 32 + j * 16 + (lane & 15);
+                const int co = co0 + wc * WT + i * 16 + (lane >> 4) * 4 + r;
+                const int k = k0 + wk * WT + j * 16 + (lane & 15);
                 if (co < N && k < K) {
                     float* o = out + (long long)co * a.kp + k;
                     if (atomic) atomicAdd(o, acc[i][j][r]);
                     else *o = acc[i][j][r];
                 }
             }
-    if (do_bias) atomicAdd(&dbs[tid & 63], bpart);
+    if (do_bias) atomicAdd(&dbs[tid % TC], bpart);
     __syncthreads();
-    if (do_bias && tid < 64 && co0 + tid < N) {
+    if (do_bias && tid < TC && co0 + tid < N) {
         if (bias_atomic) atomicAdd(&bias_out[co0 + tid], dbs[tid]);
         else bias_out[co0 + tid] = dbs[tid];
     }
@@ -1391,7 +1393,7 @@ __device__ __forceinline__ void wgrad_tile(const WgView& a, int co0, int k0, lon
 // grouped: block -> (conv, slab z, co tile, k tile).  Consecutive tasks (the
 // tiles of one slab, which re-read the same pixels through L2) are placed on
 // one XCD: dispatch hands block b to XCD b % 8, so task = bijective remap.
-template <typename T>
+template <typename T, int TC>
 __global__ __launch_bounds__(256) void k_wgrad_grouped(rnvp_wgrad_group g) {
     const int nb = gridDim.x, b = blockIdx.x;
     const int q = nb / 8, r = nb % 8, xcd = b % 8;
@@ -1399,7 +1401,7 @@ __global__ __launch_bounds__(256) void k_wgrad_grouped(rnvp_wgrad_group g) {
     int c = 0;
     while (c + 1 < g.n_conv && g.conv[c + 1].task0 <= t) ++c;
     const rnvp_wgrad_conv& cv = g.conv[c];
-    const int tco = (cv.n + 63) / 64;
+    const int tco = (cv.n + TC - 1) / TC;
     const int local = t - cv.task0;
     const int per = tco * cv.tk;
     const int z = local / per, rr = local - z * per;
@@ -1410,7 +1412,7 @@ __global__ __launch_bounds__(256) void k_wgrad_grouped(rnvp_wgrad_group g) {
     const WgView v{cv.x, cv.dy, cv.pro, g.H, g.W, cv.ks, cv.cs_in, cv.cin, cv.cs_dy, cv.n, cv.kp, cv.pro_bn_relu};
     const int rep = z % cv.nrep;
     const bool atomic = cv.nrep < cv.nz;
-    wgrad_tile<T>(v, cot * 64, kt * 64, mb, me, M, cv.ws + (long long)rep * cv.n * cv.kp, atomic,
+    wgrad_tile<T, TC>(v, cot * TC, kt * TC, mb, me, M, cv.ws + (long long)rep * cv.n * cv.kp, atomic,
                   (cv.wsb && kt == 0) ? cv.wsb + (long long)rep * cv.n : nullptr, atomic);
 }
 
@@ -1715,6 +1717,9 @@ extern "C" int rnvp_conv2d_wgrad_grouped(const rnvp_wgrad_group* gin, void* stre
     const long long M = (long long)g.B * g.H * g.W;
     const int STG = g.dtype == RNVP_BF16 ? 64 : 32;
     if (M >= (1ll << 31) || M / g.W >= (1ll << 22)) return RNVP_E_UNSUPPORTED;
+    // 64 x 64 output tiles (128 x 128 halves the operand re-reads but was
+    // measured slower at every scale of config 1: 5.0 vs 4.3 ms per step)
+    const int TC = 64;
     long long tasks = 0;
     int max_cs = 8;
     for (int c = 0; c < g.n_conv; ++c) {
@@ -1728,16 +1733,21 @@ extern "C" int rnvp_conv2d_wgrad_grouped(const rnvp_wgrad_group* gin, void* stre
         const long long steps = (M + STG - 1) / STG;
         v.m_per_slab = ((steps + v.nz - 1) / v.nz) * STG;
         if ((M + v.m_per_slab - 1) / v.m_per_slab > v.nz) return RNVP_E_INVALID;
-        v.tk = (v.ks * v.ks * v.cs_in + 63) / 64;
+        v.tk = (v.ks * v.ks * v.cs_in + TC - 1) / TC;
         v.task0 = (int)tasks;
-        tasks += (long long)v.nz * ((v.n + 63) / 64) * v.tk;
+        tasks += (long long)v.nz * ((v.n + TC - 1) / TC) * v.tk;
         if (v.cs_in > max_cs) max_cs = v.cs_in;
     }
     if (tasks <= 0 || tasks > (1ll << 30)) return RNVP_E_INVALID;
     hipStream_t s = (hipStream_t)stream;
     const size_t shm = 24 * (size_t)max_cs;
-    if (g.dtype == RNVP_F32) k_wgrad_grouped<float><<<(unsigned)tasks, 256, shm, s>>>(g);
-    else k_wgrad_grouped<bf16_t><<<(unsigned)tasks, 256, shm, s>>>(g);
+    if (g.dtype == RNVP_F32) {
+        if (TC == 128) k_wgrad_grouped<float, 128><<<(unsigned)tasks, 256, shm, s>>>(g);
+        else k_wgrad_grouped<float, 64><<<(unsigned)tasks, 256, shm, s>>>(g);
+    } else {
+        if (TC == 128) k_wgrad_grouped<bf16_t, 128><<<(unsigned)tasks, 256, shm, s>>>(g);
+        else k_wgrad_grouped<bf16_t, 64><<<(unsigned)tasks, 256, shm, s>>>(g);
+    }
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
 }

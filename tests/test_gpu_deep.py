@@ -366,6 +366,10 @@ WGRAD_CASES = [
     ("deep_1024", 16, 2, 2, 1024, 1024, 3, True),
     ("m_2pow22", 256, 128, 128, 8, 8, 3, False),      # config 4 scale 1: M = 2^22
     ("m_above_2pow22", 257, 128, 128, 8, 16, 1, True),
+    # 128 x 128 tiles (nets with mid >= 128)
+    ("s4_256_3x3", 16, 8, 8, 256, 256, 3, True),
+    ("s5_512_1x1", 64, 4, 4, 512, 512, 1, False),
+    ("ragged_128", 4, 16, 16, 136, 200, 3, True),
 ]
 
 
