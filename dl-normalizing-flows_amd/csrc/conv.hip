@@ -1613,7 +1613,15 @@ __global__ __launch_bounds__(256) void k_wn_pack(const rnvp_wn_desc* __restrict_
 // into LDS in v's [ci][tap] order (coalesced over the packed k), then the
 // weight-norm backward and the bias partial sum.
 
-__global__ void k_wn_bwd(const rnvp_wn_desc* __restrict__ descs, int n_desc, float* gbase) {
+__global__ void k_wn_bwd(const rnvp_wn_desc* __restrict__ descs, int n_desc, float* gbase, int rows, double* z0,
+                         long long n0, double* z1, long long n1) {
+    if ((int)blockIdx.x >= rows) {   // extra workgroups: zero the caller's sums ranges
+        const long long stride = (long long)(gridDim.x - rows) * blockDim.x;
+        const long long i0 = (long long)(blockIdx.x - rows) * blockDim.x + threadIdx.x;
+        for (long long i = i0; i < n0; i += stride) z0[i] = 0.0;
+        for (long long i = i0; i < n1; i += stride) z1[i] = 0.0;
+        return;
+    }
     __shared__ double red[16];
     __shared__ float rowbuf[WN_ROW_LDS];
     const int row = blockIdx.x;
@@ -1786,9 +1794,16 @@ extern "C" int rnvp_weight_norm_fwd(const rnvp_wn_desc* d, int n_desc, int total
     return RNVP_OK;
 }
 
-extern "C" int rnvp_weight_norm_bwd(const rnvp_wn_desc* d, int n_desc, int total_rows, float* grad_base, void* stream) {
+extern "C" int rnvp_weight_norm_bwd(const rnvp_wn_desc* d, int n_desc, int total_rows, float* grad_base, void* zero0,
+                                    long long zero0_bytes, void* zero1, long long zero1_bytes, void* stream) {
     if (!d || !grad_base || n_desc <= 0 || total_rows <= 0) return RNVP_E_INVALID;
-    k_wn_bwd<<<total_rows, 256, 0, (hipStream_t)stream>>>(d, n_desc, grad_base);
+    if (zero0_bytes < 0 || zero1_bytes < 0 || (zero0_bytes & 7) || (zero1_bytes & 7)) return RNVP_E_INVALID;
+    if ((zero0_bytes && (!zero0 || ((uintptr_t)zero0 & 7))) || (zero1_bytes && (!zero1 || ((uintptr_t)zero1 & 7))))
+        return RNVP_E_INVALID;
+    const long long nz = (zero0_bytes > zero1_bytes ? zero0_bytes : zero1_bytes) / 8;
+    const int extra = nz > 0 ? (int)((nz + 255) / 256 < 16 ? (nz + 255) / 256 : 16) : 0;
+    k_wn_bwd<<<total_rows + extra, 256, 0, (hipStream_t)stream>>>(d, n_desc, grad_base, total_rows, (double*)zero0,
+                                                                  zero0_bytes / 8, (double*)zero1, zero1_bytes / 8);
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
 }

@@ -264,8 +264,26 @@ __global__ __launch_bounds__(256) void k_out1(rnvp_coupling_args a, int TP, int 
 
 // z = out_bn(u) on transformed positions; ldj var term; running stats.
 template <typename T>
-__global__ void k_out2(rnvp_coupling_args a) {
+__global__ void k_out2(rnvp_coupling_args a, int main_grid) {
     extern __shared__ float sh[];   // mean[Cb], rstd[Cb], half_log_var[Cb]
+    if ((int)blockIdx.x >= main_grid) {
+        // extra workgroups: one s/t-net BatchNorm running-stat update each
+        // (the net's batch sums are complete: every conv ran before this launch)
+        const rnvp_bn_running r = a.net_running[blockIdx.x - main_grid];
+        double* tmp = (double*)sh;   // [2*C]
+        block_shard_sums(r.sums, r.C, r.shards, 0, r.C, tmp, tmp + r.C);
+        const float mom = a.momentum;
+        for (int c = threadIdx.x; c < r.C; c += blockDim.x) {
+            double mean = tmp[c] / r.count;
+            double var = tmp[r.C + c] / r.count - mean * mean;
+            if (var < 0) var = 0;
+            double unb = r.count > 1 ? var * r.count / (r.count - 1) : var;
+            r.rmean[c] = (1.f - mom) * r.rmean[c] + mom * (float)mean;
+            r.rvar[c] = (1.f - mom) * r.rvar[c] + mom * (float)unb;
+        }
+        if (threadIdx.x == 0 && r.nbt) r.nbt[0] += 1;
+        return;
+    }
     const Geo g = geo(a);
     const double cnt = (double)g.B * g.HW;
     for (int cb = threadIdx.x; cb < g.Cb; cb += blockDim.x) {
@@ -303,7 +321,7 @@ __global__ void k_out2(rnvp_coupling_args a) {
     const T* st = cptr<T>(a.st);
     const float sc = a.scale[0], ss = a.scale_shift[0];
     const long long n = (long long)g.B * g.C * g.HW;
-    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)main_grid * blockDim.x) {
         const int p = (int)(e % g.HW);
         const long long t = e / g.HW;
         const int c = (int)(t % g.C);
@@ -671,8 +689,12 @@ extern "C" int rnvp_coupling_out_fwd(const rnvp_coupling_args* a, void* stream) 
     RNVP_LAUNCH_CHECK();
     long long n = (long long)a->B * a->C * a->H * a->W;
     size_t shm = 3 * Cb * sizeof(float);
-    if (a->dtype == RNVP_F32) k_out2<float><<<rnvp_grid(n, 256, 2048), 256, shm, s>>>(*a);
-    else k_out2<bf16_t><<<rnvp_grid(n, 256, 2048), 256, shm, s>>>(*a);
+    const int nrun = (a->training && a->net_running) ? a->n_net_running : 0;
+    if (nrun < 0 || (nrun > 0 && a->net_running_cmax <= 0)) return RNVP_E_INVALID;
+    if (nrun > 0 && 16 * (size_t)a->net_running_cmax > shm) shm = 16 * (size_t)a->net_running_cmax;
+    const int g2 = rnvp_grid(n, 256, 2048);
+    if (a->dtype == RNVP_F32) k_out2<float><<<g2 + nrun, 256, shm, s>>>(*a, g2);
+    else k_out2<bf16_t><<<g2 + nrun, 256, shm, s>>>(*a, g2);
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
 }

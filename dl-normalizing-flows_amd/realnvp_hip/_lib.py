@@ -87,7 +87,8 @@ class CouplingArgs(C.Structure):
                 ("gst", vp), ("cs_gst", i32),
                 ("bwd_sums", vp), ("g_scale", vp), ("g_scale_shift", vp),
                 ("gh0", vp), ("cs_gh0", i32),
-                ("in_bwd_sums", vp), ("g_in_gamma", vp), ("g_in_beta", vp)]
+                ("in_bwd_sums", vp), ("g_in_gamma", vp), ("g_in_beta", vp),
+                ("net_running", vp), ("n_net_running", i32), ("net_running_cmax", i32)]
 
 
 class TensorRef(C.Structure):
@@ -116,7 +117,7 @@ _SIGS = {
     "rnvp_bn_bwd_apply": (i32, [C.POINTER(BNBwdArgs), vp]),
     "rnvp_weight_norm_fwd": (i32, [vp, i32, i32, i32, i32, vp]),
     "rnvp_weight_norm_tiles": (i32, [i32, i32]),
-    "rnvp_weight_norm_bwd": (i32, [vp, i32, i32, vp, vp]),
+    "rnvp_weight_norm_bwd": (i32, [vp, i32, i32, vp, vp, i64, vp, i64, vp]),
     "rnvp_coupling_in_fwd": (i32, [C.POINTER(CouplingArgs), vp]),
     "rnvp_coupling_out_fwd": (i32, [C.POINTER(CouplingArgs), vp]),
     "rnvp_coupling_reverse": (i32, [C.POINTER(CouplingArgs), vp]),

@@ -237,7 +237,7 @@ class CouplingEngine:
         sh = stat_shards(M)
         for bn, spec in self.P.bns.items():
             ar.add("s:" + bn, sh * 2 * spec.c * 8)
-        ar.alloc(device)
+        ar.alloc(device, zero=True)   # the sums start zero (persistent arenas keep them zero between steps)
         sv = dict(arena=ar, B=B, H=H, W=W, dtype=dtype, training=training, shards=sh)
         # running-stat update table for the net BNs
         if training and self.P.bns:
@@ -275,7 +275,7 @@ class CouplingEngine:
             ar.add("g:" + b, M * chan_stride(ch) * esz)
         cmax = max([chan_stride(s.cin) for s in self.P.convs.values()])
         ar.add("gtmp", M * cmax * esz)
-        ar.alloc(device)
+        ar.alloc(device, zero=True)
         # grouped weight-gradient partial sums: [nrep][cout][kp_f] (+ bias [nrep][cout])
         nz = int(_lib.lib().wgrad_slabs(M))
         nrep = int(_lib.lib().wgrad_replicas(nz))
@@ -373,10 +373,13 @@ class CouplingEngine:
             _launch("conv_fwd", nb, 2.0 * M * spec.cout * spec.ks * spec.ks * spec.cin, L.conv2d, C.byref(a), s)
 
     # ---------------------------------------------------------------- forward
-    def forward(self, x, training, dtype, full_ldj, saved=None, prepare=True, ldj_sample=None, z_out=None):
+    def forward(self, x, training, dtype, full_ldj, saved=None, prepare=True, ldj_sample=None, z_out=None,
+                zero_sums=True):
         """x: [B,C,H,W] fp32 device tensor.  Returns (z, ldj, saved) where ldj
         is the elementwise log_diag_J [B,C,H,W] (full_ldj) or this coupling's
-        per-sample sum [B] (accumulated into ldj_sample when given)."""
+        per-sample sum [B] (accumulated into ldj_sample when given).
+        zero_sums=False: the batch-statistic sums of `saved` are already zero
+        (the previous step's backward left them so: backward(zero_at_end=True))."""
         L = _lib.lib()
         B, Cc, H, W = x.shape
         assert Cc == self.C, "channel mismatch"
@@ -390,7 +393,7 @@ class CouplingEngine:
         if ldj_sample is None:
             ldj_sample = torch.zeros(B, device=dev, dtype=torch.float32)
         ldj_full = torch.empty_like(x) if full_ldj else None
-        if training:
+        if training and zero_sums:
             s0, e0 = ar.range_bytes("in_sums", list(ar.slots)[-1])
             ar.buf[s0:e0].zero_()
         a = self._coupling_args(T, x, B, H, W, dtype, training)
@@ -399,7 +402,9 @@ class CouplingEngine:
         L.coupling_in_fwd(C.byref(a), s)
         self._net_forward(T, sv, ws, training, s)
         if training and "bn_table" in sv:
-            L.bn_running_update(sv["bn_table"].data_ptr(), sv["bn_n"], sv["bn_cmax"], BN_MOMENTUM, s)
+            # the net BNs' running-stat updates ride on the out launch
+            a.net_running, a.n_net_running, a.net_running_cmax = (sv["bn_table"].data_ptr(), sv["bn_n"],
+                                                                  sv["bn_cmax"])
         a.st = ar.ptr("st")
         a.u, a.z = ar.ptr("u"), z.data_ptr()
         a.out_sums = ar.ptr("out_sums")
@@ -441,7 +446,7 @@ class CouplingEngine:
         return out, ldj
 
     # --------------------------------------------------------------- backward
-    def backward(self, sv, gz, gl_full, gl_sample, grad_block, gx=None, side=None, after=None):
+    def backward(self, sv, gz, gl_full, gl_sample, grad_block, gx=None, side=None, after=None, zero_at_end=False):
         """Returns dL/dx; parameter gradients are written into grad_block
         (flat fp32, zeroed by the caller; scale/shift grads accumulate).
 
@@ -449,7 +454,11 @@ class CouplingEngine:
         weight gradients of all the net's convs only need their (complete,
         never rewritten) output gradients and saved inputs, so they run as
         ONE grouped launch afterwards (partial slabs, no atomics), followed by
-        the weight-norm backward that sums the slabs."""
+        the weight-norm backward that sums the slabs.
+
+        zero_at_end: the backward sums are zero on entry (not re-zeroed here)
+        and the weight-norm backward launch leaves both these and the
+        forward's batch sums zero for the next step (persistent arenas)."""
         L = _lib.lib()
         x = sv["x"]
         B, H, W, dtype, training = sv["B"], sv["H"], sv["W"], sv["dtype"], sv["training"]
@@ -464,7 +473,8 @@ class CouplingEngine:
             sc = self.scratch(B, H, W, dtype, x.device)
         ar, sar, war = sv["arena"], sc["arena"], ws["arena"]
         z0, z1 = sc["zero"]
-        sar.buf[z0:z1].zero_()
+        if not zero_at_end:
+            sar.buf[z0:z1].zero_()
         gbase = grad_block.data_ptr()
 
         def gp(name):
@@ -568,7 +578,12 @@ class CouplingEngine:
             for grp in groups:
                 _launch("conv_wgrad", wg_bytes / len(groups), wg_flops / len(groups), L.conv2d_wgrad_grouped,
                         C.byref(grp), ss)
-            L.weight_norm_bwd(sc["wn_table"].data_ptr(), sc["n_wn"], sc["wn_rows"], gbase, ss)
+            if zero_at_end:
+                f0, f1 = ar.range_bytes("in_sums", list(ar.slots)[-1])
+                zr = (ar.base + f0, f1 - f0, sar.base + z0, z1 - z0)
+            else:
+                zr = (None, 0, None, 0)
+            L.weight_norm_bwd(sc["wn_table"].data_ptr(), sc["n_wn"], sc["wn_rows"], gbase, *zr, ss)
             if after is not None:
                 after()
 

@@ -304,7 +304,8 @@ class FlowTrainer:
                     torch.cuda.current_stream().wait_event(late_ready)
                 ci += 1
                 _, mod, eng, x, z, sv, _ = st
-                eng.forward(x, True, self.dtype, False, saved=sv, prepare=False, ldj_sample=self.ldj, z_out=z)
+                eng.forward(x, True, self.dtype, False, saved=sv, prepare=False, ldj_sample=self.ldj, z_out=z,
+                            zero_sums=False)
             elif st[0] == "squeeze":
                 _, a, b = st
                 L.squeeze(a.data_ptr(), b.data_ptr(), *a.shape, s)
@@ -336,7 +337,8 @@ class FlowTrainer:
                 if self.adam_ranges is not None:
                     lo, hi = self.adam_ranges[ci]
                     after = (lambda lo=lo, hi=hi: self._adam_range(lo, hi))
-                eng.backward(sv, self._g(z), None, self.g_lp, block, gx=self._g(x), side=self.side, after=after)
+                eng.backward(sv, self._g(z), None, self.g_lp, block, gx=self._g(x), side=self.side, after=after,
+                             zero_at_end=True)
                 if self.comm_stream is not None:
                     for lo, hi in self.bucket_after.get(n_coupling - 1 - ci, ()):
                         # the bucket's weight gradients were written on the side

@@ -204,7 +204,11 @@ typedef struct rnvp_wn_desc {
 int rnvp_weight_norm_tiles(int cout, int cin);
 int rnvp_weight_norm_fwd(const rnvp_wn_desc* descs_device, int n_desc, int total_rows, int total_tiles, int dtype,
                          void* stream);
-int rnvp_weight_norm_bwd(const rnvp_wn_desc* descs_device, int n_desc, int total_rows, float* grad_base, void* stream);
+/* zero0 / zero1: byte ranges (8-byte multiples, 8-byte aligned, may be
+ * NULL / 0) zeroed by the same launch -- the caller's batch-statistic sums,
+ * left zero for the next step once the coupling's backward has consumed them */
+int rnvp_weight_norm_bwd(const rnvp_wn_desc* descs_device, int n_desc, int total_rows, float* grad_base,
+                         void* zero0, long long zero0_bytes, void* zero1, long long zero1_bytes, void* stream);
 
 /* ---- affine coupling (modules_realnvp.py:239-370) -----------------------
  * kind 0 = CheckerboardAffineCoupling, 1 = ChannelwiseAffineCoupling.
@@ -242,6 +246,11 @@ typedef struct rnvp_coupling_args {
     const void* gh0; int cs_gh0;
     double* in_bwd_sums;                  /* [RNVP_COUPLING_SHARDS][2*Cb] */
     float* g_in_gamma; float* g_in_beta;  /* written */
+    /* optional, forward (rnvp_coupling_out_fwd): running-stat updates of the
+     * s/t net's BatchNorms (what rnvp_bn_running_update does), folded into
+     * the out launch; net_running is a device table of n_net_running sites
+     * with at most net_running_cmax channels */
+    const rnvp_bn_running* net_running; int n_net_running; int net_running_cmax;
 } rnvp_coupling_args;
 int rnvp_coupling_in_fwd(const rnvp_coupling_args* a, void* stream);   /* in_sums must be zeroed */
 int rnvp_coupling_out_fwd(const rnvp_coupling_args* a, void* stream);  /* out_sums must be zeroed */
