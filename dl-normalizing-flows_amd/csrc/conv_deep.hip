@@ -368,7 +368,7 @@ inline void xcd_blocks(const rnvp_conv_args* a, int gm, int gn, int bn, int esz,
     }
 }
 
-template <typename T, int BN, int NW, int WK, int DK, int NC>
+template <typename T, int BN, int NW, int WK, int DK, int NC, int KSZ>
 int launch_deep_nc(const rnvp_conv_args* a, hipStream_t s) {
     const long long M = (long long)a->B * a->H * a->W;
     const size_t shm = deep_lds_bytes<T, BN, NW, WK>(a->cs_in, a->W, a->ks);
@@ -379,13 +379,8 @@ int launch_deep_nc(const rnvp_conv_args* a, hipStream_t s) {
     const dim3 blk(64 * NW);
     int xa, xb;
     xcd_blocks(a, (int)gm, (int)gn, BN, sizeof(T), &xa, &xb);
-    if (a->ks == 3) {
-        if (a->pro_bn_relu) k_conv_deep<T, BN, 3, true, NW, WK, DK, NC><<<grid, blk, shm, s>>>(*a, sh, xa, xb);
-        else k_conv_deep<T, BN, 3, false, NW, WK, DK, NC><<<grid, blk, shm, s>>>(*a, sh, xa, xb);
-    } else {
-        if (a->pro_bn_relu) k_conv_deep<T, BN, 1, true, NW, WK, DK, NC><<<grid, blk, shm, s>>>(*a, sh, xa, xb);
-        else k_conv_deep<T, BN, 1, false, NW, WK, DK, NC><<<grid, blk, shm, s>>>(*a, sh, xa, xb);
-    }
+    if (a->pro_bn_relu) k_conv_deep<T, BN, KSZ, true, NW, WK, DK, NC><<<grid, blk, shm, s>>>(*a, sh, xa, xb);
+    else k_conv_deep<T, BN, KSZ, false, NW, WK, DK, NC><<<grid, blk, shm, s>>>(*a, sh, xa, xb);
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
 }
@@ -401,14 +396,23 @@ int launch_deep(const rnvp_conv_args* a, hipStream_t s) {
     if (a->epi_relu_bn_bwd && a->epi.sums && a->epi.shards > 2) return RNVP_E_UNSUPPORTED;
     if (a->cs_in > DEEP_MAX_CS) return RNVP_E_UNSUPPORTED;
     const int nc = a->cs_in / (WK * KS);
-    switch (nc) {
-        case 1: return launch_deep_nc<T, BN, NW, WK, DK, 1>(a, s);
-        case 2: return launch_deep_nc<T, BN, NW, WK, DK, 2>(a, s);
-        case 4: return launch_deep_nc<T, BN, NW, WK, DK, 4>(a, s);
-        case 8: return launch_deep_nc<T, BN, NW, WK, DK, 8>(a, s);
-        case 16:
-            if (a->ks == 1) return launch_deep_nc<T, BN, NW, WK, DK, 16>(a, s);
-            return RNVP_E_UNSUPPORTED;
+    if (a->ks == 1) {
+        switch (nc) {
+            case 1: return launch_deep_nc<T, BN, NW, WK, DK, 1, 1>(a, s);
+            case 2: return launch_deep_nc<T, BN, NW, WK, DK, 2, 1>(a, s);
+            case 4: return launch_deep_nc<T, BN, NW, WK, DK, 4, 1>(a, s);
+            case 8: return launch_deep_nc<T, BN, NW, WK, DK, 8, 1>(a, s);
+            case 16: return launch_deep_nc<T, BN, NW, WK, DK, 16, 1>(a, s);
+        }
+        return RNVP_E_UNSUPPORTED;
+    }
+    if constexpr (WK == 4) {   // 3x3: whole-tile-per-wave configurations only
+        switch (nc) {
+            case 1: return launch_deep_nc<T, BN, NW, WK, DK, 1, 3>(a, s);
+            case 2: return launch_deep_nc<T, BN, NW, WK, DK, 2, 3>(a, s);
+            case 4: return launch_deep_nc<T, BN, NW, WK, DK, 4, 3>(a, s);
+            case 8: return launch_deep_nc<T, BN, NW, WK, DK, 8, 3>(a, s);
+        }
     }
     return RNVP_E_UNSUPPORTED;
 }
