@@ -522,8 +522,14 @@ __global__ __launch_bounds__(256) void k_out_bwd_apply(rnvp_coupling_args a, int
     const float dss = (float)block_sum(gss, redl);
     tile_copy_out<T>(gs, t.m0, t.tp, a.cs_gst, a.gst);
     if (threadIdx.x == 0 && (dsc != 0.f || dss != 0.f)) {
-        atomicAdd(a.g_scale, dsc);
-        atomicAdd(a.g_scale_shift, dss);
+        if (a.gscale_part) {   // sharded: bounded same-address atomic depth
+            double* sp = a.gscale_part + 2 * (blockIdx.x % RNVP_COUPLING_SHARDS);
+            atomicAdd(sp, (double)dsc);
+            atomicAdd(sp + 1, (double)dss);
+        } else {
+            atomicAdd(a.g_scale, dsc);
+            atomicAdd(a.g_scale_shift, dss);
+        }
     }
 }
 
@@ -596,6 +602,23 @@ __global__ __launch_bounds__(256) void k_in_bwd_apply(rnvp_coupling_args a, int 
         if (blockIdx.x == 0) {   // the affine grads, once
             if (a.g_in_beta) a.g_in_beta[cb] = (float)s1;
             if (a.g_in_gamma) a.g_in_gamma[cb] = (float)s2;
+        }
+    }
+    if (blockIdx.x == 0 && a.gscale_part && threadIdx.x < 64) {
+        // fold the out part's sharded scale / scale_shift partials (wave 0)
+        const int l = threadIdx.x;
+        double v0 = 0.0, v1 = 0.0;
+        if (l < RNVP_COUPLING_SHARDS) {
+            v0 = a.gscale_part[2 * l];
+            v1 = a.gscale_part[2 * l + 1];
+            a.gscale_part[2 * l] = 0.0;
+            a.gscale_part[2 * l + 1] = 0.0;
+        }
+        v0 = wave_sum(v0);
+        v1 = wave_sum(v1);
+        if (l == 0) {
+            *a.g_scale += (float)v0;
+            *a.g_scale_shift += (float)v1;
         }
     }
     tile_copy_in<T>(a.gh0, t.m0, t.tp, a.cs_gh0, gh);

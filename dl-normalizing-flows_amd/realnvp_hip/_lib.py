@@ -88,7 +88,8 @@ class CouplingArgs(C.Structure):
                 ("bwd_sums", vp), ("g_scale", vp), ("g_scale_shift", vp),
                 ("gh0", vp), ("cs_gh0", i32),
                 ("in_bwd_sums", vp), ("g_in_gamma", vp), ("g_in_beta", vp),
-                ("net_running", vp), ("n_net_running", i32), ("net_running_cmax", i32)]
+                ("net_running", vp), ("n_net_running", i32), ("net_running_cmax", i32),
+                ("gscale_part", vp)]
 
 
 class TensorRef(C.Structure):

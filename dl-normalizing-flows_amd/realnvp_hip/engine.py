@@ -265,6 +265,7 @@ class CouplingEngine:
         wsz = self.weights(dtype)
         ar.add("bwd_sums", COUPLING_SHARDS * 3 * self.Cb * 8)
         ar.add("in_bwd_sums", COUPLING_SHARDS * 2 * self.Cb * 8)
+        ar.add("gscale_part", COUPLING_SHARDS * 2 * 8)   # left zero by coupling_in_bwd
         first, last = "bwd_sums", "in_bwd_sums"
         sh = stat_shards(M)
         for bn, spec in self.P.bns.items():
@@ -494,6 +495,7 @@ class CouplingEngine:
         a.gst, a.cs_gst = sar.ptr("g:st"), chan_stride(self.P.buf_ch["st"])
         a.bwd_sums = sar.ptr("bwd_sums")
         a.g_scale, a.g_scale_shift = gp("scale"), gp("scale_shift")
+        a.gscale_part = sar.ptr("gscale_part")
         L.coupling_out_bwd(C.byref(a), s)
 
         # grouped weight gradients: one launch per WGRAD_GROUP_MAX convs (the

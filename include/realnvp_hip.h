@@ -251,6 +251,12 @@ typedef struct rnvp_coupling_args {
      * the out launch; net_running is a device table of n_net_running sites
      * with at most net_running_cmax channels */
     const rnvp_bn_running* net_running; int n_net_running; int net_running_cmax;
+    /* optional: [RNVP_COUPLING_SHARDS][2] fp64 partials of the scale /
+     * scale_shift gradients -- zero on entry to rnvp_coupling_out_bwd, which
+     * adds into them (one shard per group of workgroups instead of every
+     * workgroup on one address); rnvp_coupling_in_bwd folds them into
+     * g_scale / g_scale_shift (+=) and leaves them zero */
+    double* gscale_part;
 } rnvp_coupling_args;
 int rnvp_coupling_in_fwd(const rnvp_coupling_args* a, void* stream);   /* in_sums must be zeroed */
 int rnvp_coupling_out_fwd(const rnvp_coupling_args* a, void* stream);  /* out_sums must be zeroed */
