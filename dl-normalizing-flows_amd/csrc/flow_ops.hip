@@ -213,6 +213,36 @@ extern "C" int rnvp_logit_inv(const float* x, float* y, float constraint, long l
 }
 
 // ---------------------------------------------------------------------------
+// transforms.ToTensor on the device (train.py:65-71): uint8 CHW images arrive
+// over PCIe at 1 B/pixel and become k / 255 in fp32 (correctly rounded
+// division, as torch's CPU uint8 -> float -> div(255)).  16 pixels per lane.
+// ---------------------------------------------------------------------------
+__global__ void k_u8_to_unit(const uint8_t* __restrict__ x, float* __restrict__ y, long long n) {
+    const long long n16 = n >> 4;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long q = blockIdx.x * (long long)blockDim.x + threadIdx.x; q < n16; q += stride) {
+        const uint4 v = *(const uint4*)(x + 16 * q);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        float4* o = (float4*)(y + 16 * q);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            o[j] = make_float4((float)(w[j] & 255u) / 255.f, (float)((w[j] >> 8) & 255u) / 255.f,
+                               (float)((w[j] >> 16) & 255u) / 255.f, (float)(w[j] >> 24) / 255.f);
+    }
+    for (long long e = 16 * n16 + blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += stride)
+        y[e] = (float)x[e] / 255.f;
+}
+
+extern "C" int rnvp_u8_to_unit(const uint8_t* x, float* y, long long n, void* stream) {
+    if (!x || !y || n < 0) return RNVP_E_INVALID;
+    if ((((uintptr_t)x) & 15) || (((uintptr_t)y) & 15)) return RNVP_E_INVALID;
+    if (n == 0) return RNVP_OK;
+    k_u8_to_unit<<<rnvp_grid((n + 15) / 16, 256), 256, 0, (hipStream_t)stream>>>(x, y, n);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+// ---------------------------------------------------------------------------
 // prior log-prob (flow_realnvp.py:329-340; train.py:109 prior = N(0,1))
 // ---------------------------------------------------------------------------
 __global__ void k_prior(const float* __restrict__ z, const float* __restrict__ ldj, float* __restrict__ out, int n) {

@@ -62,6 +62,11 @@ int rnvp_logit_fwd(const float* x, const float* noise, uint64_t seed, uint64_t o
                    float constraint, float* y, float* logdet, int B, int n_per_sample, void* stream);
 int rnvp_logit_inv(const float* x, float* y, float constraint, long long n, void* stream);
 
+/* ---- transforms.ToTensor of a uint8 batch (train.py:65-71) -------------
+ * y[i] = x[i] / 255.f (correctly rounded), x and y 16-byte aligned.  Lets the
+ * real-data pipeline ship 1 B/pixel over PCIe and convert on the device. */
+int rnvp_u8_to_unit(const uint8_t* x, float* y, long long n, void* stream);
+
 /* ---- prior log-prob and per-sample reduction (flow_realnvp.py:329-340) --
  * out[b] = ldj[b] + sum_i (-z_i^2/2 - log(2 pi)/2)       (N(0,1) prior)
  * bwd: gz_i = -z_i * gout[b] */
