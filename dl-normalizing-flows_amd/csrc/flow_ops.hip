@@ -234,9 +234,9 @@ __global__ void k_u8_to_unit(const uint8_t* __restrict__ x, float* __restrict__ 
 }
 
 extern "C" int rnvp_u8_to_unit(const uint8_t* x, float* y, long long n, void* stream) {
-    if (!x || !y || n < 0) return RNVP_E_INVALID;
-    if ((((uintptr_t)x) & 15) || (((uintptr_t)y) & 15)) return RNVP_E_INVALID;
-    if (n == 0) return RNVP_OK;
+    if (n < 0) return RNVP_E_INVALID;
+    if (n == 0) return RNVP_OK;   // empty tensors may carry null pointers
+    if (!x || !y || (((uintptr_t)x) & 15) || (((uintptr_t)y) & 15)) return RNVP_E_INVALID;
     k_u8_to_unit<<<rnvp_grid((n + 15) / 16, 256), 256, 0, (hipStream_t)stream>>>(x, y, n);
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
