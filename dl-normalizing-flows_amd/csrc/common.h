@@ -129,11 +129,24 @@ __device__ __forceinline__ void bn_affine(const rnvp_bn_src& s, int C, int c, fl
                                           float* mean_out = nullptr, float* rstd_out = nullptr) {
     double mean, var;
     if (s.sums) {
-        double s1 = 0, s2 = 0;
+        // shards <= 32 (rnvp_stat_shards, RNVP_COUPLING_SHARDS): every load is
+        // issued up front (clamped address, masked contribution), then added in
+        // shard order -- one memory round trip instead of one per shard
+        double v1[32], v2[32];
         const int ns = s.shards > 0 ? s.shards : 1;
-        for (int h = 0; h < ns; ++h) {
-            s1 += s.sums[(long long)h * 2 * C + c];
-            s2 += s.sums[(long long)h * 2 * C + C + c];
+#pragma unroll
+        for (int h = 0; h < 32; ++h) {
+            const long long o = (long long)(h < ns ? h : 0) * 2 * C;
+            v1[h] = s.sums[o + c];
+            v2[h] = s.sums[o + C + c];
+        }
+        double s1 = 0, s2 = 0;
+#pragma unroll
+        for (int h = 0; h < 32; ++h) {
+            if (h < ns) {
+                s1 += v1[h];
+                s2 += v2[h];
+            }
         }
         mean = s1 / s.count;
         var = s2 / s.count - mean * mean;

@@ -108,11 +108,17 @@ __device__ __forceinline__ void lds_zero(double* p, int n) {
 __device__ __forceinline__ double* cshard(double* sums, int width) {
     return sums + (long long)(blockIdx.x % RNVP_COUPLING_SHARDS) * width;
 }
-// sum over the shards of entry i of a [shards][width] reduction
+// sum over the shards of entry i of a [shards][width] reduction.  Fully
+// unrolled: all RNVP_COUPLING_SHARDS loads are independent and go out
+// together (one memory round trip, not one per unroll group), then are
+// added in shard order.
 __device__ __forceinline__ double csum(const double* sums, int width, int i) {
+    double v[RNVP_COUPLING_SHARDS];
+#pragma unroll
+    for (int h = 0; h < RNVP_COUPLING_SHARDS; ++h) v[h] = sums[(long long)h * width + i];
     double t = 0.0;
-#pragma unroll 8
-    for (int h = 0; h < RNVP_COUPLING_SHARDS; ++h) t += sums[(long long)h * width + i];
+#pragma unroll
+    for (int h = 0; h < RNVP_COUPLING_SHARDS; ++h) t += v[h];
     return t;
 }
 
