@@ -243,6 +243,60 @@ extern "C" int rnvp_u8_to_unit(const uint8_t* x, float* y, long long n, void* st
 }
 
 // ---------------------------------------------------------------------------
+// NCHW fp32 <-> NHWC (channel stride cs, fp32 / bf16) layout moves: the
+// operands of a standalone WeightNormConv2d call (modules_realnvp.py:64-71).
+// Off the training path (the coupling engine keeps the net in NHWC), so a
+// plain grid-stride element map: coalesced on the written side.
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void k_nchw_to_nhwc(const float* __restrict__ x, T* __restrict__ y, int C, int HW, int cs, long long n) {
+    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+        const long long m = e / cs;
+        const int c = (int)(e - m * cs);
+        const long long b = m / HW;
+        const int p = (int)(m - b * HW);
+        stv(&y[e], c < C ? x[(b * C + c) * HW + p] : 0.f);
+    }
+}
+
+template <typename T>
+__global__ void k_nhwc_to_nchw(const T* __restrict__ x, float* __restrict__ y, int C, int HW, int cs, long long n) {
+    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+        const int p = (int)(e % HW);
+        const long long t = e / HW;
+        const int c = (int)(t % C);
+        const long long b = t / C;
+        y[e] = ldv(&x[(b * HW + p) * cs + c]);
+    }
+}
+
+extern "C" int rnvp_nchw_to_nhwc(const float* x, void* y, int B, int C, int H, int W, int cs, int dtype, void* stream) {
+    if (B < 0 || C <= 0 || H <= 0 || W <= 0 || cs < C) return RNVP_E_INVALID;
+    if (dtype != RNVP_F32 && dtype != RNVP_BF16) return RNVP_E_INVALID;
+    const long long n = (long long)B * H * W * cs;
+    if (n == 0) return RNVP_OK;
+    if (!x || !y) return RNVP_E_INVALID;
+    hipStream_t s = (hipStream_t)stream;
+    if (dtype == RNVP_F32) k_nchw_to_nhwc<float><<<rnvp_grid(n, 256), 256, 0, s>>>(x, (float*)y, C, H * W, cs, n);
+    else k_nchw_to_nhwc<bf16_t><<<rnvp_grid(n, 256), 256, 0, s>>>(x, (bf16_t*)y, C, H * W, cs, n);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+extern "C" int rnvp_nhwc_to_nchw(const void* x, float* y, int B, int C, int H, int W, int cs, int dtype, void* stream) {
+    if (B < 0 || C <= 0 || H <= 0 || W <= 0 || cs < C) return RNVP_E_INVALID;
+    if (dtype != RNVP_F32 && dtype != RNVP_BF16) return RNVP_E_INVALID;
+    const long long n = (long long)B * C * H * W;
+    if (n == 0) return RNVP_OK;
+    if (!x || !y) return RNVP_E_INVALID;
+    hipStream_t s = (hipStream_t)stream;
+    if (dtype == RNVP_F32) k_nhwc_to_nchw<float><<<rnvp_grid(n, 256), 256, 0, s>>>((const float*)x, y, C, H * W, cs, n);
+    else k_nhwc_to_nchw<bf16_t><<<rnvp_grid(n, 256), 256, 0, s>>>((const bf16_t*)x, y, C, H * W, cs, n);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+// ---------------------------------------------------------------------------
 // prior log-prob (flow_realnvp.py:329-340; train.py:109 prior = N(0,1))
 // ---------------------------------------------------------------------------
 __global__ void k_prior(const float* __restrict__ z, const float* __restrict__ ldj, float* __restrict__ out, int n) {

@@ -3,11 +3,14 @@
 Same class names, constructor signatures, module tree, parameter
 registration order and ``state_dict`` keys as modules_realnvp.py:36-370, so
 reference checkpoints load unchanged and ``torch.manual_seed(s)`` followed by
-construction draws the same initial weights.  The arithmetic does NOT run
-through these modules' children: a coupling's forward / inverse / backward
-are executed by ``realnvp_hip.engine.CouplingEngine`` on the MI355X (HIP
-kernels behind include/realnvp_hip.h).  Inputs must live on a HIP device;
-there is no CPU path.
+construction draws the same initial weights.  A coupling's forward / inverse /
+backward do NOT run through its children: they are executed, fused, by
+``realnvp_hip.engine.CouplingEngine`` on the MI355X (HIP kernels behind
+include/realnvp_hip.h).  The s/t-network submodules are still callable on
+their own as in the reference: WeightNormConv2d runs the same HIP kernels one
+at a time (``realnvp_hip.standalone``), ResidualBlock / ResidualModule
+compose their children like modules_realnvp.py:107-114, 175-194.  Inputs
+must live on a HIP device; there is no CPU path.
 """
 import math
 
@@ -16,6 +19,7 @@ import torch
 import torch.nn as nn
 
 from realnvp_hip.functions import coupling_apply, coupling_reverse
+from realnvp_hip.standalone import wn_conv2d
 
 __all__ = ["WeightNormConv2d", "ResidualBlock", "ResidualModule", "AbstractCoupling",
            "CheckerboardAffineCoupling", "ChannelwiseAffineCoupling", "AffineCoupling"]
@@ -27,9 +31,10 @@ class _ConvParams(nn.Module):
     Initialisation follows nn.Conv2d.reset_parameters (same RNG draws) and
     weight_norm's g = ||v|| (modules_realnvp.py:53-62)."""
 
-    def __init__(self, in_dim, out_dim, kernel_size, bias, weight_norm, scale):
+    def __init__(self, in_dim, out_dim, kernel_size, bias, weight_norm, scale, padding=None):
         super().__init__()
         k = kernel_size if isinstance(kernel_size, int) else kernel_size[0]
+        self.padding = k // 2 if padding is None else (padding if isinstance(padding, int) else padding[0])
         w = torch.empty(out_dim, in_dim, k, k)
         nn.init.kaiming_uniform_(w, a=math.sqrt(5))
         b = None
@@ -57,8 +62,9 @@ class _ConvParams(nn.Module):
             else:
                 self.register_parameter("bias", None)
 
-    def forward(self, x):   # pragma: no cover - fused into the engine
-        raise NotImplementedError("convolutions run inside the coupling engine (realnvp_hip)")
+    def forward(self, x):
+        """The weight-normalised nn.Conv2d on its own (HIP kernels, fp32)."""
+        return wn_conv2d(self, x)
 
 
 class WeightNormConv2d(nn.Module):
@@ -68,11 +74,12 @@ class WeightNormConv2d(nn.Module):
         super().__init__()
         if stride != 1:
             raise NotImplementedError("only stride 1 occurs on the RealNVP path")
-        self.conv = _ConvParams(in_dim, out_dim, kernel_size, bias, weight_norm, scale)
+        self.conv = _ConvParams(in_dim, out_dim, kernel_size, bias, weight_norm, scale, padding)
         self.padding, self.scale = padding, scale
 
-    def forward(self, x):   # pragma: no cover
-        raise NotImplementedError("convolutions run inside the coupling engine (realnvp_hip)")
+    def forward(self, x):
+        """modules_realnvp.py:64-71 (standalone call: realnvp_hip.standalone)."""
+        return self.conv(x)
 
 
 class ResidualBlock(nn.Module):
@@ -94,8 +101,10 @@ class ResidualBlock(nn.Module):
                 nn.BatchNorm2d(dim), nn.ReLU(),
                 WeightNormConv2d(dim, dim, (3, 3), stride=1, padding=1, bias=True, weight_norm=weight_norm, scale=True))
 
-    def forward(self, x):   # pragma: no cover
-        raise NotImplementedError("residual blocks run inside the coupling engine (realnvp_hip)")
+    def forward(self, x):
+        """modules_realnvp.py:107-114 (standalone call; inside a coupling the
+        engine runs it fused)."""
+        return x + self.res_block(self.in_block(x))
 
 
 class ResidualModule(nn.Module):
@@ -138,8 +147,20 @@ class ResidualModule(nn.Module):
                     WeightNormConv2d(dim, out_dim, (3, 3), stride=1, padding=1, bias=True, weight_norm=weight_norm,
                                      scale=True))
 
-    def forward(self, x):   # pragma: no cover
-        raise NotImplementedError("the s/t network runs inside the coupling engine (realnvp_hip)")
+    def forward(self, x):
+        """modules_realnvp.py:175-194 (standalone call; inside a coupling the
+        engine runs it fused)."""
+        if self.res_blocks > 0:
+            x = self.in_block(x)
+            out = self.in_skip(x) if self.skip else None
+            for i in range(len(self.core_block)):
+                x = self.core_block[i](x)
+                if self.skip:
+                    out = out + self.core_skips[i](x)
+            if self.skip:
+                x = out
+            return self.out_block(x)
+        return self.block(x)
 
 
 class AbstractCoupling(nn.Module):

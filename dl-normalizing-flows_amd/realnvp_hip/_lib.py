@@ -108,6 +108,8 @@ _SIGS = {
     "rnvp_logit_fwd": (i32, [vp, vp, C.c_uint64, C.c_uint64, vp, f32, vp, vp, i32, i32, vp]),
     "rnvp_logit_inv": (i32, [vp, vp, f32, i64, vp]),
     "rnvp_u8_to_unit": (i32, [vp, vp, i64, vp]),
+    "rnvp_nchw_to_nhwc": (i32, [vp, vp, i32, i32, i32, i32, i32, i32, vp]),
+    "rnvp_nhwc_to_nchw": (i32, [vp, vp, i32, i32, i32, i32, i32, i32, vp]),
     "rnvp_prior_logprob": (i32, [vp, vp, vp, i32, i32, vp]),
     "rnvp_prior_logprob_bwd": (i32, [vp, vp, vp, i32, i32, vp]),
     "rnvp_bn_running_update": (i32, [vp, i32, i32, f32, vp]),

@@ -67,6 +67,13 @@ int rnvp_logit_inv(const float* x, float* y, float constraint, long long n, void
  * real-data pipeline ship 1 B/pixel over PCIe and convert on the device. */
 int rnvp_u8_to_unit(const uint8_t* x, float* y, long long n, void* stream);
 
+/* ---- NCHW fp32 <-> NHWC layout moves (standalone WeightNormConv2d) -----
+ * modules_realnvp.py:64-71 called on its own: the operand moves into the
+ * engine's NHWC layout (channel stride cs >= C, zero padded; dtype
+ * RNVP_F32 / RNVP_BF16) and the result back. */
+int rnvp_nchw_to_nhwc(const float* x, void* y, int B, int C, int H, int W, int cs, int dtype, void* stream);
+int rnvp_nhwc_to_nchw(const void* x, float* y, int B, int C, int H, int W, int cs, int dtype, void* stream);
+
 /* ---- prior log-prob and per-sample reduction (flow_realnvp.py:329-340) --
  * out[b] = ldj[b] + sum_i (-z_i^2/2 - log(2 pi)/2)       (N(0,1) prior)
  * bwd: gz_i = -z_i * gout[b] */
