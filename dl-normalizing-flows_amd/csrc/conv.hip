@@ -573,7 +573,7 @@ constexpr int DK_MAX_CS = 1024;
 // repeated per tap and per channel tile.  Only the weights stream from global
 // memory (register ring, DK k-steps ahead; every load unconditional).  The
 // four waves split K (interleaved k-steps) and their partial tiles are summed
-// through LDS for the fused epilogue, as in k_conv_dk.
+// through LDS for the fused epilogue.
 
 template <typename T, int BN>
 size_t halo_lds_bytes(int cs, int W, int ks) {
