@@ -1613,6 +1613,28 @@ __global__ __launch_bounds__(256) void k_wn_pack(const rnvp_wn_desc* __restrict_
 // into LDS in v's [ci][tap] order (coalesced over the packed k), then the
 // weight-norm backward and the bias partial sum.
 
+// bias sum over the replicas, and re-zeroing of the replicas (zero_after)
+__device__ __forceinline__ void wn_bwd_tail(const rnvp_wn_desc& d, float* gbase, int co, int nz, long long zs,
+                                            double* red) {
+    if (d.dbp) {
+        float bs = 0.f;
+        for (int z = threadIdx.x; z < nz; z += blockDim.x) bs += d.dbp[(long long)z * d.cout + co];
+        bs = block_sum(bs, (float*)red);
+        if (threadIdx.x == 0) gbase[d.db_off + co] = bs;
+        if (d.zero_after) {
+            __syncthreads();
+            for (int z = threadIdx.x; z < nz; z += blockDim.x) d.dbp[(long long)z * d.cout + co] = 0.f;
+        }
+    }
+    if (d.zero_after) {   // leave the replicas zero for the next atomic accumulation
+        __syncthreads();
+        float* dwz = d.dw + (long long)co * d.kp_f;
+        const int K = d.ks * d.ks * d.cs_in;
+        for (int z = 0; z < nz; ++z)
+            for (int k = threadIdx.x; k < K; k += blockDim.x) dwz[z * zs + k] = 0.f;
+    }
+}
+
 __global__ void k_wn_bwd(const rnvp_wn_desc* __restrict__ descs, int n_desc, float* gbase, int rows, double* z0,
                          long long n0, double* z1, long long n1) {
     if ((int)blockIdx.x >= rows) {   // extra workgroups: zero the caller's sums ranges
@@ -1633,12 +1655,82 @@ __global__ void k_wn_bwd(const rnvp_wn_desc* __restrict__ descs, int n_desc, flo
     const float* v = d.v + (long long)co * kr;
     const float* dw = d.dw + (long long)co * d.kp_f;
     const bool in_lds = kr <= WN_ROW_LDS;
-    float* dwz = d.dw + (long long)co * d.kp_f;
     auto dw_at = [&](int k) {
         float t = 0.f;
         for (int z = 0; z < nz; ++z) t += dw[z * zs + k];
         return t;
     };
+    if (in_lds && blockDim.x == 256 && nz <= 8 && kk * d.cs_in <= WN_ROW_LDS) {
+        // one memory round trip: every load of the row is issued up front --
+        // this thread's v elements (kept in registers for both passes) and its
+        // float4 chunks of the packed dW row, summed over the nz replicas --
+        // then the dW row is gathered into v's [ci][tap] order in LDS
+        constexpr int PT = WN_ROW_LDS / 256, P4 = (WN_ROW_LDS / 4 + 255) / 256;
+        const int K4 = kk * d.cs_in / 4;            // cs_in % 8 == 0: a chunk never straddles a tap
+        const float rcs = 1.0f / (float)d.cs_in;
+        float vr[PT];
+#pragma unroll
+        for (int j = 0; j < PT; ++j) {
+            const int i = threadIdx.x + j * 256;
+            vr[j] = v[i < kr ? i : 0];
+        }
+        float4 cw[P4];
+#pragma unroll
+        for (int j = 0; j < P4; ++j) {
+            const int q4 = threadIdx.x + j * 256;
+            const float4* src = (const float4*)dw + (q4 < K4 ? q4 : 0);
+            float4 t = src[0];
+#pragma unroll
+            for (int z = 1; z < 8; ++z) {
+                if (z < nz) {
+                    const float4 u = src[z * zs / 4];
+                    t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+                }
+            }
+            cw[j] = t;
+        }
+#pragma unroll
+        for (int j = 0; j < P4; ++j) {
+            const int q4 = threadIdx.x + j * 256;
+            if (q4 < K4) {
+                const int k = 4 * q4, tap = fdiv_small(k, rcs), ci = k - tap * d.cs_in;
+                const float e[4] = {cw[j].x, cw[j].y, cw[j].z, cw[j].w};
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (ci + u < d.cin) rowbuf[(ci + u) * kk + tap] = e[u];
+            }
+        }
+        __syncthreads();
+        float dr[PT];
+        double dot = 0;
+#pragma unroll
+        for (int j = 0; j < PT; ++j) {
+            const int i = threadIdx.x + j * 256;
+            dr[j] = i < kr ? rowbuf[i] : 0.f;
+            dot += (double)dr[j] * vr[j];
+        }
+        dot = block_sum(dot, red);
+        float* dv = gbase + d.dv_off + (long long)co * kr;
+        if (d.g) {
+            const float nrm = d.norm[co];
+            const float gs = d.g[co] / nrm;
+            const float proj = (float)(dot / ((double)nrm * nrm));
+#pragma unroll
+            for (int j = 0; j < PT; ++j) {
+                const int i = threadIdx.x + j * 256;
+                if (i < kr) dv[i] = gs * (dr[j] - proj * vr[j]);
+            }
+            if (threadIdx.x == 0 && d.dg_off >= 0) gbase[d.dg_off + co] = (float)(dot / nrm);
+        } else {
+#pragma unroll
+            for (int j = 0; j < PT; ++j) {
+                const int i = threadIdx.x + j * 256;
+                if (i < kr) dv[i] = dr[j];
+            }
+        }
+        wn_bwd_tail(d, gbase, co, nz, zs, red);
+        return;
+    }
     if (in_lds) {
         const int K = kk * d.cs_in;
         const float rcs = 1.0f / (float)d.cs_in;
@@ -1666,22 +1758,7 @@ __global__ void k_wn_bwd(const rnvp_wn_desc* __restrict__ descs, int n_desc, flo
     } else {
         for (int i = threadIdx.x; i < kr; i += blockDim.x) dv[i] = dwv(i);
     }
-    if (d.dbp) {
-        float bs = 0.f;
-        for (int z = threadIdx.x; z < nz; z += blockDim.x) bs += d.dbp[(long long)z * d.cout + co];
-        bs = block_sum(bs, (float*)red);
-        if (threadIdx.x == 0) gbase[d.db_off + co] = bs;
-        if (d.zero_after) {
-            __syncthreads();
-            for (int z = threadIdx.x; z < nz; z += blockDim.x) d.dbp[(long long)z * d.cout + co] = 0.f;
-        }
-    }
-    if (d.zero_after) {   // leave the replicas zero for the next atomic accumulation
-        __syncthreads();
-        const int K = kk * d.cs_in;
-        for (int z = 0; z < nz; ++z)
-            for (int k = threadIdx.x; k < K; k += blockDim.x) dwz[z * zs + k] = 0.f;
-    }
+    wn_bwd_tail(d, gbase, co, nz, zs, red);
 }
 
 inline bool al16(const void* p) { return (((uintptr_t)p) & 15) == 0; }

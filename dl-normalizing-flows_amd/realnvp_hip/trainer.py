@@ -444,15 +444,20 @@ class FlowTrainer:
         self.graph = torch.cuda.CUDAGraph()
         self.graph_opt = None
         self.graph_input = self.external_input
+        # thread-local capture: other threads keep their HIP calls legal
+        # meanwhile -- the RCCL process group's watchdog polls the events of
+        # the warm-up steps' all-reduces, and under the default (global) mode
+        # such a query during our capture is an error that aborts the process
+        mode = "thread_local"
         if self.pg is None or self.comm_stream is not None:
-            with torch.cuda.graph(self.graph):
+            with torch.cuda.graph(self.graph, capture_error_mode=mode):
                 self._fwd_bwd()
                 self._optimizer()
         else:
-            with torch.cuda.graph(self.graph):
+            with torch.cuda.graph(self.graph, capture_error_mode=mode):
                 self._fwd_bwd()
             self.graph_opt = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph_opt):
+            with torch.cuda.graph(self.graph_opt, capture_error_mode=mode):
                 self._optimizer()
         torch.cuda.synchronize()
         if snap is not None:
