@@ -129,7 +129,7 @@ class FlowEvaluator:
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             self._batch()
         torch.cuda.synchronize()
         self.ll_sum.copy_(snap[0])
