@@ -37,6 +37,19 @@ def stream_ptr():
     return torch.cuda.current_stream().cuda_stream
 
 
+def upload(raw, device):
+    """A host descriptor table (bytes) -> a device uint8 tensor, copied on the
+    current stream from pinned memory: a pageable copy would synchronise the
+    stream and serialise the host's launches behind the GPU (the drop-in
+    path builds some tables per call).  The caching host allocator keeps the
+    pinned block until the copy has run."""
+    host = torch.frombuffer(bytearray(raw), dtype=torch.uint8)
+    device = torch.device(device)
+    if device.type != "cuda":
+        return host
+    return host.pin_memory().to(device, non_blocking=True)
+
+
 # Optional launch timing (bench.py's per-kernel roofline): when PROFILE is a
 # list, every engine launch appends (family, algorithmic bytes, flops,
 # start event, end event), events recorded on the launch stream.
@@ -158,6 +171,7 @@ class CouplingEngine:
         self.n_params = off
         self._weights = {}
         self._scratch = {}
+        self._saved_pool = {}
 
     # ------------------------------------------------------------------ params
     def _tensors(self):
@@ -211,7 +225,7 @@ class CouplingEngine:
             tile0 += wn_tiles(spec.cout, spec.cin)
             descs.append(d)
         table = (WNDesc * len(descs))(*descs)
-        dtab = torch.frombuffer(bytearray(bytes(table)), dtype=torch.uint8).to(dev)
+        dtab = upload(bytes(table), dev)
         ws = dict(key=key, arena=ar, geo=geo, descs=descs, table=dtab, rows=row0, tiles=tile0, dtype=dtype)
         self._weights[dtype] = ws
         return ws
@@ -248,10 +262,32 @@ class CouplingEngine:
                               T[bn + "running_var"].data_ptr(), T[bn + "num_batches_tracked"].data_ptr())
                 rows.append(r)
             tab = (BNRunning * len(rows))(*rows)
-            sv["bn_table"] = torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(device)
+            sv["bn_table"] = upload(bytes(tab), device)
             sv["bn_n"] = len(rows)
             sv["bn_cmax"] = max(spec.c for spec in self.P.bns.values())
         return sv
+
+    def _pool_key(self, B, H, W, dtype, device, training):
+        return (B, H, W, dtype, str(device), bool(training))
+
+    def saved(self, B, H, W, dtype, device, training):
+        """A saved-activation arena of this shape: a released one when
+        available (the drop-in's autograd path returns them after backward), so
+        an eager training loop neither reallocates nor re-zeroes the whole
+        arena every call (forward zeroes the batch sums it accumulates)."""
+        pool = self._saved_pool.get(self._pool_key(B, H, W, dtype, device, training))
+        if pool:
+            return pool.pop()
+        return self.alloc_saved(B, H, W, dtype, device, training)
+
+    def release(self, sv):
+        """Hand an arena back (stream-ordered: later users run after the
+        kernels that read it)."""
+        sv.pop("x", None)
+        key = self._pool_key(sv["B"], sv["H"], sv["W"], sv["dtype"], sv["arena"].buf.device, sv["training"])
+        pool = self._saved_pool.setdefault(key, [])
+        if len(pool) < 2:
+            pool.append(sv)
 
     def scratch(self, B, H, W, dtype, device):
         key = (B, H, W, dtype, str(device))
@@ -312,7 +348,7 @@ class CouplingEngine:
         tab = (WNDesc * len(descs))(*descs)
         nmax = max(max(chan_stride(s.cin), chan_stride(s.cout)) for s in self.P.convs.values())
         wse = splitk_elems(M, nmax)
-        sc = dict(arena=ar, zero=zr, wn_table=torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(device),
+        sc = dict(arena=ar, zero=zr, wn_table=upload(bytes(tab), device),
                   wn_key=wsz["key"], wn_rows=wsz["rows"], n_wn=len(descs), shards=sh,
                   ws=splitk_workspace(device, wse) if wse else None, ws_elems=wse,
                   wg=wg, wg_nz=nz, wg_nrep=nrep, wg_ws=wgws)

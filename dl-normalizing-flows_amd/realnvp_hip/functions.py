@@ -11,7 +11,7 @@ import torch
 
 from . import _lib
 from ._lib import TensorRef
-from .engine import stream_ptr
+from .engine import stream_ptr, upload
 
 
 def _check_device(x, what):
@@ -29,8 +29,14 @@ class _Coupling(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, mod, training, dtype, full, *params):
         eng = mod.engine()
-        z, ldj, sv = eng.forward(x, training, dtype, full)
-        ctx.eng, ctx.sv, ctx.full = eng, sv, full
+        B, _, H, W = x.shape
+        sv = eng.saved(B, H, W, dtype, x.device, training)
+        z, ldj, sv = eng.forward(x, training, dtype, full, saved=sv)
+        if any(ctx.needs_input_grad):
+            ctx.eng, ctx.sv, ctx.full = eng, sv, full
+        else:   # no backward will read it
+            eng.release(sv)
+            ctx.eng, ctx.sv, ctx.full = eng, None, full
         ctx.mark_non_differentiable()
         return z, ldj
 
@@ -54,6 +60,7 @@ class _Coupling(torch.autograd.Function):
             else:
                 grads.append(None)
         ctx.sv = None
+        eng.release(sv)
         return (gx, None, None, None, None) + tuple(grads)
 
 
@@ -214,14 +221,27 @@ def std_normal_logprob(z, ldj):
     return _StdNormalLogProb.apply(z.contiguous(), ldj.contiguous())
 
 
+_STD_NORMAL = {}
+
+
 def is_std_normal(prior):
+    """True for torch.distributions.Normal(0, 1) (train.py:109), checked once
+    per prior: the check reads device tensors (a host sync), so its result is
+    cached against the loc / scale storage and version counters."""
     d = torch.distributions
-    if isinstance(prior, d.Normal):
-        try:
-            return bool((prior.loc == 0).all()) and bool((prior.scale == 1).all()) and prior.loc.dim() == 0
-        except Exception:
-            return False
-    return False
+    if not isinstance(prior, d.Normal):
+        return False
+    try:
+        loc, scale = prior.loc, prior.scale
+        key = (loc.data_ptr(), scale.data_ptr(), loc._version, scale._version, tuple(loc.shape))
+        hit = _STD_NORMAL.get(id(prior))
+        if hit is not None and hit[0] is prior and hit[1] == key:
+            return hit[2]
+        v = loc.dim() == 0 and bool((loc == 0).all()) and bool((scale == 1).all())
+        _STD_NORMAL[id(prior)] = (prior, key, v)
+        return v
+    except Exception:
+        return False
 
 
 # ---------------------------------------------------------------------------
@@ -231,7 +251,7 @@ def _refs_table(params, grads, device):
     rows = [TensorRef(p.data_ptr(), g.data_ptr() if g is not None else None, p.numel())
             for p, g in zip(params, grads)]
     tab = (TensorRef * len(rows))(*rows)
-    return torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(device)
+    return upload(bytes(tab), device)
 
 
 class _SumSq(torch.autograd.Function):

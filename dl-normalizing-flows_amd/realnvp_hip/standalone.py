@@ -26,7 +26,7 @@ import torch
 
 from . import _lib
 from ._lib import RNVP_F32, ConvArgs, WgradGroup, WNDesc
-from .engine import splitk_elems, splitk_workspace, stream_ptr, wn_tiles
+from .engine import splitk_elems, splitk_workspace, stream_ptr, upload, wn_tiles
 from .net import chan_stride, round_up
 
 
@@ -75,7 +75,7 @@ def _desc(cp, geo, wf, wd, norm):
 
 
 def _table(d, dev):
-    return torch.frombuffer(bytearray(bytes(d)), dtype=torch.uint8).to(dev)
+    return upload(bytes(d), dev)
 
 
 def _conv_args(geo, x, cs_in, cin, w, kp, y, cs_out, n, bias, dev):

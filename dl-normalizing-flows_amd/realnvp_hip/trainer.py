@@ -50,7 +50,8 @@ def wn_table(engines, dtype, dev):
     if not descs:
         return None
     tab = (WNDesc * len(descs))(*descs)
-    t = torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(dev)
+    from .engine import upload
+    t = upload(bytes(tab), dev)
     return (t, len(descs), row0, tile0)
 
 
