@@ -379,13 +379,27 @@ class CouplingEngine:
                        stat_shards(M))
 
     def _net_forward(self, T, sv, ws, training, s):
+        """The s/t net's conv launches.  Their argument structs depend only on
+        the saved arena, the weight set, the scratch and the parameters'
+        storage, so they are built once per arena (re-built when the weights
+        move) and replayed: per-call host work is the ctypes calls alone."""
         L = _lib.lib()
+        key = (ws["key"], bool(training))
+        plan = sv.get("fwd_plan")
+        if plan is None or plan[0] != key:
+            plan = (key, self._fwd_args(T, sv, ws, training))
+            sv["fwd_plan"] = plan
+        for a, nb, fl in plan[1]:
+            _launch("conv_fwd", nb, fl, L.conv2d, C.byref(a), s)
+
+    def _fwd_args(self, T, sv, ws, training):
         ar = sv["arena"]
         B, H, W = sv["B"], sv["H"], sv["W"]
         M = B * H * W
         dt = DTYPES[sv["dtype"]][0]
         war = ws["arena"]
         sc = self.scratch(B, H, W, sv["dtype"], ar.buf.device)
+        out = []
         for op in self.P.ops:
             spec = self.P.convs[op.conv]
             cs_in, cs_out, kp_f, _ = ws["geo"][op.conv]
@@ -407,7 +421,8 @@ class CouplingEngine:
             a.variant = CONV_VARIANT
             esz = DTYPES[sv["dtype"]][1]
             nb = esz * (M * cs_in + spec.cout * kp_f + M * cs_out * (1 + int(bool(op.residual)) + int(op.accumulate)))
-            _launch("conv_fwd", nb, 2.0 * M * spec.cout * spec.ks * spec.ks * spec.cin, L.conv2d, C.byref(a), s)
+            out.append((a, nb, 2.0 * M * spec.cout * spec.ks * spec.ks * spec.cin))
+        return out
 
     # ---------------------------------------------------------------- forward
     def forward(self, x, training, dtype, full_ldj, saved=None, prepare=True, ldj_sample=None, z_out=None,
@@ -483,6 +498,76 @@ class CouplingEngine:
         return out, ldj
 
     # --------------------------------------------------------------- backward
+    def _bwd_args(self, T, sv, sc, ws, training):
+        """(items, wgrad groups, wgrad bytes, wgrad flops) of the net backward:
+        items are ("dgrad", ConvArgs, bytes, flops, None) or ("bn", BNBwdArgs,
+        bytes, 0, bn name) in launch order; grouped weight gradients: one launch
+        per WGRAD_GROUP_MAX convs (the group travels as a by-value kernel
+        argument); R >= 6 nets have more."""
+        B, H, W, dtype = sv["B"], sv["H"], sv["W"], sv["dtype"]
+        M = B * H * W
+        dt = DTYPES[dtype][0]
+        esz = DTYPES[dtype][1]
+        ar, sar, war = sv["arena"], sc["arena"], ws["arena"]
+        items, groups = [], []
+        wg_bytes = wg_flops = 0.0
+        wbase = sc["wg_ws"].data_ptr()
+        for st in self.steps:
+            op = st.op
+            spec = self.P.convs[op.conv]
+            cs_in, cs_out, kp_f, kp_d = ws["geo"][op.conv]
+            if st.kind == "dgrad":
+                c = ConvArgs()
+                c.dtype, c.B, c.H, c.W, c.ks = dt, B, H, W, spec.ks
+                c.x, c.cs_in, c.cin = sar.ptr(st.gy), cs_out, spec.cout
+                c.w, c.kp = war.ptr("wd:" + op.conv), kp_d
+                c.y = sar.ptr(st.tmp if st.tmp else st.gx)
+                c.cs_out, c.n = cs_in, spec.cin
+                c.residual = sar.ptr(st.residual) if st.residual else None
+                c.accumulate = int(st.accumulate)
+                if op.pro_bn:
+                    c.epi_relu_bn_bwd = 1
+                    c.epi_x = ar.ptr(op.x)
+                    c.epi = self._bn(T, op.pro_bn, training, ar.ptr("s:" + op.pro_bn), M)
+                    c.epi_sums = sar.ptr("e:" + op.pro_bn)
+                if sc["ws"] is not None:
+                    c.ws, c.ws_elems = sc["ws"].data_ptr(), sc["ws_elems"]
+                c.variant = CONV_VARIANT
+                nb = esz * (M * cs_out + spec.cin * kp_d + M * cs_in * (1 + int(bool(op.pro_bn)) + int(bool(
+                    st.residual)) + int(st.accumulate)))
+                items.append(("dgrad", c, nb, 2.0 * M * spec.cout * spec.ks * spec.ks * spec.cin, None))
+            elif st.kind == "bn_apply":
+                bn = op.pro_bn
+                c = BNBwdArgs()
+                c.dtype, c.M, c.C, c.cs = dt, M, spec.cin, cs_in
+                c.g, c.x = sar.ptr(st.tmp), ar.ptr(op.x)
+                c.bn = self._bn(T, bn, training, ar.ptr("s:" + bn), M)
+                c.sums = sar.ptr("e:" + bn)
+                c.sum_shards = sc["shards"]
+                c.dx = sar.ptr(st.gx)
+                c.residual = sar.ptr(st.residual) if st.residual else None
+                c.accumulate = int(st.accumulate)
+                items.append(("bn", c, esz * M * cs_in * (3 + int(bool(st.residual)) + int(st.accumulate)), 0.0, bn))
+            else:
+                if not groups or groups[-1].n_conv >= WGRAD_GROUP_MAX:
+                    grp = WgradGroup()
+                    grp.dtype, grp.B, grp.H, grp.W = dt, B, H, W
+                    groups.append(grp)
+                grp = groups[-1]
+                c = grp.conv[grp.n_conv]
+                grp.n_conv += 1
+                ow, ob = sc["wg"][op.conv]
+                c.x, c.cs_in, c.cin, c.ks = ar.ptr(op.x), cs_in, spec.cin, spec.ks
+                if op.pro_bn:
+                    c.pro_bn_relu = 1
+                    c.pro = self._bn(T, op.pro_bn, training, ar.ptr("s:" + op.pro_bn), M)
+                c.dy, c.cs_dy, c.n = sar.ptr(st.gy), cs_out, spec.cout
+                c.ws, c.kp, c.nz, c.nrep = wbase + 4 * ow, kp_f, sc["wg_nz"], sc["wg_nrep"]
+                c.wsb = wbase + 4 * ob if ob is not None else None
+                wg_bytes += esz * (M * cs_in + M * cs_out) + 4 * sc["wg_nz"] * spec.cout * spec.ks * spec.ks * cs_in
+                wg_flops += 2.0 * M * spec.cout * spec.ks * spec.ks * spec.cin
+        return items, groups, wg_bytes, wg_flops
+
     def backward(self, sv, gz, gl_full, gl_sample, grad_block, gx=None, side=None, after=None, zero_at_end=False):
         """Returns dL/dx; parameter gradients are written into grad_block
         (flat fp32, zeroed by the caller; scale/shift grads accumulate).
@@ -534,71 +619,21 @@ class CouplingEngine:
         a.gscale_part = sar.ptr("gscale_part")
         L.coupling_out_bwd(C.byref(a), s)
 
-        # grouped weight gradients: one launch per WGRAD_GROUP_MAX convs (the
-        # group travels as a by-value kernel argument); R >= 6 nets have more
-        groups = []
-        wg_bytes = wg_flops = 0.0
-        wbase = sc["wg_ws"].data_ptr()
-        for st in self.steps:
-            op = st.op
-            spec = self.P.convs[op.conv]
-            cs_in, cs_out, kp_f, kp_d = ws["geo"][op.conv]
-            _, _, bname = self._conv_names(spec)
-            if st.kind == "dgrad":
-                c = ConvArgs()
-                c.dtype, c.B, c.H, c.W, c.ks = dt, B, H, W, spec.ks
-                c.x, c.cs_in, c.cin = sar.ptr(st.gy), cs_out, spec.cout
-                c.w, c.kp = war.ptr("wd:" + op.conv), kp_d
-                c.y = sar.ptr(st.tmp if st.tmp else st.gx)
-                c.cs_out, c.n = cs_in, spec.cin
-                c.residual = sar.ptr(st.residual) if st.residual else None
-                c.accumulate = int(st.accumulate)
-                if op.pro_bn:
-                    c.epi_relu_bn_bwd = 1
-                    c.epi_x = ar.ptr(op.x)
-                    c.epi = self._bn(T, op.pro_bn, training, ar.ptr("s:" + op.pro_bn), M)
-                    c.epi_sums = sar.ptr("e:" + op.pro_bn)
-                if sc["ws"] is not None:
-                    c.ws, c.ws_elems = sc["ws"].data_ptr(), sc["ws_elems"]
-                c.variant = CONV_VARIANT
-                esz = DTYPES[dtype][1]
-                nb = esz * (M * cs_out + spec.cin * kp_d + M * cs_in * (1 + int(bool(op.pro_bn)) + int(bool(
-                    st.residual)) + int(st.accumulate)))
-                _launch("conv_dgrad", nb, 2.0 * M * spec.cout * spec.ks * spec.ks * spec.cin, L.conv2d, C.byref(c), s)
-            elif st.kind == "bn_apply":
-                bn = op.pro_bn
-                c = BNBwdArgs()
-                c.dtype, c.M, c.C, c.cs = dt, M, spec.cin, cs_in
-                c.g, c.x = sar.ptr(st.tmp), ar.ptr(op.x)
-                c.bn = self._bn(T, bn, training, ar.ptr("s:" + bn), M)
-                c.sums = sar.ptr("e:" + bn)
-                c.sum_shards = sc["shards"]
-                c.dx = sar.ptr(st.gx)
-                c.residual = sar.ptr(st.residual) if st.residual else None
-                c.accumulate = int(st.accumulate)
-                c.dgamma, c.dbeta = gp(bn + "weight"), gp(bn + "bias")
-                esz = DTYPES[dtype][1]
-                nb = esz * M * cs_in * (3 + int(bool(st.residual)) + int(st.accumulate))
-                _launch("bn_bwd", nb, 0.0, L.bn_bwd_apply, C.byref(c), s)
+        # the net's data-gradient chain and grouped weight gradients: argument
+        # structs cached per (saved arena, scratch, weight set); only the
+        # BatchNorm-affine gradient pointers follow this call's grad block
+        key = (ws["key"], id(sc), bool(training))
+        plan = sv.get("bwd_plan")
+        if plan is None or plan[0] != key:
+            plan = (key, self._bwd_args(T, sv, sc, ws, training))
+            sv["bwd_plan"] = plan
+        items, groups, wg_bytes, wg_flops = plan[1]
+        for kind, c, nb, fl, bn in items:
+            if kind == "dgrad":
+                _launch("conv_dgrad", nb, fl, L.conv2d, C.byref(c), s)
             else:
-                if not groups or groups[-1].n_conv >= WGRAD_GROUP_MAX:
-                    grp = WgradGroup()
-                    grp.dtype, grp.B, grp.H, grp.W = dt, B, H, W
-                    groups.append(grp)
-                grp = groups[-1]
-                c = grp.conv[grp.n_conv]
-                grp.n_conv += 1
-                ow, ob = sc["wg"][op.conv]
-                c.x, c.cs_in, c.cin, c.ks = ar.ptr(op.x), cs_in, spec.cin, spec.ks
-                if op.pro_bn:
-                    c.pro_bn_relu = 1
-                    c.pro = self._bn(T, op.pro_bn, training, ar.ptr("s:" + op.pro_bn), M)
-                c.dy, c.cs_dy, c.n = sar.ptr(st.gy), cs_out, spec.cout
-                c.ws, c.kp, c.nz, c.nrep = wbase + 4 * ow, kp_f, sc["wg_nz"], sc["wg_nrep"]
-                c.wsb = wbase + 4 * ob if ob is not None else None
-                esz = DTYPES[dtype][1]
-                wg_bytes += esz * (M * cs_in + M * cs_out) + 4 * sc["wg_nz"] * spec.cout * spec.ks * spec.ks * cs_in
-                wg_flops += 2.0 * M * spec.cout * spec.ks * spec.ks * spec.cin
+                c.dgamma, c.dbeta = gp(bn + "weight"), gp(bn + "bias")
+                _launch("bn_bwd", nb, 0.0, L.bn_bwd_apply, C.byref(c), s)
         # in_bn backward closes the critical path (dL/dx of the coupling) ...
         a.gh0, a.cs_gh0 = sar.ptr("g:h0"), chan_stride(self.P.buf_ch["h0"])
         a.in_bwd_sums = sar.ptr("in_bwd_sums")

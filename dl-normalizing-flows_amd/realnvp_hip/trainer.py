@@ -22,6 +22,7 @@ MI355X-specific structure:
     (train.py:139-154, 249-250 checkpoints).
 """
 import math
+import time
 
 import numpy as np
 import torch
@@ -442,13 +443,20 @@ class FlowTrainer:
                 self.step_eager()
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
+        if self.pg is not None:
+            # the RCCL process group's watchdog thread polls the events of the
+            # warm-up all-reduces until it retires them (every ~100 ms); a poll
+            # that lands inside the capture is a fatal "operation not permitted
+            # when stream is capturing" (seen on the world-1 test), so let it
+            # retire the (already complete) work first.  Collectives issued
+            # during the capture are never handed to the watchdog.
+            time.sleep(0.5)
         self.graph = torch.cuda.CUDAGraph()
         self.graph_opt = None
         self.graph_input = self.external_input
-        # thread-local capture: other threads keep their HIP calls legal
-        # meanwhile -- the RCCL process group's watchdog polls the events of
-        # the warm-up steps' all-reduces, and under the default (global) mode
-        # such a query during our capture is an error that aborts the process
+        # thread-local capture: other threads' HIP calls are not checked
+        # against our capture (HIP still refuses an event query meanwhile,
+        # hence the drain above)
         mode = "thread_local"
         if self.pg is None or self.comm_stream is not None:
             with torch.cuda.graph(self.graph, capture_error_mode=mode):
