@@ -1525,7 +1525,8 @@ constexpr int WN_ROW_LDS = 4608;
 
 // Weight-norm forward, pass 1: ||v|| of every output row, one wave per row
 // (coalesced 4-byte loads, 8 in flight per lane; v rows need not be 16-B
-// aligned inside the parameter arena).
+// aligned inside the parameter arena).  16-B loads (an aligned body between
+// scalar head and tail) measured slower: 184 vs 147 us for config 1's rows.
 __global__ __launch_bounds__(256) void k_wn_norm(const rnvp_wn_desc* __restrict__ descs, int n_desc, int rows) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (row >= rows) return;
@@ -1554,33 +1555,50 @@ __global__ __launch_bounds__(256) void k_wn_norm(const rnvp_wn_desc* __restrict_
 // wd[ci][tp*cs_out + co] = w[co][ci][ks*ks-1-tp].  The images' padding
 // (ci >= cin, co >= cout, k >= ks*ks*cs) is zero from allocation and never
 // written.
-constexpr int WN_TCO = 32, WN_TCI = 32;
+// A 1x1 conv's tile spans WN_TCI1 input channels (the same LDS row, ks*ks = 1
+// float per channel): 8x fewer, 8x larger blocks than 32-channel tiles, with
+// 512-byte forward-image runs.  With the XCD-contiguous tile order and
+// float-reciprocal index math below, config 1's large refresh went from 376
+// to 284 us (profiles/r2_wn_pack_experiment.txt).
+constexpr int WN_TCO = 32, WN_TCI = 32, WN_TCI1 = 256;
+
+__host__ __device__ constexpr int wn_tci(int ks) { return ks == 1 ? WN_TCI1 : WN_TCI; }
 
 template <typename T>
 __global__ __launch_bounds__(256) void k_wn_pack(const rnvp_wn_desc* __restrict__ descs, int n_desc) {
     constexpr int TP = WN_TCI * 9 + 1;                      // LDS row pitch (floats), odd
+    static_assert(WN_TCI1 < TP, "1x1 tile row must fit the LDS row");
     __shared__ float tile[WN_TCO * TP];
     __shared__ float scl[WN_TCO];
-    const rnvp_wn_desc& d = descs[find_tile(descs, n_desc, blockIdx.x)];
-    const int t = blockIdx.x - d.tile0;
-    const int nci = (d.cin + WN_TCI - 1) / WN_TCI;
-    const int co0 = (t / nci) * WN_TCO, ci0 = (t % nci) * WN_TCI;
+    // consecutive tiles (the two halves of a 128-byte line of either image)
+    // on one XCD: block b runs on XCD b % 8, so remap b bijectively
+    const int nb = gridDim.x, b = blockIdx.x;
+    const int q8 = nb / 8, r8 = nb % 8, xcd = b % 8;
+    const int tg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
+    const rnvp_wn_desc& d = descs[find_tile(descs, n_desc, tg)];
+    const int t = tg - d.tile0;
+    const int tci = wn_tci(d.ks);
+    const int nci = (d.cin + tci - 1) / tci;
+    const int co0 = (t / nci) * WN_TCO, ci0 = (t % nci) * tci;
     const int kk = d.ks * d.ks, kr = d.cin * kk;
-    const int nco = min(WN_TCO, d.cout - co0), ncc = min(WN_TCI, d.cin - ci0);
+    const int nco = min(WN_TCO, d.cout - co0), ncc = min(tci, d.cin - ci0);
     const int run = ncc * kk;                               // contiguous floats per output channel
     if (threadIdx.x < WN_TCO) {
         const int co = co0 + threadIdx.x;
         scl[threadIdx.x] = (threadIdx.x < nco && d.g) ? d.g[co] / d.norm[co] : 1.f;
     }
+    // item indices stay < 2^17: float-reciprocal divisions (fdiv_small)
+    const float r_run = 1.0f / (float)run;
     for (int q = threadIdx.x; q < nco * run; q += 256) {
-        const int c = q / run, j = q - c * run;
+        const int c = fdiv_small(q, r_run), j = q - c * run;
         tile[c * TP + j] = d.v[(long long)(co0 + c) * kr + (long long)ci0 * kk + j];
     }
     __syncthreads();
     // forward image: 4 consecutive ci per item
     const int ng = (ncc + 3) / 4;
+    const float r_kng = 1.0f / (float)(kk * ng), r_ng = 1.0f / (float)ng;
     for (int q = threadIdx.x; q < nco * kk * ng; q += 256) {
-        const int c = q / (kk * ng), r = q - c * (kk * ng), tap = r / ng, c4 = (r - tap * ng) * 4;
+        const int c = fdiv_small(q, r_kng), r = q - c * (kk * ng), tap = fdiv_small(r, r_ng), c4 = (r - tap * ng) * 4;
         float w[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) w[e] = c4 + e < ncc ? scl[c] * tile[c * TP + (c4 + e) * kk + tap] : 0.f;
@@ -1594,8 +1612,9 @@ __global__ __launch_bounds__(256) void k_wn_pack(const rnvp_wn_desc* __restrict_
     if (!d.wd) return;
     // data-gradient image: 4 consecutive co per item
     const int mg = (nco + 3) / 4;
+    const float r_kmg = 1.0f / (float)(kk * mg), r_mg = 1.0f / (float)mg;
     for (int q = threadIdx.x; q < ncc * kk * mg; q += 256) {
-        const int ci = q / (kk * mg), r = q - ci * (kk * mg), tp = r / mg, o4 = (r - tp * mg) * 4;
+        const int ci = fdiv_small(q, r_kmg), r = q - ci * (kk * mg), tp = fdiv_small(r, r_mg), o4 = (r - tp * mg) * 4;
         const int tap = kk - 1 - tp;
         float w[4];
 #pragma unroll
@@ -1854,8 +1873,9 @@ extern "C" int rnvp_bn_bwd_apply(const rnvp_bn_bwd_args* a, void* stream) {
     return RNVP_OK;
 }
 
-extern "C" int rnvp_weight_norm_tiles(int cout, int cin) {
-    return ((cout + WN_TCO - 1) / WN_TCO) * ((cin + WN_TCI - 1) / WN_TCI);
+extern "C" int rnvp_weight_norm_tiles(int cout, int cin, int ks) {
+    if (cout <= 0 || cin <= 0 || (ks != 1 && ks != 3)) return RNVP_E_INVALID;
+    return ((cout + WN_TCO - 1) / WN_TCO) * ((cin + wn_tci(ks) - 1) / wn_tci(ks));
 }
 
 extern "C" int rnvp_weight_norm_fwd(const rnvp_wn_desc* d, int n_desc, int total_rows, int total_tiles, int dtype,

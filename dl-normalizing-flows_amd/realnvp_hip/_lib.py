@@ -120,7 +120,7 @@ _SIGS = {
     "rnvp_conv2d_wgrad_grouped": (i32, [C.POINTER(WgradGroup), vp]),
     "rnvp_bn_bwd_apply": (i32, [C.POINTER(BNBwdArgs), vp]),
     "rnvp_weight_norm_fwd": (i32, [vp, i32, i32, i32, i32, vp]),
-    "rnvp_weight_norm_tiles": (i32, [i32, i32]),
+    "rnvp_weight_norm_tiles": (i32, [i32, i32, i32]),
     "rnvp_weight_norm_bwd": (i32, [vp, i32, i32, vp, vp, i64, vp, i64, vp]),
     "rnvp_coupling_in_fwd": (i32, [C.POINTER(CouplingArgs), vp]),
     "rnvp_coupling_out_fwd": (i32, [C.POINTER(CouplingArgs), vp]),

@@ -123,9 +123,12 @@ def stat_shards(M):
     return int(_lib.lib().stat_shards(int(M)))
 
 
-def wn_tiles(cout, cin):
+def wn_tiles(cout, cin, ks):
     """pack tiles of one conv in rnvp_weight_norm_fwd (rnvp_weight_norm_tiles)"""
-    return int(_lib.lib().weight_norm_tiles(int(cout), int(cin)))
+    n = int(_lib.lib().weight_norm_tiles(int(cout), int(cin), int(ks)))
+    if n <= 0:
+        raise RuntimeError("rnvp_weight_norm_tiles: invalid conv shape %d x %d x %d" % (cout, cin, ks))
+    return n
 
 
 _SPLITK_WS = {}
@@ -222,7 +225,7 @@ class CouplingEngine:
             d.nz = 1
             d.tile0 = tile0
             row0 += spec.cout
-            tile0 += wn_tiles(spec.cout, spec.cin)
+            tile0 += wn_tiles(spec.cout, spec.cin, spec.ks)
             descs.append(d)
         table = (WNDesc * len(descs))(*descs)
         dtab = upload(bytes(table), dev)

@@ -107,7 +107,7 @@ class _WNConv(torch.autograd.Function):
         norm = torch.empty(geo.cout, **f32)
         d = _desc(cp, geo, wf, wd, norm)
         tab = _table(d, dev)
-        L.weight_norm_fwd(tab.data_ptr(), 1, geo.cout, wn_tiles(geo.cout, geo.cin), RNVP_F32, s)
+        L.weight_norm_fwd(tab.data_ptr(), 1, geo.cout, wn_tiles(geo.cout, geo.cin, geo.ks), RNVP_F32, s)
         xh = torch.empty(geo.M * geo.cs_in, **f32)
         L.nchw_to_nhwc(x.data_ptr(), xh.data_ptr(), geo.B, geo.cin, geo.H, geo.W, geo.cs_in, RNVP_F32, s)
         yh = torch.empty(geo.M * geo.cs_out, **f32)

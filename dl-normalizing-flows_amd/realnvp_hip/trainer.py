@@ -46,7 +46,7 @@ def wn_table(engines, dtype, dev):
             C.memmove(C.addressof(e), C.addressof(d), C.sizeof(WNDesc))
             e.row0, e.tile0 = row0, tile0
             row0 += e.cout
-            tile0 += wn_tiles(e.cout, e.cin)
+            tile0 += wn_tiles(e.cout, e.cin, e.ks)
             descs.append(e)
     if not descs:
         return None

@@ -211,9 +211,10 @@ typedef struct rnvp_wn_desc {
 } rnvp_wn_desc;
 /* fwd, for any number of convs (a whole model): one launch computes every
  * row norm, one writes both packed images on [32 co] x [32 ci] tiles
- * (total_tiles = sum over the convs of rnvp_weight_norm_tiles(cout, cin)).
+ * ([32 co] x [256 ci] for 1x1 convs; total_tiles = sum over the convs of
+ * rnvp_weight_norm_tiles(cout, cin, ks), < 0 for an invalid shape).
  * The images' padding must be zero on entry (it is never written). */
-int rnvp_weight_norm_tiles(int cout, int cin);
+int rnvp_weight_norm_tiles(int cout, int cin, int ks);
 int rnvp_weight_norm_fwd(const rnvp_wn_desc* descs_device, int n_desc, int total_rows, int total_tiles, int dtype,
                          void* stream);
 /* zero0 / zero1: byte ranges (8-byte multiples, 8-byte aligned, may be
