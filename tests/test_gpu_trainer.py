@@ -280,3 +280,76 @@ def test_capture_restores_state_and_fixes_input_mode():
     tr.set_input(x, ld)
     tr.step()
     assert int(tr.step_t.item()) == 1
+
+
+# ---------------------------------------------------------------------------
+# data parallel path at world size 2: two ranks on the one GPU over gloo
+# (RCCL needs one GPU per rank; gloo reduces device tensors through the host).
+# Each rank trains on its own batch shard; the all-reduced gradient must be
+# the mean of the two single-process gradients and both ranks must take the
+# same Adam step.
+def _dp_rank(rank, port, comm, out):
+    import os
+    import sys
+    import torch.distributed as dist
+    from conftest import PKG
+    sys.path.insert(0, PKG)
+    from realnvp_hip.trainer import FlowTrainer
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        tr = FlowTrainer(make_model(32, 8, 1), 4, dtype="fp32", process_group=dist.group.WORLD, comm=comm,
+                         bucket_mb=1)
+        tr.set_pixels(pixels(4, 3, 32, seed=5 + rank).to(DEV))
+        tr.step()
+        torch.cuda.synchronize()
+        torch.save({"grad": tr.grad.cpu(), "param": tr.param.cpu(), "nb": len(tr.buckets),
+                    "step": int(tr.step_t.item())}, out)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("comm", ["split", "overlap"])
+def test_process_group_world2_matches_mean_of_shards(comm, tmp_path):
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    outs = [str(tmp_path / ("rank%d.pt" % r)) for r in range(2)]
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_dp_rank, args=(r, port, comm, outs[r])) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+            p.join()
+    assert [p.exitcode for p in procs] == [0, 0]
+    res = [torch.load(o, weights_only=True) for o in outs]
+    # single-process gradients of the two shards (same initial weights)
+    from realnvp_hip.trainer import FlowTrainer
+    refs = []
+    for r in range(2):
+        tr = FlowTrainer(make_model(32, 8, 1), 4, dtype="fp32")
+        tr.set_pixels(pixels(4, 3, 32, seed=5 + r).to(DEV))
+        p0 = tr.param.clone()
+        tr.step()
+        torch.cuda.synchronize()
+        refs.append(tr.grad.cpu())
+    p0 = p0.cpu()
+    mean = 0.5 * (refs[0] + refs[1])
+    # the same shard twice: the noise floor of the replica atomics
+    tr = FlowTrainer(make_model(32, 8, 1), 4, dtype="fp32")
+    tr.set_pixels(pixels(4, 3, 32, seed=5).to(DEV))
+    tr.step()
+    floor = float((tr.grad.cpu() - refs[0]).norm() / refs[0].norm())
+    assert res[0]["nb"] > 1 and res[0]["step"] == res[1]["step"] == 1
+    assert torch.equal(res[0]["grad"], res[1]["grad"])      # one reduced gradient on both ranks
+    assert torch.equal(res[0]["param"], res[1]["param"])    # one Adam step on both ranks
+    assert float((res[0]["grad"] - mean).norm() / mean.norm()) < max(1e-4, 8 * floor)
+    assert float((refs[0] - mean).norm() / mean.norm()) > 1e-2   # the shards really differ
+    assert float((res[0]["param"] - p0).abs().max()) <= 2 * tr.lr * 1.01
