@@ -1867,8 +1867,10 @@ extern "C" int rnvp_bn_bwd_apply(const rnvp_bn_bwd_args* a, void* stream) {
     const int CH = a->dtype == RNVP_F32 ? 4 : 8;
     const long long nch = a->M * (a->cs / CH);
     size_t shm = 68 * (size_t)a->cs;   // 4*cs fp64 + 9*cs f32 (see k_bn_bwd)
-    if (a->dtype == RNVP_F32) k_bn_bwd<float><<<rnvp_grid(nch, 256, 2048), 256, shm, s>>>(*a);
-    else k_bn_bwd<bf16_t><<<rnvp_grid(nch, 256, 2048), 256, shm, s>>>(*a);
+    // every workgroup first reduces the fp64 statistic shards: 1024 groups
+    // (4 per CU) amortise that best (sweep 512-4096, profiles/r2_wn_pack_experiment.txt)
+    if (a->dtype == RNVP_F32) k_bn_bwd<float><<<rnvp_grid(nch, 256, 1024), 256, shm, s>>>(*a);
+    else k_bn_bwd<bf16_t><<<rnvp_grid(nch, 256, 1024), 256, shm, s>>>(*a);
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
 }
