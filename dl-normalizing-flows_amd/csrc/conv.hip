@@ -1559,7 +1559,7 @@ __global__ __launch_bounds__(256) void k_wn_norm(const rnvp_wn_desc* __restrict_
 // float per channel): 8x fewer, 8x larger blocks than 32-channel tiles, with
 // 512-byte forward-image runs.  With the XCD-contiguous tile order and
 // float-reciprocal index math below, config 1's large refresh went from 376
-// to 284 us (profiles/r2_wn_pack_experiment.txt).
+// to 284 us (profiles/r2_small_kernel_sweeps.txt).
 constexpr int WN_TCO = 32, WN_TCI = 32, WN_TCI1 = 256;
 
 __host__ __device__ constexpr int wn_tci(int ks) { return ks == 1 ? WN_TCI1 : WN_TCI; }
@@ -1868,7 +1868,7 @@ extern "C" int rnvp_bn_bwd_apply(const rnvp_bn_bwd_args* a, void* stream) {
     const long long nch = a->M * (a->cs / CH);
     size_t shm = 68 * (size_t)a->cs;   // 4*cs fp64 + 9*cs f32 (see k_bn_bwd)
     // every workgroup first reduces the fp64 statistic shards: 1024 groups
-    // (4 per CU) amortise that best (sweep 512-4096, profiles/r2_wn_pack_experiment.txt)
+    // (4 per CU) amortise that best (sweep 512-4096, profiles/r2_small_kernel_sweeps.txt)
     if (a->dtype == RNVP_F32) k_bn_bwd<float><<<rnvp_grid(nch, 256, 1024), 256, shm, s>>>(*a);
     else k_bn_bwd<bf16_t><<<rnvp_grid(nch, 256, 1024), 256, shm, s>>>(*a);
     RNVP_LAUNCH_CHECK();
