@@ -582,8 +582,9 @@ class CouplingEngine:
         the weight-norm backward that sums the slabs.
 
         zero_at_end: the backward sums are zero on entry (not re-zeroed here)
-        and the weight-norm backward launch leaves both these and the
-        forward's batch sums zero for the next step (persistent arenas)."""
+        and the weight-norm backward launch leaves the forward's batch sums
+        zero for the next step too (persistent arenas).  Either way the
+        shared backward scratch is left zero."""
         L = _lib.lib()
         x = sv["x"]
         B, H, W, dtype, training = sv["B"], sv["H"], sv["W"], sv["dtype"], sv["training"]
@@ -654,11 +655,17 @@ class CouplingEngine:
             for grp in groups:
                 _launch("conv_wgrad", wg_bytes / len(groups), wg_flops / len(groups), L.conv2d_wgrad_grouped,
                         C.byref(grp), ss)
+            # the backward reductions live in the scratch shared by every
+            # caller of this shape (trainer and drop-in autograd alike): it is
+            # ALWAYS left zero, so whichever path runs next finds it clean
+            # (the drop-in also zeroes it on entry).  The forward's batch sums
+            # belong to the saved arena: left zero only for the trainer's
+            # persistent arenas (zero_at_end).
             if zero_at_end:
                 f0, f1 = ar.range_bytes("in_sums", list(ar.slots)[-1])
                 zr = (ar.base + f0, f1 - f0, sar.base + z0, z1 - z0)
             else:
-                zr = (None, 0, None, 0)
+                zr = (None, 0, sar.base + z0, z1 - z0)
             L.weight_norm_bwd(sc["wn_table"].data_ptr(), sc["n_wn"], sc["wn_rows"], gbase, *zr, ss)
             if after is not None:
                 after()

@@ -19,7 +19,7 @@ import torch
 
 from . import _lib
 from .engine import stream_ptr
-from .trainer import wn_forward, wn_table
+from .trainer import weights_key, wn_forward, wn_table
 
 
 class FlowEvaluator:
@@ -42,10 +42,21 @@ class FlowEvaluator:
         self.counter = torch.zeros(1, dtype=torch.int64, device=self.dev)
         self.n_batches = 0
         self._plan(f32)
-        engines = [st[1].engine() for st in self.ops if st[0] == "coupling"]
-        self.table = wn_table(list(dict.fromkeys(engines)), self.dtype, self.dev)
+        self.engines = list(dict.fromkeys(st[1].engine() for st in self.ops if st[0] == "coupling"))
+        self.table = wn_table(self.engines, self.dtype, self.dev)
+        self._wkey = weights_key(self.engines, self.dtype)
         self.graph = None
         self.use_graph = graph
+
+    def _check_weights(self):
+        """Rebuild the weight-norm table and drop the captured graph when the
+        parameters moved since they were built (their packed-weight arenas
+        were re-allocated): both hold raw arena pointers."""
+        k = weights_key(self.engines, self.dtype)
+        if k != self._wkey:
+            self.table = wn_table(self.engines, self.dtype, self.dev)
+            self._wkey = k
+            self.graph = None
 
     def _plan(self, f32):
         """the op list of flow_realnvp.RealNVP.f (flow_realnvp.py:252-327) with
@@ -137,6 +148,7 @@ class FlowEvaluator:
 
     def begin(self):
         """Start a validation pass: refresh the packed weights, zero the sum."""
+        self._check_weights()
         if self.table is not None:
             wn_forward(self.table, self.dtype)
         self.ll_sum.zero_()

@@ -6,6 +6,7 @@ fresh gradient tensors (views into one flat block per call), so torch's
 accumulation / set_to_none semantics are unchanged.
 """
 import ctypes as C
+import warnings
 
 import torch
 
@@ -73,16 +74,26 @@ def coupling_apply(mod, x, full_ldj):
     return _Coupling.apply(x, mod, mod.training, mod.compute_dtype, full_ldj, *params)
 
 
+_REVERSE_WARNED = [False]
+
+
 def coupling_reverse(mod, x):
     """Inverse pass (modules_realnvp.py:284-291, 345-351).  Returns (x, log_diag_J)
     where log_diag_J is the masked log_rescale, as the reference returns."""
     _check_device(x, type(mod).__name__)
-    if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in mod.parameters())):
-        # sampling is a no-grad path in the reference loop (train.py:253-259);
-        # the engine's inverse has no backward, so refuse rather than return
-        # outputs that silently carry no gradient.
-        raise RuntimeError("%s(reverse=True): the MI355X engine's inverse pass is not differentiable; run it under "
-                           "torch.no_grad() (as train.py:253-259 does)" % type(mod).__name__)
+    if torch.is_grad_enabled() and x.requires_grad:
+        # the engine's inverse has no backward: refuse an input that asks for
+        # a gradient rather than return outputs that silently carry none
+        raise RuntimeError("%s(reverse=True): the MI355X engine's inverse pass is not differentiable with respect "
+                           "to its input; run it under torch.no_grad() (as train.py:253-259 does)"
+                           % type(mod).__name__)
+    if torch.is_grad_enabled() and not _REVERSE_WARNED[0] and any(p.requires_grad for p in mod.parameters()):
+        # the reference's RealNVP.sample()/g() work without no_grad on a model
+        # with trainable parameters: do the same, once telling the caller that
+        # the outputs are detached
+        _REVERSE_WARNED[0] = True
+        warnings.warn("%s(reverse=True) runs without autograd on the MI355X engine: the outputs carry no gradient "
+                      "with respect to the parameters" % type(mod).__name__, stacklevel=3)
     with torch.no_grad():
         out, ldj = mod.engine().reverse(x.contiguous(), mod.training, mod.compute_dtype)
     return out, ldj

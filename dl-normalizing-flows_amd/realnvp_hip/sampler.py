@@ -12,7 +12,7 @@ import torch
 
 from . import _lib
 from .engine import stream_ptr
-from .trainer import wn_forward, wn_table
+from .trainer import weights_key, wn_forward, wn_table
 
 
 class FlowSampler:
@@ -31,11 +31,26 @@ class FlowSampler:
         self.z = torch.empty(n, C, S, S, **f32)
         self.out = torch.empty(n, C, S, S, **f32)
         self._plan(f32)
-        engines = [st[1].engine() for st in self.ops if st[0] == "coupling"]
-        self.table = wn_table(list(dict.fromkeys(engines)), self.dtype, self.dev)
+        self.engines = list(dict.fromkeys(st[1].engine() for st in self.ops if st[0] == "coupling"))
+        self.table = wn_table(self.engines, self.dtype, self.dev)
+        self._wkey = weights_key(self.engines, self.dtype)
         self.graph = None
+        self.use_graph = graph
         if graph:
             self._capture()
+
+    def _check_weights(self):
+        """Rebuild the weight-norm table (and the graph) when the parameters
+        moved since capture: both hold raw packed-weight arena pointers, and
+        the old arena has been freed (e.g. a FlowTrainer built after this
+        sampler re-pointed the parameters into its flat arena)."""
+        k = weights_key(self.engines, self.dtype)
+        if k != self._wkey:
+            self.table = wn_table(self.engines, self.dtype, self.dev)
+            self._wkey = k
+            self.graph = None
+            if self.use_graph:
+                self._capture()
 
     def _plan(self, f32):
         """the op list of flow_realnvp.RealNVP.g with persistent buffers"""
@@ -131,6 +146,7 @@ class FlowSampler:
         """n images in [0, 1] (or the flow's x when logit_reverse=False).
         z: an optional [n, C, H, W] latent to invert instead of a fresh draw
         (eager path; used by the parity test)."""
+        self._check_weights()
         if z is not None:
             with torch.no_grad():
                 self.z.copy_(z)

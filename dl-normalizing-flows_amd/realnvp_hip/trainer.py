@@ -22,7 +22,6 @@ MI355X-specific structure:
     (train.py:139-154, 249-250 checkpoints).
 """
 import math
-import time
 
 import numpy as np
 import torch
@@ -54,6 +53,15 @@ def wn_table(engines, dtype, dev):
     from .engine import upload
     t = upload(bytes(tab), dev)
     return (t, len(descs), row0, tile0)
+
+
+def weights_key(engines, dtype):
+    """Identity of the packed-weight arenas of these couplings: changes when
+    a coupling's parameter storage moved (e.g. a FlowTrainer re-pointed the
+    parameters into its flat arena), which makes CouplingEngine.weights()
+    rebuild -- and free -- the arena a weight-norm table or a captured graph
+    points into."""
+    return tuple(e.weights(dtype)["key"] for e in engines)
 
 
 def wn_forward(table, dtype):
@@ -112,6 +120,8 @@ class FlowTrainer:
         if reduce_dtype not in ("fp32", "bf16"):
             raise ValueError("reduce_dtype must be 'fp32' or 'bf16'")
         self.comm, self.reduce_dtype = comm, reduce_dtype
+        self._reduce_pg = None
+        self._cap_pg = None
         self.comm_stream = None
         if self.pg is not None and comm == "overlap":
             self.comm_stream = torch.cuda.Stream(device=self.dev)
@@ -249,7 +259,34 @@ class FlowTrainer:
     def _reduce_bucket(self, lo, hi):
         """Average grad[lo:hi) over the process group (on the current stream)."""
         from .dist import average_slice
-        average_slice(self.grad, lo, hi, self.pg, self.reduce_buf)
+        pg = self._reduce_pg if self._reduce_pg is not None else self.pg
+        average_slice(self.grad, lo, hi, pg, self.reduce_buf)
+
+    def _capture_group(self):
+        """The process group the captured step all-reduces over.
+
+        RCCL's process group hands every eager collective to a watchdog
+        thread that polls the collective's completion event on the group's
+        communication stream until it retires it.  Inside a capture that
+        stream joins the graph, and an event poll on a capturing stream is a
+        fatal HIP error (it aborted the world-1 test twice in round 2, when a
+        warm-up all-reduce was still on the watchdog's list).  So the capture
+        uses a second group over the same ranks, created here, connected
+        eagerly (no collective) and used ONLY inside captures: its watchdog
+        list is empty by construction, and the warm-up group's stream never
+        captures.  Collectives issued while capturing are not handed to any
+        watchdog.  gloo (CPU tests) needs no second group."""
+        if self.pg is None or self.comm_stream is None:
+            return None
+        if getattr(self, "_cap_pg", None) is not None:
+            return self._cap_pg
+        import torch.distributed as dist
+        if dist.get_backend(self.pg) != "nccl":
+            return self.pg
+        ranks = dist.get_process_group_ranks(self.pg)
+        g = dist.new_group(ranks=ranks, backend="nccl")
+        g._get_backend(self.dev).eager_connect_single_device(self.dev)
+        return g
 
     def _add_coupling(self, mod, x):
         eng = mod.engine()
@@ -443,14 +480,9 @@ class FlowTrainer:
                 self.step_eager()
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
-        if self.pg is not None:
-            # the RCCL process group's watchdog thread polls the events of the
-            # warm-up all-reduces until it retires them (every ~100 ms); a poll
-            # that lands inside the capture is a fatal "operation not permitted
-            # when stream is capturing" (seen on the world-1 test), so let it
-            # retire the (already complete) work first.  Collectives issued
-            # during the capture are never handed to the watchdog.
-            time.sleep(0.5)
+        # the captured all-reduces go through a group of their own (see
+        # _capture_group); warm-up and eager collectives stay on self.pg
+        self._cap_pg = self._capture_group()
         self.graph = torch.cuda.CUDAGraph()
         self.graph_opt = None
         self.graph_input = self.external_input
@@ -459,9 +491,13 @@ class FlowTrainer:
         # hence the drain above)
         mode = "thread_local"
         if self.pg is None or self.comm_stream is not None:
-            with torch.cuda.graph(self.graph, capture_error_mode=mode):
-                self._fwd_bwd()
-                self._optimizer()
+            try:
+                self._reduce_pg = self._cap_pg
+                with torch.cuda.graph(self.graph, capture_error_mode=mode):
+                    self._fwd_bwd()
+                    self._optimizer()
+            finally:
+                self._reduce_pg = None
         else:
             with torch.cuda.graph(self.graph, capture_error_mode=mode):
                 self._fwd_bwd()
@@ -560,15 +596,29 @@ class FlowTrainer:
         if self.graph is not None:
             self.drop_graph()    # lr / betas are baked into the captured launches
 
+    def rng_state(self):
+        """The dequantisation noise stream: k_logit_fwd draws step t's noise
+        from Philox(seed, counter = t), so (seed, t) is the whole RNG state
+        (the reference saves none, train.py:249-250)."""
+        return {"seed": int(self.seed), "step": int(self.step_t.item())}
+
     def state_dict(self):
-        """{'model': model.state_dict(), 'optimizer': torch-Adam-format state}
-        (the two files train.py:249-250 writes)."""
-        return {"model": self.model.state_dict(), "optimizer": self.optimizer_state_dict()}
+        """{'model': model.state_dict(), 'optimizer': torch-Adam-format state,
+        'rng': rng_state()} (the two files train.py:249-250 writes, plus the
+        noise stream so a resumed run draws the same noise as an unbroken one)."""
+        return {"model": self.model.state_dict(), "optimizer": self.optimizer_state_dict(),
+                "rng": self.rng_state()}
 
     def load_state_dict(self, sd):
         with torch.no_grad():
             self.model.load_state_dict(sd["model"])
         self.load_optimizer_state_dict(sd["optimizer"])
+        rng = sd.get("rng")
+        if rng is not None:
+            if int(rng["seed"]) != self.seed:
+                self.seed = int(rng["seed"])
+                self.drop_graph()    # the seed is a captured launch argument
+            self.step_t.fill_(int(rng["step"]))
 
     def reset_optimizer(self):
         self.exp_avg.zero_()

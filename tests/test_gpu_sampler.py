@@ -58,3 +58,48 @@ def test_sampler_graph_replay_equals_eager_path():
     assert float((a - ref).abs().max()) < 1e-5
     with pytest.raises(RuntimeError):
         FlowSampler(model.train(), 4)
+
+
+def test_sampler_built_before_trainer_follows_moved_weights():
+    """a FlowSampler captured before a FlowTrainer re-points the
+    parameters into its flat arena (which makes the engines rebuild, and free,
+    their packed-weight arenas) rebuilds its weight-norm table and graph on
+    the next call instead of writing into freed memory; its samples then
+    match the eager inverse of the current weights."""
+    import utils
+    from realnvp_hip.sampler import FlowSampler
+    from realnvp_hip.trainer import FlowTrainer
+    model = make_model(32, 8, 1).eval()
+    s = FlowSampler(model, 8)
+    s.sample()
+    key0 = s._wkey
+    model.train()
+    tr = FlowTrainer(model, 4, dtype="fp32")
+    from formula_init import pixels
+    tr.set_pixels(pixels(4, 3, 32, seed=2).to(DEV))
+    tr.step()
+    model.eval()
+    model.set_precision(s.dtype)
+    a = s.sample().clone()
+    assert s._wkey != key0
+    with torch.no_grad():
+        ref, _ = utils.logit_transform(model.g(s.z.clone()), reverse=True)
+    assert float((a - ref).abs().max()) < 1e-5
+
+
+def test_reverse_without_no_grad_on_a_trainable_model():
+    """The reference's g() works without torch.no_grad() on a model whose
+    parameters require grad: the inverse runs detached with a
+    warning; an input that requires grad is refused."""
+    model = make_model(32, 8, 1).eval()
+    z = torch.randn(2, 3, 32, 32, device=DEV)
+    with pytest.warns(UserWarning):
+        import realnvp_hip.functions as F
+        F._REVERSE_WARNED[0] = False
+        x = model.g(z)
+    with torch.no_grad():
+        ref = model.g(z)
+    assert not x.requires_grad and torch.equal(x, ref)
+    mod = next(model.couplings())
+    with pytest.raises(RuntimeError):
+        mod(torch.randn(2, 3, 32, 32, device=DEV, requires_grad=True), reverse=True)

@@ -167,16 +167,19 @@ def _one_step(model, pg=None, graph=False, **kw):
     return tr, p0
 
 
+@pytest.mark.parametrize("side", [False, True], ids=["onestream", "sidestream"])
 @pytest.mark.parametrize("graph", [False, True], ids=["eager", "hipgraph"])
 @pytest.mark.parametrize("comm", ["overlap", "split"])
-def test_process_group_step_matches_single_process(nccl_world1, comm, graph):
+def test_process_group_step_matches_single_process(nccl_world1, comm, graph, side):
     """The DP step (bucketed all-reduce on the communication stream during
     backward, or between the captured graphs) with a world-size-1 RCCL group
     equals the single-process step: same gradients (up to the replica
-    atomics' summation order), same Adam update, same step counter."""
+    atomics' summation order), same Adam update, same step counter.  With
+    side=True the weight gradients run on the side stream and each bucket's
+    all-reduce waits for them through an event (trainer.py _backward)."""
     ref, p0 = _one_step(make_model(32, 8, 1))
     ref2, _ = _one_step(make_model(32, 8, 1))
-    tr, q0 = _one_step(make_model(32, 8, 1), pg=nccl_world1, graph=graph, comm=comm, bucket_mb=1)
+    tr, q0 = _one_step(make_model(32, 8, 1), pg=nccl_world1, graph=graph, comm=comm, bucket_mb=1, overlap=side)
     assert len(tr.buckets) > 1
     assert torch.equal(p0, q0)
 
@@ -288,7 +291,7 @@ def test_capture_restores_state_and_fixes_input_mode():
 # Each rank trains on its own batch shard; the all-reduced gradient must be
 # the mean of the two single-process gradients and both ranks must take the
 # same Adam step.
-def _dp_rank(rank, port, comm, out):
+def _dp_rank(rank, port, comm, out, side=False):
     import os
     import sys
     import torch.distributed as dist
@@ -299,7 +302,7 @@ def _dp_rank(rank, port, comm, out):
     dist.init_process_group("gloo", rank=rank, world_size=2)
     try:
         tr = FlowTrainer(make_model(32, 8, 1), 4, dtype="fp32", process_group=dist.group.WORLD, comm=comm,
-                         bucket_mb=1)
+                         bucket_mb=1, overlap=side)
         tr.set_pixels(pixels(4, 3, 32, seed=5 + rank).to(DEV))
         tr.step()
         torch.cuda.synchronize()
@@ -309,8 +312,9 @@ def _dp_rank(rank, port, comm, out):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("comm", ["split", "overlap"])
-def test_process_group_world2_matches_mean_of_shards(comm, tmp_path):
+@pytest.mark.parametrize("comm,side", [("split", False), ("overlap", False), ("overlap", True)],
+                         ids=["split", "overlap", "overlap-sidestream"])
+def test_process_group_world2_matches_mean_of_shards(comm, side, tmp_path):
     import socket
     import torch.multiprocessing as mp
     s = socket.socket()
@@ -319,7 +323,7 @@ def test_process_group_world2_matches_mean_of_shards(comm, tmp_path):
     s.close()
     outs = [str(tmp_path / ("rank%d.pt" % r)) for r in range(2)]
     ctx = mp.get_context("spawn")
-    procs = [ctx.Process(target=_dp_rank, args=(r, port, comm, outs[r])) for r in range(2)]
+    procs = [ctx.Process(target=_dp_rank, args=(r, port, comm, outs[r], side)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
@@ -353,3 +357,56 @@ def test_process_group_world2_matches_mean_of_shards(comm, tmp_path):
     assert float((res[0]["grad"] - mean).norm() / mean.norm()) < max(1e-4, 8 * floor)
     assert float((refs[0] - mean).norm() / mean.norm()) > 1e-2   # the shards really differ
     assert float((res[0]["param"] - p0).abs().max()) <= 2 * tr.lr * 1.01
+
+
+def test_checkpoint_carries_the_noise_stream():
+    """FlowTrainer.state_dict() holds the dequantisation RNG (seed, Philox
+    counter = step): a trainer built with another seed and resumed from the
+    checkpoint draws the same noise as the unbroken run, so its next step
+    (device logit_transform inside the step) is identical."""
+    from realnvp_hip.trainer import FlowTrainer
+    pix = pixels(4, 3, 32, seed=9).to(DEV)
+    ta = FlowTrainer(make_model(32, 8, 1), 4, dtype="fp32", seed=1234)
+    ta.set_pixels(pix)
+    for _ in range(2):
+        ta.step()
+    sd = ta.state_dict()
+    assert sd["rng"] == {"seed": 1234, "step": 2}
+    tb = FlowTrainer(make_model(32, 8, 1), 4, dtype="fp32", seed=7)
+    tb.load_state_dict(sd)
+    assert tb.seed == 1234 and int(tb.step_t.item()) == 2
+    tb.set_pixels(pix)
+    for t in (ta, tb):
+        t.reset_metrics()
+        t.step()
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(tb.mean_logll(1), ta.mean_logll(1), rtol=1e-6)
+    assert torch.equal(tb.xl, ta.xl)    # the same noise was drawn
+    assert float((tb.param - ta.param).abs().max()) <= 2 * ta.lr * 1.01
+
+
+def test_dropin_backward_between_trainer_steps():
+    """the drop-in autograd path and the trainer share a coupling's
+    backward scratch (same batch shape).  A drop-in forward/backward between
+    two trainer steps must leave that scratch zero: the second trainer step
+    then has the same gradient as a run without the drop-in call."""
+    from realnvp_hip.trainer import FlowTrainer
+    res = []
+    for dropin in (False, False, True):
+        model = make_model(32, 8, 1)
+        tr = FlowTrainer(model, 4, dtype="fp32")
+        x, ld = _batch(0)
+        tr.set_input(x, ld)
+        tr.step()
+        if dropin:
+            lp, ws = model(x)
+            (-(lp + ld).mean() + 5e-5 * ws).backward()
+            model.zero_grad(set_to_none=True)
+        tr.step()
+        torch.cuda.synchronize()
+        res.append(tr.grad.clone())
+    g0, g1, g2 = res
+
+    def d(a, b):
+        return float((a - b).norm() / b.norm())
+    assert d(g2, g0) < max(1e-4, 8 * d(g1, g0)), (d(g2, g0), d(g1, g0))
