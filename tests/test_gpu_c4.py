@@ -1,0 +1,110 @@
+"""BASELINE config 4 at its real width: 128x128x3, 6 scales (the reference's
+5-scale hard-coding generalised, /root/reference/flow_realnvp.py:46-95, with
+the base dim doubling per scale as at :57-59), base dim 64, so scale 6 runs
+2048-channel convs at 4x4 -- beyond the deep conv family's 1024-channel
+table, on the generic dispatch (kernel-level cases: tests/test_gpu_conv.py
+c4_*, tests/test_gpu_deep.py c4_s6_* weight gradients).
+
+  * the full model (R4, 1.886 B parameters): one graph-captured bf16 trainer
+    step at the per-GPU batch of 256 -- finite loss, every gradient finite
+    and non-zero where trainable;
+  * the same model in fp32 eval mode: g(f(x)) reconstructs x to 1e-5
+    normwise (B = 2);
+  * the narrowest model that still routes through the 2048-channel dispatch
+    (D64, R1, B = 2): train-mode log-prob against the CPU oracle to 1e-5.
+"""
+import numpy as np
+import pytest
+import torch
+
+from formula_init import formula_state, formula_value, pixels, uniform_noise
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+SIZE, N_SCALES, BASE_DIM = 128, 6, 64
+
+
+def build(res_blocks, formula=False):
+    import flow_realnvp
+    import utils
+    torch.manual_seed(0)
+    prior = torch.distributions.Normal(torch.tensor(0.0, device=DEV), torch.tensor(1.0, device=DEV),
+                                       validate_args=False)
+    hp = utils.Hyperparameters(BASE_DIM, res_blocks, True, True, True, True)
+    with torch.device(DEV):
+        m = flow_realnvp.RealNVP(3, SIZE, prior, hp, n_scales=N_SCALES)
+    if formula:
+        m.load_state_dict(formula_state(m, device=DEV))
+    return m
+
+
+def inputs(B):
+    import utils
+    return utils.logit_transform(pixels(B, 3, SIZE, seed=21).to(DEV), noise=uniform_noise(B, 3, SIZE, seed=22).to(DEV))
+
+
+@pytest.fixture(scope="module")
+def c4_model():
+    m = build(4)
+    mid6 = max(mod.mid_dim for mod in m.couplings())
+    assert mid6 == 2048
+    n = sum(p.numel() for p in m.parameters() if p.requires_grad)
+    assert n == 1_885_361_634, n     # config 4's trainable parameters
+    yield m
+    del m
+    torch.cuda.empty_cache()
+
+
+def test_c4_bf16_trainer_step_full_batch(c4_model):
+    from realnvp_hip.trainer import FlowTrainer
+    model = c4_model.train()
+    B = 256
+    tr = FlowTrainer(model, B, dtype="bf16")
+    tr.set_pixels(pixels(B, 3, SIZE, seed=3).to(DEV))
+    tr.capture(warmup=1)
+    tr.reset_metrics()
+    tr.step()
+    torch.cuda.synchronize()
+    ll = tr.mean_logll(1)
+    assert np.isfinite(ll)
+    bpd = tr.bits_per_dim(ll)
+    assert 3.0 < bpd < 14.0, bpd
+    # the step's gradient arena (the graph zeroes it at the start of the step)
+    assert bool(torch.isfinite(tr.grad).all())
+    trainable = tr.mask > 0
+    frac_nz = float((tr.grad[trainable] != 0).float().mean())
+    assert frac_nz > 0.5, frac_nz
+    assert bool(torch.isfinite(tr.param).all())
+    del tr
+    torch.cuda.empty_cache()
+
+
+def test_c4_fp32_eval_reconstruction(c4_model):
+    model = c4_model.eval()
+    model.set_precision("fp32")
+    x, _ = inputs(2)
+    with torch.no_grad():
+        z, _ = model.f(x)
+        xr = model.g(z)
+    err = float((xr - x).norm() / x.norm())
+    assert err < 1e-5, err
+
+
+def test_c4_narrow_train_logprob_vs_oracle():
+    """D64 / R1: every scale's widths of config 4 (scale 6 at 2048 channels)
+    with one residual block per net -- the narrowest model that takes the
+    2048-channel dispatch -- against the oracle's generalised 6-scale flow."""
+    import realnvp_oracle as O
+    model = build(1, formula=True).train()
+    model.set_precision("fp32")
+    assert max(mod.mid_dim for mod in model.couplings()) == 2048
+    x, logdet = inputs(2)
+    with torch.no_grad():
+        lp, _ = model(x)
+    spec = O.FlowSpec(3, SIZE, O.HP(BASE_DIM, 1), n_scales=N_SCALES)
+    S = O.build_state(O.flow_spec_entries(spec), formula_value)
+    with torch.no_grad():
+        lpo = O.log_prob(S, spec, x.cpu(), training=True)
+    np.testing.assert_allclose(lp.cpu().numpy(), lpo.numpy(), rtol=1e-5)
+    del model
+    torch.cuda.empty_cache()

@@ -33,7 +33,11 @@ def bf16_round(t):
 
 
 def run_case(B, H, W, cin, cout, ks, dtype, pro=False, residual=False, acc=False, stats=False, dgrad=False,
-             bias=True, variant=0, seed=0):
+             bias=True, variant=0, seed=0, rows=None):
+    """rows: compute the float64 reference only at these output pixels
+    (config 4's M = 2^22 shapes, whose full float64 conv is too slow on the
+    host); the statistics are then checked against the float64 sums of the
+    kernel's own output (the epilogue reduction), the values row by row."""
     from realnvp_hip import _lib
     from realnvp_hip._lib import BNSrc, ConvArgs
     from realnvp_hip.engine import splitk_workspace, stat_shards
@@ -46,11 +50,13 @@ def run_case(B, H, W, cin, cout, ks, dtype, pro=False, residual=False, acc=False
     x = torch.randn(M, cin, generator=g, dtype=torch.float64)
     w = torch.randn(cout, ks, ks, cin, generator=g, dtype=torch.float64) / np.sqrt(ks * ks * cin)
     bvec = torch.randn(cout, generator=g, dtype=torch.float64) if bias else torch.zeros(cout, dtype=torch.float64)
-    res = torch.randn(M, cout, generator=g, dtype=torch.float64)
-    yold = torch.randn(M, cout, generator=g, dtype=torch.float64)
-    ex = torch.randn(M, cout, generator=g, dtype=torch.float64)
     rnd = (lambda t: t.float().double()) if dtype == "fp32" else bf16_round
-    x, w, res, yold, ex, bvec = rnd(x), rnd(w), rnd(res), rnd(yold), rnd(ex), bvec.float().double()
+    # operands the flags do not use are not drawn (config 4's M = 2^22 cases)
+    zero = torch.zeros(1, cout, dtype=torch.float64)
+    res = rnd(torch.randn(M, cout, generator=g, dtype=torch.float64)) if residual else zero
+    yold = rnd(torch.randn(M, cout, generator=g, dtype=torch.float64)) if acc else zero
+    ex = rnd(torch.randn(M, cout, generator=g, dtype=torch.float64)) if dgrad else zero
+    x, w, bvec = rnd(x), rnd(w), bvec.float().double()
 
     def nhwc(t, cs):
         out = torch.zeros(t.shape[0], cs, dtype=tdt)
@@ -65,7 +71,7 @@ def run_case(B, H, W, cin, cout, ks, dtype, pro=False, residual=False, acc=False
             wp[:, base:base + cin] = w[:, ky, kx, :].to(tdt)
     dx, dw = nhwc(x, csi), wp.to(DEV)
     dy = nhwc(yold, cso) if acc else torch.zeros(M, cso, dtype=tdt, device=DEV)
-    dres, dex = nhwc(res, cso), nhwc(ex, cso)
+    dres, dex = nhwc(res, cso), nhwc(ex, cso)      # 1-row placeholders when unused
     db = bvec.float().to(DEV)
 
     # BN statistics for the prologue / dgrad epilogue, as sharded fp64 sums
@@ -123,23 +129,40 @@ def run_case(B, H, W, cin, cout, ks, dtype, pro=False, residual=False, acc=False
     assert torch.count_nonzero(full[:, cout:]) == 0, "channel padding must stay zero"
 
     # float64 reference
-    a4 = act.reshape(B, H, W, cin).permute(0, 3, 1, 2)
-    w4 = w.permute(0, 3, 1, 2)
-    ref = torch.nn.functional.conv2d(a4, w4, bias=bvec, padding=ks // 2).permute(0, 2, 3, 1).reshape(M, cout)
+    if rows is None:
+        a4 = act.reshape(B, H, W, cin).permute(0, 3, 1, 2)
+        w4 = w.permute(0, 3, 1, 2)
+        ref = torch.nn.functional.conv2d(a4, w4, bias=bvec, padding=ks // 2).permute(0, 2, 3, 1).reshape(M, cout)
+        sel = slice(None)
+    else:
+        sel = rows
+        pb, rem = rows // (H * W), rows % (H * W)
+        py, px = rem // W, rem % W
+        ref = bvec.view(1, -1).expand(len(rows), cout).clone()
+        for ky in range(ks):
+            for kx in range(ks):
+                yy, xx = py + ky - ks // 2, px + kx - ks // 2
+                ok = (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W)
+                src = (pb * H + yy.clamp(0, H - 1)) * W + xx.clamp(0, W - 1)
+                ref = ref + (act[src] * ok.view(-1, 1).double()) @ w[:, ky, kx, :].T
     if residual:
-        ref = ref + res
+        ref = ref + res[sel]
     if acc:
-        ref = ref + yold
+        ref = ref + yold[sel]
     s1 = s2 = None
+    out = ref if rows is None else got
     if dgrad:
         escale = (egam * erstd).float().double()
         eshift = (ebet - emean.float().double() * egam * erstd).float().double()
-        ref = ref * ((ex * escale + eshift) > 0)
+        ref = ref * ((ex[sel] * escale + eshift) > 0)
+        out = ref if rows is None else got
         xhat = (ex - emean.float().double()) * erstd
-        s1, s2 = ref.sum(0), (ref * xhat).sum(0)
+        s1, s2 = out.sum(0), (out * xhat).sum(0)
     elif stats:
-        s1, s2 = ref.sum(0), (ref * ref).sum(0)
+        s1, s2 = out.sum(0), (out * out).sum(0)
     sums = osums.sum(0).cpu() if (stats or dgrad) else None
+    if rows is not None:
+        got = got[rows]
     return got, ref, sums, s1, s2
 
 
@@ -180,7 +203,48 @@ CASES = [
     ("c1_full_3x3_dgrad", 64, 64, 64, 32, 32, 3, dict(dgrad=True, residual=True, acc=True, bias=False)),
     ("c1_full_1x1_dgrad", 64, 64, 64, 32, 32, 1, dict(dgrad=True, bias=False)),
     ("c1_full_in_dgrad", 64, 64, 64, 32, 7, 3, dict(bias=False)),
+    # config 4's widest convs: scale 6 of the 128x128 / 6-scale / D64 flow, mid
+    # 2048 at 4x4 (beyond the deep family's 1024-channel table: generic path)
+    ("c4_s6_3x3_pro_stats", 16, 4, 4, 2048, 2048, 3, dict(pro=True, stats=True, bias=False)),
+    ("c4_s6_3x3_plain", 16, 4, 4, 2048, 2048, 3, dict(stats=True, bias=False)),
+    ("c4_s6_1x1_pro_res", 16, 4, 4, 2048, 2048, 1, dict(pro=True, residual=True, stats=True)),
+    ("c4_s6_1x1_plain", 16, 4, 4, 2048, 2048, 1, dict(stats=True)),
+    ("c4_s6_skip_acc", 16, 4, 4, 2048, 2048, 1, dict(acc=True, stats=True)),
+    ("c4_s6_3x3_dgrad", 16, 4, 4, 2048, 2048, 3, dict(dgrad=True, bias=False)),
+    ("c4_s6_1x1_dgrad_res", 16, 4, 4, 2048, 2048, 1, dict(dgrad=True, residual=True, bias=False)),
+    ("c4_s6_3x3_plain_dgrad", 16, 4, 4, 2048, 2048, 3, dict(bias=False)),
+    ("c4_s6_in_3x3", 16, 4, 4, 193, 2048, 3, dict(stats=True)),
+    ("c4_s6_out_1x1", 16, 4, 4, 2048, 192, 1, dict(pro=True)),
+    ("c4_s6_1x1_full_batch", 256, 4, 4, 2048, 2048, 1, dict(pro=True, stats=True)),
 ]
+
+# config 4 scale 1 at its per-GPU batch (B = 256, 128 x 128: M = 2^22), mid 64;
+# float64 reference on 4,096 sampled output pixels (run_case rows=)
+C4_S1 = [
+    ("c4_s1_in_3x3", 256, 128, 128, 7, 64, 3, dict(stats=True)),
+    ("c4_s1_3x3_pro_stats", 256, 128, 128, 64, 64, 3, dict(pro=True, stats=True, bias=False)),
+    ("c4_s1_1x1_pro_res", 256, 128, 128, 64, 64, 1, dict(pro=True, residual=True, stats=True)),
+    ("c4_s1_skip_acc", 256, 128, 128, 64, 64, 1, dict(acc=True, stats=True)),
+    ("c4_s1_out_1x1", 256, 128, 128, 64, 6, 1, dict(pro=True)),
+    ("c4_s1_3x3_dgrad", 256, 128, 128, 64, 64, 3, dict(dgrad=True, residual=True, acc=True, bias=False)),
+    ("c4_s1_1x1_dgrad", 256, 128, 128, 64, 64, 1, dict(dgrad=True, bias=False)),
+]
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("case", C4_S1, ids=[c[0] for c in C4_S1])
+def test_conv_c4_scale1_sampled(case, dtype):
+    name, B, H, W, cin, cout, ks, fl = case
+    M = B * H * W
+    rows = torch.from_numpy(np.random.default_rng(7).choice(M, 4096, replace=False)).long()
+    rows = torch.cat([rows, torch.tensor([0, W - 1, M - W, M - 1])])   # image corners (padding taps)
+    got, ref, sums, s1, s2 = run_case(B, H, W, cin, cout, ks, dtype, rows=rows, **fl)
+    tol = 1e-5 if dtype == "fp32" else 4e-3
+    assert rel(got, ref) < tol, rel(got, ref)
+    if s1 is not None:     # the epilogue's sums against the float64 sums of its own output
+        stol = 1e-5 if dtype == "fp32" else 10 * tol    # bf16: sums of the unrounded values
+        assert rel(sums[0], s1) < stol, rel(sums[0], s1)
+        assert rel(sums[1], s2) < stol, rel(sums[1], s2)
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])

@@ -54,6 +54,13 @@ def model_inputs(B, size):
     return x_in, logdet
 
 
+def make_model_chirp(size, bd, rb):
+    """formula init with full-rank (chirp) weights, as tools/make_bf16_golden.py"""
+    m = make_model(size, bd, rb)
+    m.load_state_dict(formula_state(m, style="chirp"))
+    return m
+
+
 def make_model(size, bd, rb, n_scales=5, device_init=False):
     import flow_realnvp
     prior = torch.distributions.Normal(torch.tensor(0.0, device=DEV), torch.tensor(1.0, device=DEV),
@@ -246,18 +253,56 @@ def test_trainer_config1_full_batch_fp32():
 
 
 def test_trainer_config1_full_batch_bf16():
-    """bf16 s/t network (bf16 operands and stored activations / activation
-    gradients, fp32 accumulation; fp32 couplings, log-det, BN statistics) at
-    the benchmarked batch against the fp32 reference.  Measured: per-sample
-    log-prob within 1.1e-3, per-tensor gradient-norm vector 0.37 off.  The
-    gradient gap is the precision of bf16 activations through 28 batch-stat
-    couplings, not a kernel error: the fp32 CPU oracle with the same
-    roundings emulated by torch (tools/bf16_emulation.py: bf16 conv operands /
-    outputs / output gradients) lands 0.28 from fp32 at this config (B=16), and the kernels
-    themselves are checked in bf16 against fp64 in test_gpu_conv.  Bounds:
-    2e-3 on log-prob, 0.5 on the norm vector."""
-    lp_err, g_err = _trainer_step_check("bf16", 2e-3, 0.5)
-    print("bf16 B=64: max log-prob rel err %.3g, grad-norm vector rel err %.3g" % (lp_err, g_err))
+    """The benchmarked step itself (config 1, B = 64, bf16 s/t net) pinned to
+    a bf16-faithful CPU golden (tools/make_bf16_golden.py): the oracle with
+    the engine's bf16 rounding points (stored conv outputs, packed operands
+    and weights, stored activation gradients), computed twice with different
+    conv summation orders (fp32 vs fp64-accumulated), beside the fp32 oracle.
+    The model has full-rank weights (formula init, chirp style).
+
+    The three CPU references are as far from each other as bf16 itself
+    scatters (measured: per-sample log-prob L2 1.7e-4 / max 4.2e-4, mean
+    3.5e-5; per-tensor gradient-norm vector 0.023, per-tensor 90th percentile
+    0.066): two correct bf16 implementations differ by that floor.  The HIP
+    step must land within 3x the floor of EACH reference.  (Against the
+    round-2 bound -- 2e-3 log-prob, 0.5 norm vector on rank-2 weights -- the
+    norm-vector bound is 7x tighter; a kernel error of a few percent in any
+    large gradient tensor moves the vector past it.)"""
+    from realnvp_hip.trainer import FlowTrainer
+    g = load_golden("bf16emu_model_m64_d32_r4_b64.npz")
+    refs = ("fp32", "emu", "emu_wide")
+    model = make_model_chirp(64, 32, 4)
+    tr = FlowTrainer(model, 64, dtype="bf16")
+    x, logdet = model_inputs(64, 64)
+    tr.set_input(x.to(DEV), logdet.to(DEV))
+    p0 = tr.param.clone()
+    ws = sum(float(p.detach().double().pow(2).sum()) for n, p in model.named_parameters()
+             if p.requires_grad and n.split(".")[-1] in ("weight_g", "scale"))
+    tr.step_eager()
+    torch.cuda.synchronize()
+    lp = tr.lp.double().cpu().numpy()
+    loss = -tr.mean_logll(1) + 5e-5 * ws
+    grad = tr.grad + (tr.mask == 2).float() * (2 * 5e-5) * p0
+    names = list(g["grad_names"])
+    sizes = {n: p.numel() for n, p in model.named_parameters()}
+    norms = np.array([float(grad[tr.offsets[n]:tr.offsets[n] + sizes[n]].double().norm()) for n in names])
+
+    def metrics(lp_a, loss_a, n_a, lp_b, loss_b, n_b):
+        big = n_b > 1e-4 * np.linalg.norm(n_b)
+        per = np.abs(n_a[big] - n_b[big]) / n_b[big]
+        return np.array([rel(lp_a, lp_b), np.max(np.abs(lp_a - lp_b) / np.abs(lp_b)),
+                         abs(loss_a - loss_b) / abs(loss_b), rel(n_a, n_b), np.percentile(per, 90)])
+    floor = np.max([metrics(g[a + "_logprob"], float(g[a + "_loss"]), g[a + "_grad_norms"],
+                            g[b + "_logprob"], float(g[b + "_loss"]), g[b + "_grad_norms"])
+                    for a in refs for b in refs if a != b], axis=0)
+    labels = ("log-prob L2", "log-prob max", "loss", "grad-norm vector", "per-tensor p90")
+    for r in refs:
+        m = metrics(lp, loss, norms, g[r + "_logprob"], float(g[r + "_loss"]), g[r + "_grad_norms"])
+        print("HIP bf16 vs %-8s " % r + "  ".join("%s %.3g (floor %.3g)" % (k, v, f)
+                                                  for k, v, f in zip(labels, m, floor)))
+        # the loss floor is a difference of near-equal means: floor it at 1e-4
+        bound = 3 * np.maximum(floor, [0, 0, 1e-4, 0, 0])
+        assert np.all(m < bound), (r, dict(zip(labels, m)), dict(zip(labels, bound)))
 
 
 # ---------------------------------------------------------------------------
@@ -370,6 +415,10 @@ WGRAD_CASES = [
     ("s4_256_3x3", 16, 8, 8, 256, 256, 3, True),
     ("s5_512_1x1", 64, 4, 4, 512, 512, 1, False),
     ("ragged_128", 4, 16, 16, 136, 200, 3, True),
+    # config 4's widest nets (scale 6: mid 2048 at 4x4; in-conv 193 -> 2048)
+    ("c4_s6_2048_1x1", 16, 4, 4, 2048, 2048, 1, True),
+    ("c4_s6_2048_3x3", 16, 4, 4, 2048, 2048, 3, True),
+    ("c4_s6_in_193", 16, 4, 4, 193, 2048, 3, False),
 ]
 
 
@@ -377,8 +426,6 @@ WGRAD_CASES = [
 @pytest.mark.parametrize("case", WGRAD_CASES, ids=[c[0] for c in WGRAD_CASES])
 def test_grouped_wgrad_vs_torch(case, dtype):
     name, B, H, W, cin, cout, ks, pro = case
-    if name.startswith("m_") and dtype == "fp32":
-        pytest.skip("large-M cases run in bf16 (the mode config 4 trains in)")
     got, ref, gotb, refb = _wgrad_case(B, H, W, cin, cout, ks, dtype, pro)
     tol = 1e-5 if dtype == "fp32" else 1e-4
     assert rel(got.cpu(), ref.cpu()) < tol, rel(got.cpu(), ref.cpu())
