@@ -69,6 +69,13 @@ def parse():
                         "launch (for rocprofv3 --pmc passes, tools/pmc_traffic.py)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="per-family PMC HBM bytes per launch (tools/pmc_traffic.py output) for roofline.traffic")
+    p.add_argument("--mfma", default=os.path.join(ROOT, "profiles", "pmc_mfma.json"),
+                   help="per-family MFMA busy %% (tools/pmc_mfma.py output) for roofline.mfma_busy_pct")
+    p.add_argument("--rocprof-families", default=os.path.join(ROOT, "profiles", "rocprof_families.json"),
+                   help="per-family rocprof durations of the graph-replayed step (tools/trace_families.py output)")
+    p.add_argument("--graph-markers", default=None,
+                   help="capture a marker dispatch around every engine launch INTO the step graph and write the "
+                        "families here (for a rocprofv3 kernel trace split by family, tools/trace_families.py)")
     a = p.parse_args()
     cfg = CONFIGS[a.config]
     for k in ("batch", "size", "res_blocks", "base_dim"):
@@ -86,7 +93,16 @@ def synthetic_pixels(B, C, S, seed):
     return torch.from_numpy((k / 255.0).astype(np.float32))
 
 
-def kernel_roofline(trainer, markers=None, traffic=None, config=None):
+def _load_for(path, config):
+    """a profiles/*.json family table, if it was measured on this config"""
+    if path and os.path.exists(path):
+        t = json.load(open(path))
+        if t.get("config") == config:
+            return t.get("families", {})
+    return {}
+
+
+def kernel_roofline(trainer, markers=None, traffic=None, config=None, mfma=None, rocprof=None):
     """One instrumented eager step: HIP events around every engine launch
     (recorded on the launch stream).  Returns per-family totals and the
     roofline object of the dominant (largest total time) family.  `traffic`
@@ -132,15 +148,30 @@ def kernel_roofline(trainer, markers=None, traffic=None, config=None):
     roof.update(kernel=dom, launches_per_step=d["launches"], avg_launch_us=round(avg_ms * 1e3, 2),
                 alg_bytes_per_launch=int(bytes_per_launch), flops_per_launch=int(flops_per_launch),
                 traffic=None)
-    if traffic and os.path.exists(traffic):
-        t = json.load(open(traffic))
-        row = t.get("families", {}).get(dom)
-        if t.get("config") == config and row:
-            roof["traffic"] = row["traffic_per_launch"]
-            roof["traffic_source"] = "PMC 2*FETCH_SIZE+WRITE_SIZE, %s" % os.path.relpath(traffic, ROOT)
+    row = _load_for(traffic, config).get(dom)
+    if row:
+        roof["traffic"] = row["traffic_per_launch"]
+        roof["traffic_source"] = "PMC 2*FETCH_SIZE+WRITE_SIZE, %s" % os.path.relpath(traffic, ROOT)
+    mf = _load_for(mfma, config)
+    if dom in mf:
+        roof["mfma_busy_pct"] = mf[dom]["mfma_busy_pct"]
+        roof["mfma_source"] = "PMC SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs), %s" % (
+            os.path.relpath(mfma, ROOT))
+    rp = _load_for(rocprof, config)
+    if dom in rp:
+        # the same family's mean duration in the graph-replayed step (rocprof);
+        # avg_launch_us above is HIP events around each launch of an eager step
+        roof["rocprof_avg_launch_us"] = rp[dom]["avg_launch_us"]
+        roof["rocprof_achieved"] = round(bytes_per_launch / (rp[dom]["avg_launch_us"] * 1e-6) / 1e9, 1)
+        roof["rocprof_source"] = os.path.relpath(rocprof, ROOT)
     families = {k: dict(ms=round(v["ms"], 3), launches=v["launches"],
                         gbs=round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1),
                         tflops=round(v["flops"] / max(v["ms"], 1e-9) / 1e9, 2)) for k, v in fam.items()}
+    for k, v in families.items():
+        if k in mf:
+            v["mfma_busy_pct"] = mf[k]["mfma_busy_pct"]
+        if k in rp:
+            v["rocprof_ms"] = rp[k]["total_ms"]
     return roof, families
 
 
@@ -274,6 +305,52 @@ def secondary(args, dev):
     return out
 
 
+def dp_diagnostics(tr, pg, step_s, dev):
+    """What an 8-GPU run needs to be read: the world size RCCL reports, every
+    rank's own step time, and the gradient all-reduce time -- inside an eager
+    instrumented step (events on the communication stream around each bucket)
+    and in isolation for both wire dtypes (the bucket plan over the gradient
+    arena, back to back on one stream)."""
+    import torch.distributed as dist
+    from realnvp_hip.dist import average_slice
+    world = dist.get_world_size(pg)
+    t = torch.tensor([step_s * 1e3], dtype=torch.float64, device=dev)
+    ranks = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(ranks, t, group=pg)
+    out = dict(world_size_rccl=world, backend=dist.get_backend(pg),
+               rank_ms_per_step=[round(float(r.item()), 3) for r in ranks],
+               buckets=len(tr.buckets), bucket_mb=round(tr.bucket_elems * 4 / 2 ** 20, 1),
+               reduce_dtype=tr.reduce_dtype, comm=tr.comm)
+    if tr.comm_stream is not None:
+        tr.comm_events = []
+        torch.cuda.synchronize()
+        tr.step_eager()
+        torch.cuda.synchronize()
+        ev = tr.comm_events
+        tr.comm_events = None
+        out["allreduce_ms_in_step"] = round(sum(e0.elapsed_time(e1) for _, e0, e1 in ev), 3)
+    iso = {}
+    for rd in ("fp32", "bf16"):
+        buf = torch.empty(tr.n, device=dev, dtype=torch.bfloat16) if rd == "bf16" else None
+        g = torch.zeros_like(tr.grad)
+        for rep in range(3):
+            dist.barrier(group=pg)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for lo, hi, _ in tr.buckets:
+                average_slice(g, lo, hi, pg, buf)
+            e1.record()
+            e1.synchronize()
+        ms = e0.elapsed_time(e1)
+        nbytes = tr.n * (2 if rd == "bf16" else 4)
+        # ring all-reduce moves 2 (N-1)/N of the buffer through every rank's links
+        iso[rd] = dict(ms=round(ms, 3), bus_gbs=round(2 * (world - 1) / world * nbytes / (ms * 1e-3) / 1e9, 1))
+        del g, buf
+    out["allreduce_isolated"] = iso
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -282,11 +359,21 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus %d needs torch.distributed.run --nproc-per-node %d" % (args.gpus, args.gpus))
+    # RNVP_BENCH_BACKEND=gloo: a rehearsal of the multi-rank path on a box with
+    # fewer GPUs than ranks (ranks share devices round-robin; eager only, as
+    # gloo collectives cannot be captured).  The driver's runs use RCCL.
+    backend = os.environ.get("RNVP_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % torch.cuda.device_count()
+        args.no_graph = True
     torch.cuda.set_device(local)
     pg = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
         pg = dist.group.WORLD
 
     from realnvp_hip.dist import max_over_ranks, mean_over_ranks, rank_seed
@@ -298,8 +385,21 @@ def main():
                      overlap=args.overlap, comm=args.comm, reduce_dtype=args.reduce_dtype)
     tr.set_pixels(synthetic_pixels(args.batch, 3, args.size, seed=rank_seed(0, rank)).to(dev))
 
+    cfg_key = dict(size=args.size, res_blocks=args.res_blocks, base_dim=args.base_dim, batch=args.batch,
+                   dtype=args.dtype)
     if not args.no_graph:
-        tr.capture(warmup=2)
+        before = None
+        if args.graph_markers:
+            from realnvp_hip import engine as E
+
+            def before():
+                E.MARKERS = True
+                E.MARKER_FAMILIES = []
+        tr.capture(warmup=2, before_capture=before)
+        if args.graph_markers:
+            E.MARKERS = False
+            if rank == 0:
+                json.dump(dict(config=cfg_key, families=E.MARKER_FAMILIES), open(args.graph_markers, "w"))
 
     def barrier():
         if pg is not None:
@@ -317,9 +417,9 @@ def main():
     bpd = tr.bits_per_dim(mean_ll)
     imgs = world * args.batch * args.steps
     value = imgs / dt
-    cfg_key = dict(size=args.size, res_blocks=args.res_blocks, base_dim=args.base_dim, batch=args.batch,
-                   dtype=args.dtype)
-    roof, fams = kernel_roofline(tr, args.pmc_markers if rank == 0 else None, args.traffic, cfg_key)
+    dp = dp_diagnostics(tr, pg, dt / args.steps, dev) if pg is not None else None
+    roof, fams = kernel_roofline(tr, args.pmc_markers if rank == 0 else None, args.traffic, cfg_key, args.mfma,
+                                 args.rocprof_families)
     alg_bytes = CONFIGS[args.config]["alg_bytes"]
     label = CONFIGS[args.config]["label"]
     if args.custom:
@@ -352,6 +452,8 @@ def main():
             "kernel_families": fams,
             "cpu_baseline": None,
         }
+        if dp is not None:
+            out["dp"] = dp
     del tr, model
     torch.cuda.empty_cache()
     if rank == 0 and world == 1:

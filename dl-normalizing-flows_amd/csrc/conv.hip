@@ -1817,6 +1817,23 @@ extern "C" int rnvp_conv2d_wgrad_grouped(const rnvp_wgrad_group* gin, void* stre
     if (gin->dtype != RNVP_F32 && gin->dtype != RNVP_BF16) return RNVP_E_INVALID;
     if (gin->B < 0 || gin->H <= 0 || gin->W <= 0) return RNVP_E_INVALID;
     if (gin->B == 0) return RNVP_OK;
+    // bf16: the tap-shared kernel (wgrad_tap.hip) where it applies;
+    // RNVP_WGRAD=0 forces the per-tap kernel below (A/B diagnostics)
+    static const int wmode = [] { const char* e = getenv("RNVP_WGRAD"); return e ? atoi(e) : 1; }();
+    if (wmode == 1 && gin->dtype == RNVP_BF16) {
+        for (int c = 0; c < gin->n_conv; ++c) {
+            const rnvp_wgrad_conv& v = gin->conv[c];
+            if (!v.x || !v.dy || !v.ws) return RNVP_E_INVALID;
+            if (v.ks != 1 && v.ks != 3) return RNVP_E_UNSUPPORTED;
+            if (v.n <= 0 || v.cin <= 0 || v.nz <= 0 || v.nrep <= 0 || v.nrep > v.nz) return RNVP_E_INVALID;
+            if ((v.cs_in & 7) || (v.cs_dy & 7) || v.cs_in < v.cin || v.cs_dy < v.n) return RNVP_E_INVALID;
+            if (v.kp < v.ks * v.ks * v.cs_in) return RNVP_E_INVALID;
+            if (!al16(v.x) || !al16(v.dy)) return RNVP_E_INVALID;
+        }
+        rnvp_wgrad_group gt = *gin;
+        const int rc = rnvp_wgrad_tap_launch(&gt, (hipStream_t)stream);
+        if (rc != RNVP_E_UNSUPPORTED) return rc;
+    }
     rnvp_wgrad_group g = *gin;
     const long long M = (long long)g.B * g.H * g.W;
     const int STG = g.dtype == RNVP_BF16 ? 64 : 32;

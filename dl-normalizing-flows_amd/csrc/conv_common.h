@@ -220,3 +220,7 @@ __device__ __forceinline__ int fdiv_exact(int q, int d, float r) {
 constexpr int RNVP_DEEP_CFGS = 4;
 int rnvp_deep_launch(const rnvp_conv_args* a, hipStream_t s, int cfg);
 int rnvp_deep_auto_cfg(const rnvp_conv_args* a);
+
+// tap-shared bf16 weight gradients (wgrad_tap.hip): RNVP_E_UNSUPPORTED when a
+// conv of the group is outside its staging limits (the caller falls back)
+int rnvp_wgrad_tap_launch(rnvp_wgrad_group* g, hipStream_t s);

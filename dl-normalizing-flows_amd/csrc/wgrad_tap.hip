@@ -1,0 +1,405 @@
+// Grouped weight gradients of one coupling's s/t-net convs, bf16, tap-shared
+// (modules_realnvp.py:36-71 WeightNormConv2d backward, for every conv of a
+// ResidualModule in one launch).
+//
+//   dW[co][t*cs_in + ci] = sum_p dy[p][co] * act(x)[p + off(t)][ci]     (+ bias: sum_p dy[p][co])
+//
+// The round-2 kernel (conv.hip k_wgrad_grouped) gave every tap of a 3x3 its own
+// 64x64 (co x k) tile: the activation rows were re-read, re-decoded and
+// re-transformed (BN+ReLU) once per tap and per co tile, and each 64-pixel
+// stage cost ~350 VALU instructions against 8 MFMAs (PMC: 4.7 % MFMA busy).
+// Here a workgroup owns a (co tile) x (ci tile) x ALL taps block:
+//   * per stage of 128 output pixels (whole image rows) the dy rows and the
+//     activation rows + halo are staged ONCE in LDS, the activations BN+ReLU'd
+//     once and laid out as zero-padded image rows ((W+2) columns, a zero row
+//     above and below every image): every tap reads its operand at a fixed
+//     row offset with no border masks;
+//   * MFMA operands come from LDS by ds_read_b64_tr_b16 (8 pixels of one
+//     channel per lane), one A fragment (dy^T) serving all 9 taps;
+//   * the next stage's global loads are in flight under the current stage's
+//     MFMAs (register staging, one stage ahead; one barrier per stage);
+//   * the bias gradient rides on the MFMAs (dy^T x a ones fragment).
+// Output: the same packed fp32 slabs / replicas as k_wgrad_grouped (plain
+// stores when every slab has its replica, atomics otherwise), summed by the
+// weight-norm backward.
+#include "common.h"
+#include "conv_common.h"
+
+namespace {
+
+constexpr int WT_NT = 512;     // 8 waves
+constexpr int WT_SP = 128;     // output pixels per stage: 4 MFMA k-steps of 32
+constexpr int WT_KST = WT_SP / 32;
+
+// tile classes: (co tile, ci tile, kernel size, waves over co, waves over ci,
+// tap groups, x chunks per thread)
+template <int C> struct WtCfg;
+template <> struct WtCfg<0> { static constexpr int TCO = 64, TCI = 64, KS = 3, WCO = 2, WCI = 4, WTG = 1, NX = 7; };
+template <> struct WtCfg<1> { static constexpr int TCO = 128, TCI = 128, KS = 1, WCO = 2, WCI = 4, WTG = 1, NX = 4; };
+template <> struct WtCfg<2> { static constexpr int TCO = 32, TCI = 32, KS = 3, WCO = 2, WCI = 2, WTG = 2, NX = 4; };
+template <> struct WtCfg<3> { static constexpr int TCO = 64, TCI = 64, KS = 1, WCO = 2, WCI = 4, WTG = 1, NX = 2; };
+
+__host__ __device__ inline int wt_class(int ks, int cs_in, int cs_dy) {
+    if (ks == 3) return (cs_in <= 32 && cs_dy <= 32) ? 2 : 0;
+    return (cs_in <= 64 && cs_dy <= 64) ? 3 : 1;
+}
+__host__ __device__ inline int wt_tco(int c) { return c == 1 ? 128 : (c == 2 ? 32 : 64); }
+__host__ __device__ inline int wt_tci(int c) { return c == 1 ? 128 : (c == 2 ? 32 : 64); }
+__host__ __device__ inline int wt_ks(int c) { return (c == 0 || c == 2) ? 3 : 1; }
+__host__ __device__ inline int wt_pitch(int t) { return t * 2 + 16; }            // bytes per LDS row
+// padded rows a stage of rs output rows can touch (image boundaries add 2 each)
+__host__ __device__ inline int wt_npr(int rs, int H) { return rs + 2 + 2 * ((rs - 1 + H - 1) / H); }
+
+__host__ __device__ inline size_t wt_stage_bytes(int c, int H, int W) {
+    const int tco = wt_tco(c), tci = wt_tci(c);
+    const size_t dy = (size_t)WT_SP * wt_pitch(tco);
+    size_t x;
+    if (wt_ks(c) == 1) x = (size_t)WT_SP * wt_pitch(tci);
+    else x = (size_t)wt_npr(WT_SP / W, H) * (W + 2) * wt_pitch(tci);
+    return dy + x;
+}
+__host__ __device__ inline size_t wt_lds_bytes(int c, int H, int W) {
+    return 2 * wt_stage_bytes(c, H, W) + 24 * (size_t)wt_tci(c);   // 2 stages + BN table + fp64 scratch
+}
+
+__device__ __forceinline__ u32x4 tr_pair(const char* base, int pitch) {
+    const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)base);
+    const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)(base + 4 * pitch));
+    const uint2 l = __builtin_bit_cast(uint2, lo), h = __builtin_bit_cast(uint2, hi);
+    return u32x4{l.x, l.y, h.x, h.y};
+}
+
+// the fields of one conv a block needs, by value (a reference into the
+// by-value group argument would be indexed dynamically from scratch)
+struct WtConv {
+    const void* x; const void* dy; float* ws; float* wsb;
+    rnvp_bn_src pro;
+    int cs_in, cin, cs_dy, n, kp, pro_bn_relu, nz, nrep, B, H, W;
+    long long m_per_slab;
+};
+
+template <int CLS>
+__device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int z, char* lds) {
+    using Cfg = WtCfg<CLS>;
+    constexpr int TCO = Cfg::TCO, TCI = Cfg::TCI, KS = Cfg::KS, T = KS * KS;
+    constexpr int WCO = Cfg::WCO, WCI = Cfg::WCI, WTG = Cfg::WTG, NX = Cfg::NX;
+    constexpr int FCO = TCO / (16 * WCO), FCI = TCI / (16 * WCI);
+    constexpr int TPW = (T + WTG - 1) / WTG;                    // taps per wave
+    constexpr int DP = TCO * 2 + 16, XP = TCI * 2 + 16;         // LDS row pitches (bytes)
+    constexpr int CPO = TCO / 8, CPI = TCI / 8;                 // 16-byte chunks per row
+    constexpr int NDY = WT_SP * CPO / WT_NT;
+    static_assert(WCO * WCI * WTG * 64 == WT_NT, "wave layout");
+    static_assert(NDY * WT_NT == WT_SP * CPO && WT_NT % CPI == 0, "chunk layout");
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wg = wid % WTG, wci = (wid / WTG) % WCI, wco = wid / (WTG * WCI);
+    const int gq = lane >> 4, li = lane & 15, qq = li >> 2, pp = li & 3;
+    const int H = cv.H, W = cv.W, Bn = cv.B;
+    const long long M = (long long)Bn * H * W;
+    const int cs = cv.cs_in, csd = cv.cs_dy, N = cv.n;
+    const int co0 = cot * TCO, ci0 = cit * TCI;
+    const long long mb = (long long)z * cv.m_per_slab;
+    const long long me = (mb + cv.m_per_slab < M) ? mb + cv.m_per_slab : M;
+    const int ns = mb < me ? (int)((me - mb + WT_SP - 1) / WT_SP) : 0;
+    const int PW = KS == 3 ? W + 2 : 0;
+    const int RS = WT_SP / W;                                   // output rows per stage (launcher: W | 128)
+    const int NPR = KS == 3 ? wt_npr(RS, H) : 0;
+    const int xrows = KS == 3 ? NPR * PW : WT_SP;               // staged x positions per stage
+    const int xtot = xrows * CPI;                               // x chunks per stage
+    const size_t sbytes = wt_stage_bytes(CLS, H, W);
+    float* bnp = (float*)(lds + 2 * sbytes);                    // scale [TCI] | shift [TCI] | fp64 scratch [2 TCI]
+    const bool pro = cv.pro_bn_relu != 0;
+
+    // ---- BN+ReLU table of this ci tile (channels >= cin: scale = shift = 0) ----
+    if (pro) block_bn_table(cv.pro, cv.cin, ci0, TCI, bnp, bnp + TCI, nullptr, nullptr, (double*)(bnp + 2 * TCI));
+    __syncthreads();
+    const int cch = tid % CPI;                                  // this thread's x channel chunk (fixed)
+    float sc[8], sh[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        sc[e] = pro ? bnp[cch * 8 + e] : 1.f;
+        sh[e] = pro ? bnp[TCI + cch * 8 + e] : 0.f;
+    }
+    const bool xcol_ok = ci0 + cch * 8 < cs;
+    const int dch = tid % CPO;                                  // this thread's dy channel chunk (fixed)
+    const bool dcol_ok = co0 + dch * 8 < csd;
+    const float rPW = KS == 3 ? 1.0f / (float)PW : 0.f, rH2 = 1.0f / (float)(H + 2);   // PW, H+2 > 0
+    const float rW = 1.0f / (float)W, rH = 1.0f / (float)H;
+
+    // buffer resources: an out-of-range offset (invalid pixel / channel chunk)
+    // returns zeros without a memory access
+    const __amdgpu_buffer_rsrc_t XR = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<void*>(cv.x), 0, (int)((long long)M * cs * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t DR = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<void*>(cv.dy), 0, (int)((long long)M * csd * 2), 0x00020000);
+    constexpr int OOB = 0x7ffffff0;
+    u32x4 rx[NX], rd[NDY];
+    unsigned xm = 0;                                            // x chunk validity (the transform of 0 is not 0)
+    // stage-invariant part of this thread's x chunks: padded (row slot, column)
+    int xjp[NX];
+#pragma unroll
+    for (int u = 0; u < NX; ++u) {
+        const int q = tid + u * WT_NT, pos = q / CPI;
+        if constexpr (KS == 3) {
+            const int j = fdiv_small(pos, rPW);
+            xjp[u] = (q < xtot) ? (j << 8) | (pos - j * PW) : -1;      // PW <= 130
+        } else {
+            xjp[u] = (q < xtot) ? pos : -1;
+        }
+    }
+
+    // global loads of stage s into registers
+    auto gload = [&](int s) {
+        const int p0 = (int)(mb + (long long)s * WT_SP);
+#pragma unroll
+        for (int u = 0; u < NDY; ++u) {
+            const int p = p0 + (tid + u * WT_NT) / CPO;
+            const bool ok = (p < me) & dcol_ok;
+            rd[u] = __builtin_amdgcn_raw_buffer_load_b128(DR, ok ? (p * csd + co0 + dch * 8) * 2 : OOB, 0, 0);
+        }
+        xm = 0;
+        if constexpr (KS == 1) {
+#pragma unroll
+            for (int u = 0; u < NX; ++u) {
+                const int p = p0 + xjp[u];
+                const bool ok = (xjp[u] >= 0) & (p < me) & xcol_ok;
+                rx[u] = __builtin_amdgcn_raw_buffer_load_b128(XR, ok ? (p * cs + ci0 + cch * 8) * 2 : OOB, 0, 0);
+                xm |= (unsigned)ok << u;
+            }
+        } else {
+            // padded row G of slot j: G = gs + j, gs = G(o0) - 1 where G(o) =
+            // o + 2 (o / H) + 1 is the padded row of output row o (a zero row
+            // above and below every image; p0 is row aligned)
+            const int o0 = p0 / W;
+            const int gs = o0 + 2 * fdiv_small(o0, rH);
+#pragma unroll
+            for (int u = 0; u < NX; ++u) {
+                const int j = xjp[u] >> 8, pc = xjp[u] & 255;
+                const int G = gs + j;                             // < 2^22 (launcher)
+                const int bb = fdiv_small(G, rH2);
+                const int yy = G - bb * (H + 2) - 1, xx = pc - 1;
+                const bool ok = (xjp[u] >= 0) & (bb < Bn) & (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W) & xcol_ok;
+                const int pix = (bb * H + yy) * W + xx;
+                rx[u] = __builtin_amdgcn_raw_buffer_load_b128(XR, ok ? (pix * cs + ci0 + cch * 8) * 2 : OOB, 0, 0);
+                xm |= (unsigned)ok << u;
+            }
+        }
+    };
+    // transform + store of the loaded stage into LDS buffer buf
+    auto lstore = [&](int buf) {
+        char* dyL = lds + (size_t)buf * sbytes;
+        char* xL = dyL + (size_t)WT_SP * DP;
+#pragma unroll
+        for (int u = 0; u < NDY; ++u) {
+            const int r = (tid + u * WT_NT) / CPO;
+            *(u32x4*)(dyL + r * DP + dch * 16) = rd[u];
+        }
+#pragma unroll
+        for (int u = 0; u < NX; ++u) {
+            if (xjp[u] < 0) continue;
+            const int pos = (tid + u * WT_NT) / CPI;
+            u32x4 v = rx[u];
+            if (pro) {
+                float f[8];
+                unpack(v, f, bf16_t());
+#pragma unroll
+                for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e] * sc[e] + sh[e], 0.f);
+                v = pack(f, bf16_t());
+                const uint32_t k = ((xm >> u) & 1u) ? ~0u : 0u;
+                v &= u32x4{k, k, k, k};
+            }
+            *(u32x4*)(xL + pos * XP + cch * 16) = v;
+        }
+    };
+
+    floatx4 acc[FCO][FCI][TPW];
+    floatx4 bacc[FCO];
+#pragma unroll
+    for (int a = 0; a < FCO; ++a) {
+        bacc[a] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int b = 0; b < FCI; ++b)
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) acc[a][b][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    const bool do_bias = cv.wsb != nullptr && cit == 0 && wci == 0 && wg == 0;
+    const u32x4 ones = u32x4{0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u};   // bf16 1.0 x 8
+    // per-tap LDS row offsets (positions) of this wave's taps
+    int toff[TPW];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        const int tap = wg * TPW + t;
+        toff[t] = KS == 3 ? ((tap / 3 - 1) * PW + (tap % 3 - 1)) : 0;
+    }
+
+    if (ns > 0) {
+        gload(0);
+        lstore(0);
+    }
+    __syncthreads();
+#ifndef WT_PROBE
+#define WT_PROBE 0
+#endif
+    for (int s = 0; s < ns; ++s) {
+        const int cur = s & 1;
+        if (WT_PROBE != 2 && s + 1 < ns) gload(s + 1);
+        const char* dyL = lds + (size_t)cur * sbytes;
+        const char* xL = dyL + (size_t)WT_SP * DP;
+        int o0 = 0, ob0 = 0;
+        if constexpr (KS == 3) {
+            o0 = (int)((mb + (long long)s * WT_SP) / W);
+            ob0 = fdiv_small(o0, rH);
+        }
+#pragma unroll
+        for (int kk = 0; kk < (WT_PROBE == 1 ? 0 : WT_KST); ++kk) {
+            const int jl = kk * 32 + 8 * gq + qq;                 // pixel rows of this lane (lo; hi = +4)
+            u32x4 af[FCO];
+#pragma unroll
+            for (int a = 0; a < FCO; ++a)
+                af[a] = tr_pair(dyL + jl * DP + (wco * FCO * 16 + a * 16 + 4 * pp) * 2, DP);
+            if (do_bias) {
+#pragma unroll
+                for (int a = 0; a < FCO; ++a) Mf<bf16_t>::step(af[a], ones, bacc[a]);
+            }
+            int plo, phi;                                          // LDS x positions of pixel rows jl, jl + 4
+            if constexpr (KS == 1) {
+                plo = jl;
+                phi = jl + 4;
+            } else {
+                // pixel j of the stage: output row o0 + j / W, column j % W;
+                // its slot = rows since o0 + 2 per image boundary crossed + 1
+                auto posof = [&](int j) {
+                    const int jr = fdiv_small(j, rW), xx = j - jr * W;
+                    const int ob = fdiv_small(o0 + jr, rH);
+                    return (jr + 2 * (ob - ob0) + 1) * PW + xx + 1;
+                };
+                plo = posof(jl);
+                phi = posof(jl + 4);
+            }
+            (void)0;
+#pragma unroll
+            for (int b = 0; b < FCI; ++b) {
+                const int col = (wci * FCI * 16 + b * 16 + 4 * pp) * 2;
+#pragma unroll
+                for (int t = 0; t < TPW; ++t) {
+                    if (wg * TPW + t >= T) continue;
+                    const char* pl = xL + (plo + toff[t]) * XP + col;
+                    const char* ph = xL + (phi + toff[t]) * XP + col;
+                    const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)pl);
+                    const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)ph);
+                    const uint2 l = __builtin_bit_cast(uint2, lo), h = __builtin_bit_cast(uint2, hi);
+                    const u32x4 bf = u32x4{l.x, l.y, h.x, h.y};
+#pragma unroll
+                    for (int a = 0; a < FCO; ++a) Mf<bf16_t>::step(af[a], bf, acc[a][b][t]);
+                }
+            }
+        }
+        if (s + 1 < ns) lstore(cur ^ 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue: D rows = co, cols = ci; k = tap * cs_in + ci ----
+    const int rep = z % cv.nrep;
+    const bool atomic = cv.nrep < cv.nz;
+    float* out = cv.ws + (long long)rep * N * cv.kp;
+#pragma unroll
+    for (int a = 0; a < FCO; ++a)
+#pragma unroll
+        for (int b = 0; b < FCI; ++b)
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) {
+                const int tap = wg * TPW + t;
+                if (tap >= T) continue;
+                const int ci = ci0 + wci * FCI * 16 + b * 16 + li;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int co = co0 + wco * FCO * 16 + a * 16 + gq * 4 + r;
+                    if (co < N && ci < cs) {
+                        float* o = out + (long long)co * cv.kp + tap * cs + ci;
+                        if (atomic) atomicAdd(o, acc[a][b][t][r]);
+                        else *o = acc[a][b][t][r];
+                    }
+                }
+            }
+    if (do_bias && li == 0) {
+        float* bo = cv.wsb + (long long)rep * N;
+#pragma unroll
+        for (int a = 0; a < FCO; ++a)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int co = co0 + wco * FCO * 16 + a * 16 + gq * 4 + r;
+                if (co < N) {
+                    if (atomic) atomicAdd(bo + co, bacc[a][r]);
+                    else bo[co] = bacc[a][r];
+                }
+            }
+    }
+}
+
+// block -> (conv, slab, co tile, ci tile); consecutive tasks (one slab's tiles,
+// which share the slab's pixels through L2) go to one XCD
+__global__ __launch_bounds__(WT_NT) void k_wgrad_tap(rnvp_wgrad_group g) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const int nb = gridDim.x, b = blockIdx.x;
+    const int q = nb / 8, r = nb % 8, xcd = b % 8;
+    const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
+    int c = 0;
+    while (c + 1 < g.n_conv && g.conv[c + 1].task0 <= t) ++c;
+    const rnvp_wgrad_conv& gc = g.conv[c];
+    const WtConv cv{gc.x, gc.dy, gc.ws, gc.wsb, gc.pro, gc.cs_in, gc.cin, gc.cs_dy, gc.n, gc.kp, gc.pro_bn_relu,
+                    gc.nz, gc.nrep, g.B, g.H, g.W, gc.m_per_slab};
+    const int cls = wt_class(gc.ks, gc.cs_in, gc.cs_dy);
+    const int tco = (gc.n + wt_tco(cls) - 1) / wt_tco(cls), tci = gc.tk;
+    const int local = t - gc.task0;
+    const int per = tco * tci;
+    const int z = local / per, rr = local - z * per;
+    const int cot = rr / tci, cit = rr - cot * tci;
+    switch (cls) {
+        case 0: wt_body<0>(cv, cot, cit, z, lds); break;
+        case 1: wt_body<1>(cv, cot, cit, z, lds); break;
+        case 2: wt_body<2>(cv, cot, cit, z, lds); break;
+        default: wt_body<3>(cv, cot, cit, z, lds); break;
+    }
+}
+
+}  // namespace
+
+// Launch of the tap-shared kernel for a bf16 group; RNVP_E_UNSUPPORTED when a
+// conv's shape is outside what it stages (the caller then uses the per-tap
+// kernel).  Fills task0 / tk (= ci tiles) / m_per_slab of the group's copy.
+int rnvp_wgrad_tap_launch(rnvp_wgrad_group* g, hipStream_t s) {
+    if (g->dtype != RNVP_BF16) return RNVP_E_UNSUPPORTED;
+    const long long M = (long long)g->B * g->H * g->W;
+    const int H = g->H, W = g->W;
+    if (W > WT_SP || WT_SP % W) return RNVP_E_UNSUPPORTED;            // stages are whole rows
+    if ((long long)g->B * (H + 2) >= (1ll << 22) || M >= (1ll << 31)) return RNVP_E_UNSUPPORTED;
+    long long tasks = 0;
+    size_t shm = 0;
+    for (int c = 0; c < g->n_conv; ++c) {
+        rnvp_wgrad_conv& v = g->conv[c];
+        const int cls = wt_class(v.ks, v.cs_in, v.cs_dy);
+        // 32-bit buffer offsets (bytes)
+        if (M * v.cs_in * 2 >= (1ll << 31) || M * v.cs_dy * 2 >= (1ll << 31)) return RNVP_E_UNSUPPORTED;
+        const size_t lb = wt_lds_bytes(cls, H, W);
+        if (lb > 160 * 1024) return RNVP_E_UNSUPPORTED;
+        if (wt_ks(cls) == 3) {
+            const int npr = wt_npr(WT_SP / W, H);
+            const int cpi = wt_tci(cls) / 8;
+            const int nx = cls == 0 ? WtCfg<0>::NX : WtCfg<2>::NX;
+            if ((long long)npr * (W + 2) * cpi > (long long)nx * WT_NT) return RNVP_E_UNSUPPORTED;
+        }
+        if (lb > shm) shm = lb;
+        // slabs of whole stages; the slab count must stay v.nz (the replica
+        // workspace and the weight-norm backward are sized by it)
+        const long long stages = (M + WT_SP - 1) / WT_SP;
+        v.m_per_slab = ((stages + v.nz - 1) / v.nz) * WT_SP;
+        if ((M + v.m_per_slab - 1) / v.m_per_slab != v.nz) return RNVP_E_UNSUPPORTED;
+        v.tk = (v.cs_in + wt_tci(cls) - 1) / wt_tci(cls);
+        v.task0 = (int)tasks;
+        tasks += (long long)v.nz * ((v.n + wt_tco(cls) - 1) / wt_tco(cls)) * v.tk;
+    }
+    if (tasks <= 0 || tasks > (1ll << 30)) return RNVP_E_INVALID;
+    k_wgrad_tap<<<(unsigned)tasks, WT_NT, shm, s>>>(*g);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}

@@ -8,7 +8,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librealnvp_hip.so")
+# RNVP_LIB_PATH: a probe build of the same library (tools/, timing experiments)
+LIB_PATH = os.environ.get("RNVP_LIB_PATH") or os.path.join(_HERE, "librealnvp_hip.so")
 
 RNVP_F32, RNVP_BF16 = 0, 1
 

@@ -62,19 +62,25 @@ MARKER_FAMILIES = []
 
 
 def _launch(family, nbytes, flops, fn, *args):
-    if PROFILE is None:
+    """One engine launch.  MARKERS alone (no PROFILE) also works under graph
+    capture: the markers are captured with the step, so a rocprofv3 kernel
+    trace of the replayed graph splits by family too (tools/trace_families.py)."""
+    if PROFILE is None and not MARKERS:
         return fn(*args)
     if MARKERS:
         _lib.lib().marker(len(MARKER_FAMILIES), stream_ptr())
         MARKER_FAMILIES.append(family)
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
-    e0.record()
-    fn(*args)
-    e1.record()
+    if PROFILE is None:
+        fn(*args)
+    else:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn(*args)
+        e1.record()
+        PROFILE.append((family, nbytes, flops, e0, e1))
     if MARKERS:
         _lib.lib().marker(-1, stream_ptr())
-    PROFILE.append((family, nbytes, flops, e0, e1))
 
 
 class Arena:

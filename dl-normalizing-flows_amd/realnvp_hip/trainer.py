@@ -122,6 +122,7 @@ class FlowTrainer:
         self.comm, self.reduce_dtype = comm, reduce_dtype
         self._reduce_pg = None
         self._cap_pg = None
+        self.comm_events = None
         self.comm_stream = None
         if self.pg is not None and comm == "overlap":
             self.comm_stream = torch.cuda.Stream(device=self.dev)
@@ -386,7 +387,14 @@ class FlowTrainer:
                         ev.record(self.side if self.side is not None else torch.cuda.current_stream())
                         self.comm_stream.wait_event(ev)
                         with torch.cuda.stream(self.comm_stream):
+                            if self.comm_events is not None:     # bench.py: per-bucket timing (eager)
+                                e0 = torch.cuda.Event(enable_timing=True)
+                                e0.record()
                             self._reduce_bucket(lo, hi)
+                            if self.comm_events is not None:
+                                e1 = torch.cuda.Event(enable_timing=True)
+                                e1.record()
+                                self.comm_events.append((hi - lo, e0, e1))
             elif st[0] == "squeeze":
                 _, a, b = st
                 L.undo_squeeze(self._g(b).data_ptr(), self._g(a).data_ptr(), *a.shape, s)
@@ -459,7 +467,7 @@ class FlowTrainer:
             for n, b in self.model.named_buffers():
                 b.copy_(bufs[n])
 
-    def capture(self, warmup=2, restore=True):
+    def capture(self, warmup=2, restore=True, before_capture=None):
         """Warm up eagerly on a side stream, then capture the step into HIP
         graphs.  The warm-up steps move the parameters, Adam moments, step
         counter (and with it the dequantisation noise) and BN running stats;
@@ -483,6 +491,8 @@ class FlowTrainer:
         # the captured all-reduces go through a group of their own (see
         # _capture_group); warm-up and eager collectives stay on self.pg
         self._cap_pg = self._capture_group()
+        if before_capture is not None:
+            before_capture()
         self.graph = torch.cuda.CUDAGraph()
         self.graph_opt = None
         self.graph_input = self.external_input

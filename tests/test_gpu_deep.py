@@ -429,4 +429,8 @@ def test_grouped_wgrad_vs_torch(case, dtype):
     got, ref, gotb, refb = _wgrad_case(B, H, W, cin, cout, ks, dtype, pro)
     tol = 1e-5 if dtype == "fp32" else 1e-4
     assert rel(got.cpu(), ref.cpu()) < tol, rel(got.cpu(), ref.cpu())
-    assert rel(gotb.cpu(), refb.cpu()) < tol
+    # the bias gradient is a plain sum of M fp32 terms (~N(0,1) here): its
+    # rounding error grows ~sqrt(M) (measured 1.25e-5 at M = 2^22 in fp32)
+    M = B * H * W
+    tolb = tol * max(1.0, (M / 2.0 ** 18) ** 0.5)
+    assert rel(gotb.cpu(), refb.cpu()) < tolb, rel(gotb.cpu(), refb.cpu())

@@ -1,0 +1,17 @@
+#!/bin/bash
+# GPU box: PMC passes (one counter set per run) over one conv_microbench case.
+#   TAG=... CASE="wgrad s5 3x3" bash tools/gpu_pmc.sh
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/${TAG:-pmc}
+mkdir -p $O
+step() { local log=$1; shift; "$@" > $O/$log 2>&1; local rc=$?; echo "$log rc=$rc"; if [ $rc -ne 0 ]; then tail -3 $O/$log; exit $rc; fi; }
+P1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU"
+P2="TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_PENDING_STALL_CYCLES_sum TCP_TOTAL_CACHE_ACCESSES_sum GRBM_GUI_ACTIVE"
+P3="TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_REQ_sum"
+P4="SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_MFMA"
+i=0
+for P in "$P1" "$P2" "$P3" "$P4"; do
+  i=$((i+1))
+  step pmc$i.log timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d $GRAFT_REPO_ROOT/$O/pmc$i -o run -- python3 $GRAFT_REPO_ROOT/tools/conv_microbench.py "--case=$CASE"
+done
