@@ -25,6 +25,8 @@
 #include "common.h"
 #include "conv_common.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int WT_NT = 512;     // 8 waves
@@ -32,12 +34,12 @@ constexpr int WT_SP = 128;     // output pixels per stage: 4 MFMA k-steps of 32
 constexpr int WT_KST = WT_SP / 32;
 
 // tile classes: (co tile, ci tile, kernel size, waves over co, waves over ci,
-// tap groups, x chunks per thread)
 template <int C> struct WtCfg;
-template <> struct WtCfg<0> { static constexpr int TCO = 64, TCI = 64, KS = 3, WCO = 2, WCI = 4, WTG = 1, NX = 7; };
-template <> struct WtCfg<1> { static constexpr int TCO = 128, TCI = 128, KS = 1, WCO = 2, WCI = 4, WTG = 1, NX = 4; };
-template <> struct WtCfg<2> { static constexpr int TCO = 32, TCI = 32, KS = 3, WCO = 2, WCI = 2, WTG = 2, NX = 4; };
-template <> struct WtCfg<3> { static constexpr int TCO = 64, TCI = 64, KS = 1, WCO = 2, WCI = 4, WTG = 1, NX = 2; };
+// tap groups, x chunks per thread per stage, stages of global loads in flight)
+template <> struct WtCfg<0> { static constexpr int TCO = 64, TCI = 64, KS = 3, WCO = 2, WCI = 4, WTG = 1, NX = 5, DEPTH = 1; };
+template <> struct WtCfg<1> { static constexpr int TCO = 128, TCI = 128, KS = 1, WCO = 2, WCI = 4, WTG = 1, NX = 4, DEPTH = 1; };
+template <> struct WtCfg<2> { static constexpr int TCO = 32, TCI = 32, KS = 3, WCO = 2, WCI = 2, WTG = 2, NX = 4, DEPTH = 2; };
+template <> struct WtCfg<3> { static constexpr int TCO = 64, TCI = 64, KS = 1, WCO = 2, WCI = 4, WTG = 1, NX = 2, DEPTH = 2; };
 
 __host__ __device__ inline int wt_class(int ks, int cs_in, int cs_dy) {
     if (ks == 3) return (cs_in <= 32 && cs_dy <= 32) ? 2 : 0;
@@ -82,7 +84,7 @@ template <int CLS>
 __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int z, char* lds) {
     using Cfg = WtCfg<CLS>;
     constexpr int TCO = Cfg::TCO, TCI = Cfg::TCI, KS = Cfg::KS, T = KS * KS;
-    constexpr int WCO = Cfg::WCO, WCI = Cfg::WCI, WTG = Cfg::WTG, NX = Cfg::NX;
+    constexpr int WCO = Cfg::WCO, WCI = Cfg::WCI, WTG = Cfg::WTG, NX = Cfg::NX, DEPTH = Cfg::DEPTH;
     constexpr int FCO = TCO / (16 * WCO), FCI = TCI / (16 * WCI);
     constexpr int TPW = (T + WTG - 1) / WTG;                    // taps per wave
     constexpr int DP = TCO * 2 + 16, XP = TCI * 2 + 16;         // LDS row pitches (bytes)
@@ -133,8 +135,8 @@ __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int 
     const __amdgpu_buffer_rsrc_t DR = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<void*>(cv.dy), 0, (int)((long long)M * csd * 2), 0x00020000);
     constexpr int OOB = 0x7ffffff0;
-    u32x4 rx[NX], rd[NDY];
-    unsigned xm = 0;                                            // x chunk validity (the transform of 0 is not 0)
+    u32x4 rx[DEPTH][NX], rd[DEPTH][NDY];
+    unsigned xm[DEPTH];                                         // x chunk validity (the transform of 0 is not 0)
     // stage-invariant part of this thread's x chunks: padded (row slot, column)
     int xjp[NX];
 #pragma unroll
@@ -148,23 +150,24 @@ __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int 
         }
     }
 
-    // global loads of stage s into registers
-    auto gload = [&](int s) {
+    // global loads of stage s into register slot SL
+    auto gload = [&](int s, auto SLC) {
+        constexpr int SL = decltype(SLC)::value;
         const int p0 = (int)(mb + (long long)s * WT_SP);
 #pragma unroll
         for (int u = 0; u < NDY; ++u) {
             const int p = p0 + (tid + u * WT_NT) / CPO;
             const bool ok = (p < me) & dcol_ok;
-            rd[u] = __builtin_amdgcn_raw_buffer_load_b128(DR, ok ? (p * csd + co0 + dch * 8) * 2 : OOB, 0, 0);
+            rd[SL][u] = __builtin_amdgcn_raw_buffer_load_b128(DR, ok ? (p * csd + co0 + dch * 8) * 2 : OOB, 0, 0);
         }
-        xm = 0;
+        unsigned m = 0;
         if constexpr (KS == 1) {
 #pragma unroll
             for (int u = 0; u < NX; ++u) {
                 const int p = p0 + xjp[u];
                 const bool ok = (xjp[u] >= 0) & (p < me) & xcol_ok;
-                rx[u] = __builtin_amdgcn_raw_buffer_load_b128(XR, ok ? (p * cs + ci0 + cch * 8) * 2 : OOB, 0, 0);
-                xm |= (unsigned)ok << u;
+                rx[SL][u] = __builtin_amdgcn_raw_buffer_load_b128(XR, ok ? (p * cs + ci0 + cch * 8) * 2 : OOB, 0, 0);
+                m |= (unsigned)ok << u;
             }
         } else {
             // padded row G of slot j: G = gs + j, gs = G(o0) - 1 where G(o) =
@@ -180,32 +183,34 @@ __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int 
                 const int yy = G - bb * (H + 2) - 1, xx = pc - 1;
                 const bool ok = (xjp[u] >= 0) & (bb < Bn) & (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W) & xcol_ok;
                 const int pix = (bb * H + yy) * W + xx;
-                rx[u] = __builtin_amdgcn_raw_buffer_load_b128(XR, ok ? (pix * cs + ci0 + cch * 8) * 2 : OOB, 0, 0);
-                xm |= (unsigned)ok << u;
+                rx[SL][u] = __builtin_amdgcn_raw_buffer_load_b128(XR, ok ? (pix * cs + ci0 + cch * 8) * 2 : OOB, 0, 0);
+                m |= (unsigned)ok << u;
             }
         }
+        xm[SL] = m;
     };
-    // transform + store of the loaded stage into LDS buffer buf
-    auto lstore = [&](int buf) {
+    // transform + store of register slot SL into LDS buffer buf
+    auto lstore = [&](int buf, auto SLC) {
+        constexpr int SL = decltype(SLC)::value;
         char* dyL = lds + (size_t)buf * sbytes;
         char* xL = dyL + (size_t)WT_SP * DP;
 #pragma unroll
         for (int u = 0; u < NDY; ++u) {
             const int r = (tid + u * WT_NT) / CPO;
-            *(u32x4*)(dyL + r * DP + dch * 16) = rd[u];
+            *(u32x4*)(dyL + r * DP + dch * 16) = rd[SL][u];
         }
 #pragma unroll
         for (int u = 0; u < NX; ++u) {
             if (xjp[u] < 0) continue;
             const int pos = (tid + u * WT_NT) / CPI;
-            u32x4 v = rx[u];
+            u32x4 v = rx[SL][u];
             if (pro) {
                 float f[8];
                 unpack(v, f, bf16_t());
 #pragma unroll
                 for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e] * sc[e] + sh[e], 0.f);
                 v = pack(f, bf16_t());
-                const uint32_t k = ((xm >> u) & 1u) ? ~0u : 0u;
+                const uint32_t k = ((xm[SL] >> u) & 1u) ? ~0u : 0u;
                 v &= u32x4{k, k, k, k};
             }
             *(u32x4*)(xL + pos * XP + cch * 16) = v;
@@ -232,70 +237,91 @@ __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int 
         toff[t] = KS == 3 ? ((tap / 3 - 1) * PW + (tap % 3 - 1)) : 0;
     }
 
-    if (ns > 0) {
-        gload(0);
-        lstore(0);
-    }
-    __syncthreads();
-#ifndef WT_PROBE
-#define WT_PROBE 0
-#endif
-    for (int s = 0; s < ns; ++s) {
-        const int cur = s & 1;
-        if (WT_PROBE != 2 && s + 1 < ns) gload(s + 1);
+    // MFMAs of the stage in LDS buffer cur (stage s)
+    auto compute = [&](int s, int cur) {
         const char* dyL = lds + (size_t)cur * sbytes;
         const char* xL = dyL + (size_t)WT_SP * DP;
-        int o0 = 0, ob0 = 0;
-        if constexpr (KS == 3) {
-            o0 = (int)((mb + (long long)s * WT_SP) / W);
-            ob0 = fdiv_small(o0, rH);
+        // this lane's LDS x positions (pixel rows lo = jl, hi = jl + 4) per k-step
+        int plo[WT_KST], phi[WT_KST];
+        if constexpr (KS == 1) {
+#pragma unroll
+            for (int kk = 0; kk < WT_KST; ++kk) {
+                plo[kk] = kk * 32 + 8 * gq + qq;
+                phi[kk] = plo[kk] + 4;
+            }
+        } else {
+            // pixel j of the stage: output row o0 + j / W, column j % W; its
+            // slot = rows since o0 + 2 per image boundary crossed + 1
+            const int o0 = (int)((mb + (long long)s * WT_SP) / W);
+            const int ob0 = fdiv_small(o0, rH);
+            auto posof = [&](int j) {
+                const int jr = fdiv_small(j, rW), xx = j - jr * W;
+                const int ob = fdiv_small(o0 + jr, rH);
+                return (jr + 2 * (ob - ob0) + 1) * PW + xx + 1;
+            };
+#pragma unroll
+            for (int kk = 0; kk < WT_KST; ++kk) {
+                plo[kk] = posof(kk * 32 + 8 * gq + qq);
+                phi[kk] = posof(kk * 32 + 8 * gq + qq + 4);
+            }
         }
 #pragma unroll
-        for (int kk = 0; kk < (WT_PROBE == 1 ? 0 : WT_KST); ++kk) {
-            const int jl = kk * 32 + 8 * gq + qq;                 // pixel rows of this lane (lo; hi = +4)
+        for (int kk = 0; kk < WT_KST; ++kk) {
+            const int jl = kk * 32 + 8 * gq + qq;                 // dy pixel rows of this lane (lo; hi = +4)
             u32x4 af[FCO];
 #pragma unroll
             for (int a = 0; a < FCO; ++a)
                 af[a] = tr_pair(dyL + jl * DP + (wco * FCO * 16 + a * 16 + 4 * pp) * 2, DP);
-            if (do_bias) {
-#pragma unroll
-                for (int a = 0; a < FCO; ++a) Mf<bf16_t>::step(af[a], ones, bacc[a]);
-            }
-            int plo, phi;                                          // LDS x positions of pixel rows jl, jl + 4
-            if constexpr (KS == 1) {
-                plo = jl;
-                phi = jl + 4;
-            } else {
-                // pixel j of the stage: output row o0 + j / W, column j % W;
-                // its slot = rows since o0 + 2 per image boundary crossed + 1
-                auto posof = [&](int j) {
-                    const int jr = fdiv_small(j, rW), xx = j - jr * W;
-                    const int ob = fdiv_small(o0 + jr, rH);
-                    return (jr + 2 * (ob - ob0) + 1) * PW + xx + 1;
-                };
-                plo = posof(jl);
-                phi = posof(jl + 4);
-            }
-            (void)0;
+            // every B fragment of the k-step is read before the MFMAs (one LDS wait)
+            u32x4 bfr[FCI][TPW];
 #pragma unroll
             for (int b = 0; b < FCI; ++b) {
                 const int col = (wci * FCI * 16 + b * 16 + 4 * pp) * 2;
 #pragma unroll
                 for (int t = 0; t < TPW; ++t) {
                     if (wg * TPW + t >= T) continue;
-                    const char* pl = xL + (plo + toff[t]) * XP + col;
-                    const char* ph = xL + (phi + toff[t]) * XP + col;
-                    const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)pl);
-                    const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)ph);
+                    const i16x4 lo =
+                        __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)(xL + (plo[kk] + toff[t]) * XP + col));
+                    const i16x4 hi =
+                        __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)(xL + (phi[kk] + toff[t]) * XP + col));
                     const uint2 l = __builtin_bit_cast(uint2, lo), h = __builtin_bit_cast(uint2, hi);
-                    const u32x4 bf = u32x4{l.x, l.y, h.x, h.y};
-#pragma unroll
-                    for (int a = 0; a < FCO; ++a) Mf<bf16_t>::step(af[a], bf, acc[a][b][t]);
+                    bfr[b][t] = u32x4{l.x, l.y, h.x, h.y};
                 }
             }
+            if (do_bias) {
+#pragma unroll
+                for (int a = 0; a < FCO; ++a) Mf<bf16_t>::step(af[a], ones, bacc[a]);
+            }
+#pragma unroll
+            for (int b = 0; b < FCI; ++b)
+#pragma unroll
+                for (int t = 0; t < TPW; ++t) {
+                    if (wg * TPW + t >= T) continue;
+#pragma unroll
+                    for (int a = 0; a < FCO; ++a) Mf<bf16_t>::step(af[a], bfr[b][t], acc[a][b][t]);
+                }
         }
-        if (s + 1 < ns) lstore(cur ^ 1);
+    };
+
+    // stage pipeline: DEPTH stages of global loads in flight (register slots
+    // s % DEPTH), LDS double buffer (s & 1), one barrier per stage
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, DEPTH - 1>;
+    if (ns > 0) gload(0, I0{});
+    if (DEPTH == 2 && ns > 1) gload(1, I1{});
+    if (ns > 0) lstore(0, I0{});
+    __syncthreads();
+    auto iter = [&](int s, auto SLC) {
+        constexpr int SL = decltype(SLC)::value;                   // slot of stage s (free: stored already)
+        constexpr int SN = (SL + 1) % DEPTH;                       // slot of stage s + 1
+        if (s + DEPTH < ns) gload(s + DEPTH, std::integral_constant<int, SL>{});
+        compute(s, s & 1);
+        if (s + 1 < ns) lstore((s + 1) & 1, std::integral_constant<int, SN>{});
         __syncthreads();
+    };
+    for (int s = 0; s < ns; s += DEPTH) {
+        iter(s, I0{});
+        if (DEPTH == 2 && s + 1 < ns) iter(s + 1, I1{});
     }
 
     // ---- epilogue: D rows = co, cols = ci; k = tap * cs_in + ci ----
@@ -385,7 +411,7 @@ int rnvp_wgrad_tap_launch(rnvp_wgrad_group* g, hipStream_t s) {
         if (wt_ks(cls) == 3) {
             const int npr = wt_npr(WT_SP / W, H);
             const int cpi = wt_tci(cls) / 8;
-            const int nx = cls == 0 ? WtCfg<0>::NX : WtCfg<2>::NX;
+            const int nx = cls == 0 ? WtCfg<0>::NX : WtCfg<2>::NX;   // class 0: W = 128 (config 4 scale 1) falls back
             if ((long long)npr * (W + 2) * cpi > (long long)nx * WT_NT) return RNVP_E_UNSUPPORTED;
         }
         if (lb > shm) shm = lb;
