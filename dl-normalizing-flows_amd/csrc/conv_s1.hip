@@ -1,0 +1,293 @@
+// Streaming 1x1 conv for the wide scales (bf16; N <= 64 outputs, cs_in <= 64):
+// WeightNormConv2d (modules_realnvp.py:64-71) with the fused BatchNorm+ReLU
+// prologue and the bias / residual / skip / next-BN-statistics (or the
+// dgrad ReLU/BN-backward) epilogue, as rnvp_conv2d's other families.
+//
+// At 64x64 / 32x32 pixels with 32-64 channels a 1x1 conv is a pure stream:
+// read x (and the residual / previous skip sum), write y, ~16 FLOP per byte.
+// The round-2 streaming kernel issued a tile's loads only after the previous
+// tile's epilogue (one memory latency per 64-pixel tile: ~1.7-2.8 TB/s).
+// Here every lane keeps its weights (an MFMA A fragment per 16 outputs and
+// k-step) and its BN prologue coefficients in registers, and each wave walks
+// its tiles with the NEXT tile's pixel chunks and epilogue operands already in
+// flight (register ring of two tiles): no LDS on the data path, no barrier.
+// Product D[n][m] = W[n][k] X[m][k]^T: a lane owns 4 consecutive output
+// channels of one pixel (8-byte epilogue vectors).
+#include "common.h"
+#include "conv_common.h"
+
+#include <type_traits>
+
+namespace {
+
+// NOPS epilogue operand streams per element (residual, previous y, the dgrad
+// epilogue's pre-BN x -- in that order, those present)
+template <int NT, int NKS, int TW, int NOPS>
+__global__ __launch_bounds__(256) void k_conv_s1(rnvp_conv_args a, int shards) {
+    constexpr int CH = 8, KS = 32;            // bf16: 8 channels per 16-B chunk, 32 per k-step
+    constexpr int NC = 16 * NT;
+    __shared__ double red[4][NC][2];
+    __shared__ double tmp[2 * 64];
+    __shared__ float bnp[2 * 64];
+    __shared__ float etab[4 * NC];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, li = lane & 15;
+    const int M = a.B * a.H * a.W;             // < 2^31 (host)
+    const int N = a.n, cs = a.cs_in, cso = a.cs_out;
+    const bool pro = a.pro_bn_relu != 0, epi_bn = a.epi_relu_bn_bwd != 0;
+    const bool has_acc = a.accumulate != 0;
+
+    // ---- tables (every thread: block-wide reductions) ----
+    if (pro) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + cs, nullptr, nullptr, tmp);
+    if (epi_bn) block_bn_table(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp);
+    __syncthreads();
+
+    // ---- per-lane constants: weights, prologue coefficients, bias ----
+    const bf16_t* __restrict__ Wg = (const bf16_t*)a.w;
+    u32x4 wv[NKS][NT];
+#pragma unroll
+    for (int s = 0; s < NKS; ++s)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const int n = j * 16 + li, k = s * KS + g * CH;
+            wv[s][j] = (n < N && k < cs) ? *(const u32x4*)(Wg + (long long)n * a.kp + k) : u32x4{0u, 0u, 0u, 0u};
+        }
+    float psc[NKS][CH], psh[NKS][CH];
+#pragma unroll
+    for (int s = 0; s < NKS; ++s)
+#pragma unroll
+        for (int e = 0; e < CH; ++e) {
+            const int c = s * KS + g * CH + e;
+            psc[s][e] = (pro && c < cs) ? bnp[c] : 1.f;
+            psh[s][e] = (pro && c < cs) ? bnp[cs + c] : 0.f;
+        }
+    float bias[NT][4];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int n = j * 16 + 4 * g + r;
+            bias[j][r] = (a.bias && n < N) ? a.bias[n] : 0.f;
+        }
+
+    // buffer resources: out-of-range offsets read zeros without a memory access
+    const __amdgpu_buffer_rsrc_t XR = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0,
+                                                                        (int)((long long)M * cs * 2), 0x00020000);
+    // epilogue streams: role 0 residual, 1 previous y (skip accumulation), 2 pre-BN x
+    // (stream q takes the q-th present role; the host picked NOPS = their count)
+    const bool p0 = a.residual != nullptr, p1 = has_acc;
+    int role[3];
+    role[0] = p0 ? 0 : (p1 ? 1 : 2);
+    role[1] = (p0 && p1) ? 1 : 2;
+    role[2] = 2;
+    __amdgpu_buffer_rsrc_t OR[NOPS > 0 ? NOPS : 1];
+#pragma unroll
+    for (int q = 0; q < NOPS; ++q) {
+        const void* src = role[q] == 0 ? a.residual : (role[q] == 1 ? (const void*)a.y : a.epi_x);
+        OR[q] = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(src), 0, (int)((long long)M * cso * 2),
+                                                  0x00020000);
+    }
+    constexpr int OOB = 0x7ffffff0;
+
+    // ---- tile ring: pixel chunks + epilogue operands of two tiles ----
+    struct Tile {
+        u32x4 x[TW][NKS];
+        uint2 o[NOPS > 0 ? NOPS : 1][TW][NT];
+    };
+    Tile ring[2];
+    const int ntiles = (M + 16 * TW - 1) / (16 * TW);
+    const int nwaves = gridDim.x * 4;
+    const int w0 = blockIdx.x * 4 + wid;
+    auto load = [&](int t, auto SLC) __attribute__((always_inline)) {
+        constexpr int SL = decltype(SLC)::value;
+        Tile& T = ring[SL];
+#pragma unroll
+        for (int i = 0; i < TW; ++i) {
+            const int m = t * (16 * TW) + i * 16 + li;
+            const bool okm = (t < ntiles) & (m < M);
+#pragma unroll
+            for (int s = 0; s < NKS; ++s) {
+                const int k = s * KS + g * CH;
+                T.x[i][s] = __builtin_amdgcn_raw_buffer_load_b128(XR, (okm & (k < cs)) ? (m * cs + k) * 2 : OOB, 0, 0);
+            }
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                const int n0 = j * 16 + 4 * g;
+                const int off = (okm & (n0 < cso)) ? (m * cso + n0) * 2 : OOB;
+#pragma unroll
+                for (int q = 0; q < NOPS; ++q)
+                    T.o[q][i][j] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(OR[q], off, 0, 0));
+            }
+        }
+    };
+
+    double s1[NT][4], s2[NT][4];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.0;
+    bf16_t* __restrict__ Y = (bf16_t*)a.y;
+
+    auto run = [&](int t, auto SLC) __attribute__((always_inline)) {
+        constexpr int SL = decltype(SLC)::value;
+        const Tile& T = ring[SL];
+        floatx4 acc[TW][NT];
+#pragma unroll
+        for (int i = 0; i < TW; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < TW; ++i)
+#pragma unroll
+            for (int s = 0; s < NKS; ++s) {
+                u32x4 v = T.x[i][s];
+                if (pro) {
+                    float f[CH];
+                    unpack(v, f, bf16_t());
+#pragma unroll
+                    for (int e = 0; e < CH; ++e) f[e] = fmaxf(f[e] * psc[s][e] + psh[s][e], 0.f);
+                    v = pack(f, bf16_t());
+                    // a pixel outside the image / a channel chunk beyond cs stays zero
+                    const int m = t * (16 * TW) + i * 16 + li, k = s * KS + g * CH;
+                    const uint32_t keep = ((m < M) & (k < cs)) ? ~0u : 0u;
+                    v &= u32x4{keep, keep, keep, keep};
+                }
+#pragma unroll
+                for (int j = 0; j < NT; ++j) Mf<bf16_t>::step(wv[s][j], v, acc[i][j]);
+            }
+        // epilogue: lane owns channels j*16 + 4g .. +3 of pixel t*16*TW + i*16 + li
+#pragma unroll
+        for (int i = 0; i < TW; ++i) {
+            const int m = t * (16 * TW) + i * 16 + li;
+            if (m >= M) continue;
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                const int n0 = j * 16 + 4 * g;
+                if (n0 >= cso) continue;
+                float v[4], xv[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bias[j][r];
+#pragma unroll
+                for (int q = 0; q < NOPS; ++q) {
+                    const uint2 u = T.o[q][i][j];
+                    const float f[4] = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                                        __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
+                    if (role[q] == 2) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) xv[r] = f[r];
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) v[r] += f[r];
+                    }
+                }
+                if (epi_bn) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int n = n0 + r;
+                        if (xv[r] * etab[n] + etab[NC + n] <= 0.f) v[r] = 0.f;
+                        s1[j][r] += v[r];
+                        s2[j][r] += v[r] * (xv[r] - etab[2 * NC + n]) * etab[3 * NC + n];
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        s1[j][r] += v[r];
+                        s2[j][r] += (double)v[r] * v[r];
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (n0 + r >= N) v[r] = 0.f;
+                st4(Y + (long long)m * cso + n0, v);
+            }
+        }
+    };
+
+    // walk this wave's tiles w0, w0 + nwaves, ... with the next one in flight
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    int t = w0;
+    if (t < ntiles) load(t, I0{});
+    while (t < ntiles) {
+        if (t + nwaves < ntiles) load(t + nwaves, I1{});
+        run(t, I0{});
+        t += nwaves;
+        if (t >= ntiles) break;
+        if (t + nwaves < ntiles) load(t + nwaves, I0{});
+        run(t, I1{});
+        t += nwaves;
+    }
+
+    // ---- batch statistics: DPP row sums, LDS across waves, sharded fp64 atomics ----
+    const bool want_sums = a.out_sums || (epi_bn && a.epi_sums);
+    if (want_sums) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double u1 = row_sum16(s1[j][r]), u2 = row_sum16(s2[j][r]);
+                if (li == 0) {
+                    red[wid][j * 16 + 4 * g + r][0] = u1;
+                    red[wid][j * 16 + 4 * g + r][1] = u2;
+                }
+            }
+        __syncthreads();
+        double* sums = shard_ptr(epi_bn ? a.epi_sums : a.out_sums, shards, N);
+        for (int n = tid; n < N; n += 256) {
+            double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                t1 += red[w][n][0];
+                t2 += red[w][n][1];
+            }
+            atomicAdd(&sums[n], t1);
+            atomicAdd(&sums[N + n], t2);
+        }
+    }
+}
+
+template <int NT, int NKS, int TW, int NOPS>
+int launch_s1(const rnvp_conv_args* a, hipStream_t s) {
+    const long long M = (long long)a->B * a->H * a->W;
+    const long long ntiles = (M + 16 * TW - 1) / (16 * TW);
+    // one resident wave of workgroups, each wave walking several tiles with
+    // the next one in flight (a second round of workgroups would restart the
+    // pipeline)
+    static const int per_cu = [] {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_conv_s1<NT, NKS, TW, NOPS>, 256, 0) != hipSuccess || n < 1)
+            n = 1;
+        return n;
+    }();
+    long long grid = (ntiles + 3) / 4;
+    if (grid > 256LL * per_cu) grid = 256LL * per_cu;
+    k_conv_s1<NT, NKS, TW, NOPS><<<(unsigned)grid, 256, 0, s>>>(*a, rnvp_stat_shards(M));
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+template <int NT, int NKS, int TW>
+int launch_s1_ops(const rnvp_conv_args* a, hipStream_t s) {
+    const int nops = (a->residual ? 1 : 0) + (a->accumulate ? 1 : 0) + (a->epi_relu_bn_bwd ? 1 : 0);
+    switch (nops) {
+        case 0: return launch_s1<NT, NKS, TW, 0>(a, s);
+        case 1: return launch_s1<NT, NKS, TW, 1>(a, s);
+        case 2: return launch_s1<NT, NKS, TW, 2>(a, s);
+        default: return launch_s1<NT, NKS, TW, 3>(a, s);
+    }
+}
+
+}  // namespace
+
+// 1x1, bf16, N <= 64, cs_in <= 64, M >= 16k: the register-pipelined stream
+int rnvp_conv_s1_launch(const rnvp_conv_args* a, hipStream_t s) {
+    if (a->dtype != RNVP_BF16 || a->ks != 1 || a->n > 64 || a->cs_in > 64 || a->cs_out > 64) return RNVP_E_UNSUPPORTED;
+    const long long M = (long long)a->B * a->H * a->W;
+    if (M < 16384 || M * 64 * 2 >= (1ll << 31)) return RNVP_E_UNSUPPORTED;
+    if (((uintptr_t)a->y & 7) || (a->residual && ((uintptr_t)a->residual & 7)) ||
+        (a->epi_relu_bn_bwd && ((uintptr_t)a->epi_x & 7)))
+        return RNVP_E_UNSUPPORTED;
+    const bool k1 = a->cs_in <= 32;
+    if (a->n <= 16) return k1 ? launch_s1_ops<1, 1, 4>(a, s) : launch_s1_ops<1, 2, 4>(a, s);
+    if (a->n <= 32) return k1 ? launch_s1_ops<2, 1, 4>(a, s) : launch_s1_ops<2, 2, 4>(a, s);
+    return k1 ? launch_s1_ops<4, 1, 2>(a, s) : launch_s1_ops<4, 2, 2>(a, s);
+}
