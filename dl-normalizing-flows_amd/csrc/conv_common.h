@@ -213,6 +213,88 @@ __device__ __forceinline__ int fdiv_exact(int q, int d, float r) {
     return t;
 }
 
+// BatchNorm backward apply over the blocks blk = 0..nblk-1 of a (virtual)
+// grid: every block reduces the statistic shards into its LDS table, then
+// grid-strides over the 16-byte chunks.  dsm: 68*cs bytes of LDS
+// (tmp [2*cs] | gsum [2*cs] fp64 | p [5*cs] f32 | table [4*cs] f32).
+template <typename T>
+__device__ __forceinline__ void bn_bwd_body(const rnvp_bn_bwd_args& a, double* dsm, int blk, int nblk) {
+    constexpr int CH = Mf<T>::CH;
+    const int cs = a.cs, C = a.C;
+    const double cnt = (double)a.M;
+    double* gs = dsm + 2 * cs;
+    float* p = (float*)(dsm + 4 * cs);   // per channel: coef, k1, k2, mean, rstd
+    float* t_sc = p + 5 * cs;            // scratch: scale, shift, mean, rstd [cs each]
+    {   // both shard reductions (forward BN stats, backward g-sums) in one pass
+        if (a.bn.sums) {
+            const ShardSrc src[2] = {{a.sums, C, a.sum_shards, 0, C, gs, gs + cs},
+                                     {a.bn.sums, C, a.bn.shards, 0, C, dsm, dsm + cs}};
+            block_shard_sums_n<2>(src);
+        } else {
+            const ShardSrc src[1] = {{a.sums, C, a.sum_shards, 0, C, gs, gs + cs}};
+            block_shard_sums_n<1>(src);
+        }
+        block_bn_finish(a.bn, C, 0, cs, t_sc, t_sc + cs, t_sc + 2 * cs, t_sc + 3 * cs, dsm);
+    }
+    for (int c = threadIdx.x; c < cs; c += blockDim.x) {
+        float coef = 0.f, k1 = 0.f, k2 = 0.f, mean = 0.f, rstd = 1.f;
+        if (c < C) {
+            mean = t_sc[2 * cs + c];
+            rstd = t_sc[3 * cs + c];
+            const float gam = a.bn.gamma ? a.bn.gamma[c] : 1.f;
+            coef = gam * rstd;
+            const double g1 = gs[c], g2 = gs[cs + c];
+            if (a.bn.sums) {   // train mode: batch statistics carry gradient
+                k1 = (float)(g1 / cnt);
+                k2 = (float)(g2 / cnt);
+            }
+            if (blk == 0) {
+                if (a.dbeta) a.dbeta[c] = (float)g1;
+                if (a.dgamma) a.dgamma[c] = (float)g2;
+            }
+        }
+        p[5 * c] = coef; p[5 * c + 1] = k1; p[5 * c + 2] = k2; p[5 * c + 3] = mean; p[5 * c + 4] = rstd;
+    }
+    __syncthreads();
+    const T* G = (const T*)a.g;
+    const T* X = (const T*)a.x;
+    const T* R = (const T*)a.residual;
+    T* DX = (T*)a.dx;
+    const int cpr = cs / CH;
+    const long long nch = a.M * cpr;
+    const long long q0 = blk * (long long)blockDim.x + threadIdx.x, qs = (long long)nblk * blockDim.x;
+    // the grid stride is a multiple of the chunks per pixel in practice: the
+    // channel chunk of a thread is then fixed (no 64-bit modulo per chunk)
+    const bool fixed = qs % cpr == 0;
+    int c0 = (int)(q0 % cpr) * CH;
+    for (long long q = q0; q < nch; q += qs) {
+        const long long o = q * CH;
+        if (!fixed) c0 = (int)(q % cpr) * CH;
+        float g[CH], x[CH], d[CH];
+        unpack(*(const u32x4*)(G + o), g, T());
+        unpack(*(const u32x4*)(X + o), x, T());
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const float* pp = p + 5 * (c0 + j);
+            const float xh = (x[j] - pp[3]) * pp[4];
+            d[j] = pp[0] * (g[j] - pp[1] - xh * pp[2]);
+        }
+        if (R) {
+            float r[CH];
+            unpack(*(const u32x4*)(R + o), r, T());
+#pragma unroll
+            for (int j = 0; j < CH; ++j) d[j] += r[j];
+        }
+        if (a.accumulate) {
+            float r[CH];
+            unpack(*(const u32x4*)(DX + o), r, T());
+#pragma unroll
+            for (int j = 0; j < CH; ++j) d[j] += r[j];
+        }
+        *(u32x4*)(DX + o) = pack(d, T());
+    }
+}
+
 }  // namespace
 
 // deep-scale conv family (conv_deep.hip): number of configurations and the

@@ -17,355 +17,14 @@
 // K (deep K: 3x3 at 256..1024 channels); with WK = 1 the waves split the
 // pixels and each walks all of K (1x1 at small K).  Per-shape configuration:
 // rnvp_deep_auto_cfg, measured with tools/conv_microbench.py.
-#include "common.h"
-#include "conv_common.h"
-
-#include <stdlib.h>
+#include "conv_deep.h"
 
 namespace {
 
-constexpr int DEEP_BM = 64;
-
-// phase stamps for tools/probe/deep_stamps.hip (compiled out of the product)
-#ifdef RNVP_DEEP_STAMPS
-__device__ unsigned long long* g_deep_stamps;
-#define DEEP_STAMP(i) \
-    do { if (threadIdx.x == 0) g_deep_stamps[blockIdx.x * 8 + (i)] = wall_clock64(); } while (0)
-#else
-#define DEEP_STAMP(i) do {} while (0)
-#endif
-constexpr int DEEP_MAX_CS = 1024;    // prologue BN table capacity (channels)
-
-template <typename T>
-__host__ __device__ constexpr int deep_pitch(int cs) { return cs + Mf<T>::CH; }
-
-template <typename T, int BN, int NW, int WK>
-size_t deep_lds_bytes(int cs, int W, int ks) {
-    constexpr int BM = DEEP_BM, TM = BM / 16, WM = NW / WK;
-    constexpr int G = WK > 1 ? TM : WM;
-    const int hal = (ks / 2) * (W + 1), R = BM + 2 * hal;
-    const size_t head = 4 * (5 * (size_t)BN) + 8 * (2 * (size_t)G * BN) + 4 * 2 * (size_t)cs;
-    const size_t zrow = (size_t)deep_pitch<T>(cs) * sizeof(T);
-    size_t act = (size_t)R * deep_pitch<T>(cs) * sizeof(T);
-    const size_t red = WK > 1 ? (size_t)WK * BM * (BN + 4) * 4 : 0;
-    return head + zrow + (act > red ? act : red);
-}
-
 template <typename T, int BN, int KSZ, bool PRO, int NW, int WK, int DK, int NC>
 __global__ __launch_bounds__(64 * NW) void k_conv_deep(rnvp_conv_args a, int shards, int xa, int xb) {
-    constexpr int NT = 64 * NW;
-    constexpr int BM = DEEP_BM;
-    constexpr int CH = Mf<T>::CH, KS = 4 * CH;
-    constexpr int TM = BM / 16, TN = BN / 16;
-    constexpr int WM = NW / WK;
-    constexpr int TMW = TM / WM;                 // 16-pixel fragment rows per wave
-    static_assert(WM * WK == NW && TMW * WM == TM, "wave layout");
-    constexpr int PAD = KSZ / 2;
-    constexpr int RP = BN + 4;                   // partial-tile row pitch (floats)
-    constexpr int G = WK > 1 ? TM : WM;          // stat partial groups per column
-    constexpr int FR = WK > 1 ? (TM * TN) / NW : 1;
-    static_assert(WK == 1 || FR * NW == TM * TN, "final tiles");
-    constexpr int CPT = (DEEP_MAX_CS + NT - 1) / NT;
-    constexpr int SB = (20 * 256) / NT;          // staged chunks per thread per batch
-    constexpr int NSTEP = KSZ * KSZ * NC;        // k-steps of one wave (static: fully unrolled)
     extern __shared__ __attribute__((aligned(16))) char lds[];
-
-    const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wk = wid % WK, wm = wid / WK;
-    const int M = a.B * a.H * a.W, W = a.W, H = a.H;
-    const int N = a.n, cs = a.cs_in;
-    const int gm = (M + BM - 1) / BM;
-    // tiles of one channel block (same weights) are consecutive and share an XCD
-    const int nb = gridDim.x, b = blockIdx.x;
-    const int q8 = nb / 8, r8 = nb % 8, xcd = b % 8;
-    const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
-    // consecutive t share an XCD; tile order: blocks of xa pixel tiles x xb
-    // channel tiles (xa | gm, xb | gn), or channel-major (xa == 0: tiles of one
-    // channel block together) / pixel-major (xa < 0)
-    int mt, nt;
-    if (xa > 0) {
-        const int per = xa * xb, bi = t / per, w = t - bi * per, gmb = gm / xa;
-        const int bm = bi % gmb, bn = bi / gmb;
-        mt = bm * xa + w % xa;
-        nt = bn * xb + w / xa;
-    } else if (xa == 0) {
-        nt = t / gm;
-        mt = t - nt * gm;
-    } else {
-        const int gn = gridDim.x / gm;
-        mt = t / gn;
-        nt = t - mt * gn;
-    }
-    const int m0 = mt * BM, n0 = nt * BN;
-    const T* __restrict__ X = (const T*)a.x;
-    const T* __restrict__ Wt = (const T*)a.w;
-    const bool epi_bn = a.epi_relu_bn_bwd != 0;
-    static_assert(BN <= NT, "bias / table loads: one channel per thread");
-
-    const int hal = PAD * (W + 1);
-    const int R = BM + 2 * hal;
-    const int pitch = deep_pitch<T>(cs);
-    float* etab = (float*)lds;                   // scale | shift | mean | rstd [BN each]
-    float* btab = etab + 4 * BN;                 // bias [BN]
-    double* sred = (double*)(btab + BN);         // [G][BN][2]
-    float* bnp = (float*)(sred + G * BN * 2);    // prologue scale | shift [cs each]
-    T* zrow = (T*)(bnp + 2 * cs);                // [pitch] zeros
-    T* act = zrow + pitch;                       // [R][pitch]; after the K loop: red [WK][BM][RP] f32
-
-    // ---- prologue: every independent load at once (weight ring, BN-table
-    // sums, activation rows), one wait, the transform into LDS ----
-    const int cpr = cs / CH;
-    const int total = R * cpr;
-    const float rcpr = 1.0f / (float)cpr;
-    u32x4 sv[SB];
-    auto stage_load = [&](int q0) {
-#pragma unroll
-        for (int u = 0; u < SB; ++u) {
-            const int q = q0 + u * NT + tid;
-            const int r = fdiv_small(q, rcpr), c = q - r * cpr;
-            const int p = m0 - hal + r;
-            const bool ok = (q < total) & (p >= 0) & (p < M);
-            sv[u] = *(const u32x4*)(X + (ok ? (long long)p * cs + c * CH : 0));
-        }
-    };
-    auto stage_store = [&](int q0) {
-#pragma unroll
-        for (int u = 0; u < SB; ++u) {
-            const int q = q0 + u * NT + tid;
-            if (q >= total) continue;
-            const int r = fdiv_small(q, rcpr), c = q - r * cpr;
-            const int p = m0 - hal + r;
-            u32x4 w = sv[u];
-            if (PRO) {
-                float f[CH];
-                unpack(w, f, T());
-                const int c0 = c * CH;
-#pragma unroll
-                for (int e = 0; e < CH; e += 4) {
-                    const floatx4 sc = *(const floatx4*)&bnp[c0 + e];
-                    const floatx4 sh = *(const floatx4*)&bnp[cs + c0 + e];
-                    f[e] = fmaxf(f[e] * sc.x + sh.x, 0.f);
-                    f[e + 1] = fmaxf(f[e + 1] * sc.y + sh.y, 0.f);
-                    f[e + 2] = fmaxf(f[e + 2] * sc.z + sh.z, 0.f);
-                    f[e + 3] = fmaxf(f[e + 3] * sc.w + sh.w, 0.f);
-                }
-                w = pack(f, T());
-            }
-            const uint32_t keep = (p >= 0 && p < M) ? ~0u : 0u;
-            *(u32x4*)(act + r * pitch + c * CH) = w & u32x4{keep, keep, keep, keep};
-        }
-    };
-    DEEP_STAMP(0);
-    // epilogue elements of this thread: (pixel m, tile column col) of element e
-    constexpr int NE = WK > 1 ? FR : TMW * TN;
-    auto elem = [&](int e, int& m, int& col) {
-        if constexpr (WK > 1) {
-            m = m0 + (wid % TM) * 16 + li;
-            col = ((wid / TM) * FR + e) * 16 + 4 * g;
-        } else {
-            m = m0 + (wm * TMW + e / TN) * 16 + li;
-            col = (e % TN) * 16 + 4 * g;
-        }
-    };
-    const int cso = a.cs_out;
-    // issue order = wait order (vmcnt is in order): the small table / bias /
-    // epilogue operands first, then the activation rows, then the weight ring
-    BnTab<CPT> ptab;
-    BnTab<1> etb;
-    if (PRO) tab_issue<CPT, NT>(a.pro, a.cin, 0, cs, ptab);
-    if (epi_bn) tab_issue<1, NT>(a.epi, N, n0, BN, etb);
-    const float bval = (tid < BN && a.bias && n0 + tid < N) ? a.bias[n0 + tid] : 0.f;
-    EpiPre pre[NE];
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-        int m, col;
-        elem(e, m, col);
-        epi_prefetch<T>(a, (long long)m * cso + n0 + col, m < M && n0 + col < cso, pre[e]);
-    }
-    stage_load(0);
-    const T* wrow[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        // rows >= N (clamped to row 0) only feed output columns that are never stored
-        const int row = n0 + j * 16 + li;
-        wrow[j] = Wt + (long long)(row < N ? row : 0) * a.kp + g * CH;
-    }
-    // wave wk's k-step s: tap s / NC, channel chunk (s % NC) * WK + wk of KS
-    u32x4 rb[DK][TN];
-    auto bload = [&](int st) {   // st is a compile-time constant after unrolling
-        const int tp = st / NC, ch = st - (st / NC) * NC;
-        const int k = tp * cs + (ch * WK + wk) * KS;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) rb[st % DK][j] = *(const u32x4*)(wrow[j] + k);
-    };
-#pragma unroll
-    for (int u = 0; u < DK; ++u)
-        if (u < NSTEP) bload(u);
-    if (PRO) tab_finish<CPT, NT>(a.pro, a.cin, 0, cs, ptab, bnp, bnp + cs, nullptr, nullptr);
-    if (epi_bn) tab_finish<1, NT>(a.epi, N, n0, BN, etb, etab, etab + BN, etab + 2 * BN, etab + 3 * BN);
-    if (tid < BN) btab[tid] = bval;
-    for (int c = tid * CH; c < pitch; c += NT * CH) *(u32x4*)(zrow + c) = u32x4{0u, 0u, 0u, 0u};
-    __syncthreads();
-    DEEP_STAMP(1);
-
-
-    // ---- act(x) rows [m0 - hal, m0 + BM + hal) -> LDS (transformed once) ----
-    stage_store(0);
-    for (int q0 = NT * SB; q0 < total; q0 += NT * SB) {
-        stage_load(q0);
-        stage_store(q0);
-    }
-    __syncthreads();
-    DEEP_STAMP(2);
-
-    // ---- per-lane pixel state of this wave's fragment rows ----
-    int rowoff[TMW];     // LDS element offset of the pixel's own row (+ the lane's k-group)
-    unsigned tvm[TMW];   // bit tap set iff that tap of this output pixel is inside the image
-    const float rW = 1.0f / (float)W, rH = 1.0f / (float)H;
-#pragma unroll
-    for (int i = 0; i < TMW; ++i) {
-        const int lp = (wm * TMW + i) * 16 + li, m = m0 + lp;
-        rowoff[i] = (lp + hal) * pitch + g * CH;
-        const int mm = m < M ? m : 0;
-        const int row = fdiv_small(mm, rW);
-        const int x = mm - row * W, y = row - fdiv_small(row, rH) * H;
-        unsigned bits = 0;
-#pragma unroll
-        for (int tp = 0; tp < KSZ * KSZ; ++tp) {
-            const int yy = y + tp / KSZ - PAD, xx = x + tp % KSZ - PAD;
-            bits |= (unsigned)((m < M) & (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W)) << tp;
-        }
-        tvm[i] = bits;
-    }
-    floatx4 acc[TMW][TN];
-#pragma unroll
-    for (int i = 0; i < TMW; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-    // The whole K sequence of the wave is static (taps x NC channel chunks):
-    // ring slots, tap offsets and the per-tap zero-row select are resolved at
-    // compile time or once per tap, and every A fragment of a step is read
-    // from LDS before its MFMAs.
-#pragma unroll
-    for (int tp = 0; tp < KSZ * KSZ; ++tp) {
-        const int toff = ((tp / KSZ - PAD) * W + (tp % KSZ - PAD)) * pitch + wk * KS;
-        const T* base[TMW];
-#pragma unroll
-        for (int i = 0; i < TMW; ++i) base[i] = ((tvm[i] >> tp) & 1u) ? act + rowoff[i] + toff : zrow;
-#pragma unroll
-        for (int ch = 0; ch < NC; ++ch) {
-            const int st = tp * NC + ch;
-            u32x4 av[TMW];
-#pragma unroll
-            for (int i = 0; i < TMW; ++i) av[i] = *(const u32x4*)(base[i] + ch * WK * KS);
-#pragma unroll
-            for (int i = 0; i < TMW; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j) Mf<T>::step(rb[st % DK][j], av[i], acc[i][j]);
-            // refill this ring slot after its MFMAs (no register copies)
-            if (st + DK < NSTEP) bload(st + DK);
-        }
-    }
-
-    DEEP_STAMP(3);
-    // ---- epilogue ----
-    const bool want_sums = a.out_sums || (epi_bn && a.epi_sums);
-    constexpr int NS = WK > 1 ? FR : TN;          // stat slots (distinct columns) per thread
-    double s1[NS][4], s2[NS][4];
-#pragma unroll
-    for (int f = 0; f < NS; ++f)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s1[f][r] = s2[f][r] = 0.0;
-    const int grp = WK > 1 ? wid % TM : wm;
-    if constexpr (WK > 1) {
-        // sum the WK partial tiles through LDS (aliases the activation tile)
-        float* red = (float*)act;
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < TMW; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-                *(floatx4*)&red[(wk * BM + (wm * TMW + i) * 16 + li) * RP + j * 16 + 4 * g] = acc[i][j];
-        __syncthreads();
-        const int fi = wid % TM;
-#pragma unroll
-        for (int f = 0; f < FR; ++f) {
-            int m, col;
-            elem(f, m, col);
-            const int n = n0 + col;
-            if (m >= M || n >= cso) continue;
-            floatx4 v = *(const floatx4*)&red[(fi * 16 + li) * RP + col];
-#pragma unroll
-            for (int w = 1; w < WK; ++w) v += *(const floatx4*)&red[(w * BM + fi * 16 + li) * RP + col];
-            epi4p<T>(a, (long long)m * cso + n, v, btab + col, epi_bn, etab + col, BN, s1[f], s2[f], N - n, pre[f]);
-        }
-    } else {
-#pragma unroll
-        for (int e = 0; e < NE; ++e) {
-            int m, col;
-            elem(e, m, col);
-            const int n = n0 + col;
-            if (m >= M || n >= cso) continue;
-            epi4p<T>(a, (long long)m * cso + n, acc[e / TN][e % TN], btab + col, epi_bn, etab + col, BN, s1[e % TN],
-                     s2[e % TN], N - n, pre[e]);
-        }
-    }
-    DEEP_STAMP(4);
-    if (want_sums) {
-#pragma unroll
-        for (int f = 0; f < NS; ++f)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const double u1 = row_sum16(s1[f][r]), u2 = row_sum16(s2[f][r]);
-                if (li == 0) {
-                    const int cb = (WK > 1 ? ((wid / TM) * FR + f) : f) * 16 + 4 * g;
-                    sred[(grp * BN + cb + r) * 2] = u1;
-                    sred[(grp * BN + cb + r) * 2 + 1] = u2;
-                }
-            }
-        __syncthreads();
-        double* sums = (epi_bn ? a.epi_sums : a.out_sums) + (long long)(blockIdx.x % shards) * 2 * N;
-        for (int col = tid; col < BN; col += NT) {
-            const int n = n0 + col;
-            if (n >= N) continue;
-            double t1 = 0.0, t2 = 0.0;
-#pragma unroll
-            for (int q = 0; q < G; ++q) {
-                t1 += sred[(q * BN + col) * 2];
-                t2 += sred[(q * BN + col) * 2 + 1];
-            }
-            atomicAdd(&sums[n], t1);
-            atomicAdd(&sums[N + n], t2);
-        }
-    }
-    DEEP_STAMP(5);
-}
-
-// Tile -> XCD order.  Every tile reads its pixel block's activation rows
-// (+ halo) and its channel block's weight rows; the 8 XCD groups of
-// consecutive tiles each hold ~grid/8 tiles, so pick the xa x xb block of
-// pixel x channel tiles (xa | gm, xb | gn, xa * xb = grid / 8) whose unique
-// bytes (xa activation tiles + xb weight slices) are smallest: that is what
-// one XCD's L2 has to bring in.
-inline void xcd_blocks(const rnvp_conv_args* a, int gm, int gn, int bn, int esz, int* xa, int* xb) {
-    static const int mode = [] { const char* e = getenv("RNVP_DEEP_XMAP"); return e ? atoi(e) : 2; }();
-    *xa = mode == 0 ? 0 : -1;
-    *xb = 1;
-    if (mode != 2) return;
-    const long long per = (long long)gm * gn / 8;
-    const int hal = (a->ks / 2) * (a->W + 1);
-    const double act = (double)(DEEP_BM + 2 * hal) * a->cs_in * esz;
-    const double wsl = (double)bn * a->ks * a->ks * a->cs_in * esz;
-    double best = 1e300;
-    for (int x = 1; x <= gm; ++x) {
-        if (gm % x || per % x) continue;
-        const long long y = per / x;
-        if (y < 1 || gn % y) continue;
-        const double bytes = x * act + y * wsl;
-        if (bytes < best) { best = bytes; *xa = x; *xb = (int)y; }
-    }
+    deep_tile<T, BN, KSZ, PRO, NW, WK, DK, NC>(a, shards, xa, xb, blockIdx.x, gridDim.x, lds);
 }
 
 template <typename T, int BN, int NW, int WK, int DK, int NC, int KSZ>

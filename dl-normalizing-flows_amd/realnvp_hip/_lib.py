@@ -48,6 +48,15 @@ class BNBwdArgs(C.Structure):
                 ("dgamma", vp), ("dbeta", vp)]
 
 
+RNVP_STEP_CONV, RNVP_STEP_BN_BWD = 0, 1
+NET_CHAIN_BARRIER_BYTES = 64
+
+
+class NetStep(C.Structure):
+    _fields_ = [("kind", i32), ("conv", ConvArgs), ("bn", BNBwdArgs), ("dgamma_off", i64), ("dbeta_off", i64),
+                ("cfg", i32), ("nc", i32), ("shards", i32), ("xa", i32), ("xb", i32), ("tiles", i32)]
+
+
 class WNDesc(C.Structure):
     _fields_ = [("v", vp), ("g", vp), ("wf", vp), ("wd", vp), ("norm", vp),
                 ("dw", vp), ("dv_off", i64), ("dg_off", i64),
@@ -134,6 +143,8 @@ _SIGS = {
     "rnvp_adam_update": (i32, [vp, vp, vp, vp, i64, vp, i64, f32, f32, f32, f32, f32, vp, f32, vp]),
     "rnvp_step_increment": (i32, [vp, vp]),
     "rnvp_fill_f64": (i32, [vp, i64, f64, vp]),
+    "rnvp_net_chain_prepare": (i32, [vp, i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]),
+    "rnvp_net_chain": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, vp]),
 }
 
 EXPORTED = sorted(_SIGS)
@@ -149,7 +160,7 @@ class _Lib:
             fn.restype = res
             fn.argtypes = args
             raw = name in ("rnvp_version", "rnvp_stat_shards", "rnvp_wgrad_slabs", "rnvp_wgrad_replicas",
-                           "rnvp_weight_norm_tiles") or res is not i32
+                           "rnvp_weight_norm_tiles", "rnvp_net_chain_prepare") or res is not i32
             setattr(self, name[len("rnvp_"):], fn if raw else self._wrap(name, fn))
 
     def _wrap(self, name, fn):

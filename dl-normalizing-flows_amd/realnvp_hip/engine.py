@@ -19,8 +19,8 @@ from collections import OrderedDict
 import torch
 
 from . import _lib
-from ._lib import (BNBwdArgs, BNRunning, BNSrc, ConvArgs, CouplingArgs, WgradConv, WgradGroup, WNDesc, RNVP_BF16,
-                   RNVP_F32, WGRAD_GROUP_MAX)
+from ._lib import (BNBwdArgs, BNRunning, BNSrc, ConvArgs, CouplingArgs, NetStep, WgradConv, WgradGroup, WNDesc,
+                   NET_CHAIN_BARRIER_BYTES, RNVP_BF16, RNVP_F32, RNVP_STEP_BN_BWD, RNVP_STEP_CONV, WGRAD_GROUP_MAX)
 from .net import backward_program, build_program, chan_stride, round_up
 
 BN_EPS = 1e-5
@@ -31,6 +31,9 @@ DTYPES = {"fp32": (RNVP_F32, 4, torch.float32), "bf16": (RNVP_BF16, 2, torch.bfl
 # conv kernel family override for A/B diagnostics (rnvp_conv_args.variant):
 # 0 = per-shape tuned dispatch, 1 = generic LDS-tiled kernels only
 CONV_VARIANT = int(os.environ.get("RNVP_CONV_VARIANT", "0"))
+# persistent net chains (rnvp_net_chain) for runs of deep-scale net steps:
+# opt-in (RNVP_NET_CHAIN=1); measured slower than one launch per step
+NET_CHAIN = int(os.environ.get("RNVP_NET_CHAIN", "0"))
 
 
 def stream_ptr():
@@ -153,6 +156,50 @@ def splitk_workspace(device, elems):
 
 def splitk_elems(M, nmax):
     return 8 * M * nmax if M <= 16384 else 0
+
+
+def plan_chains(steps, device):
+    """Group consecutive net steps (host NetStep structs) into persistent
+    chain launches: the longest run from each position that
+    rnvp_net_chain_prepare accepts (>= 2 steps) becomes one launch, the
+    rest stay single launches.  Returns [("chain", i0, i1, klass, grid, lds,
+    device table) | ("single", i)]."""
+    L = _lib.lib()
+    out = []
+    n = len(steps)
+    i = 0
+    enabled = NET_CHAIN and CONV_VARIANT == 0 and torch.device(device).type == "cuda"
+    while i < n:
+        best = None
+        j = i + 2
+        while enabled and j <= n:
+            arr = (NetStep * (j - i))(*steps[i:j])
+            k, g, lb = C.c_int(), C.c_int(), C.c_int()
+            if L.net_chain_prepare(arr, j - i, C.byref(k), C.byref(g), C.byref(lb)) != 0:
+                break
+            best = (j, arr, k.value, g.value, lb.value)
+            j += 1
+        if best is not None:
+            j, arr, k, g, lb = best
+            out.append(("chain", i, j, k, g, lb, upload(bytes(arr), device)))
+            i = j
+        else:
+            out.append(("single", i))
+            i += 1
+    return out
+
+
+_BARRIERS = {}
+
+
+def chain_barrier(key, device):
+    """Grid-barrier words of one engine's chains (zeroed once; every chain
+    leaves them reusable)."""
+    t = _BARRIERS.get((key, str(device)))
+    if t is None:
+        t = torch.zeros(NET_CHAIN_BARRIER_BYTES // 4, dtype=torch.int32, device=device)
+        _BARRIERS[(key, str(device))] = t
+    return t
 
 
 class CouplingEngine:
@@ -396,10 +443,28 @@ class CouplingEngine:
         key = (ws["key"], bool(training))
         plan = sv.get("fwd_plan")
         if plan is None or plan[0] != key:
-            plan = (key, self._fwd_args(T, sv, ws, training))
+            args = self._fwd_args(T, sv, ws, training)
+            steps = []
+            for a, _, _ in args:
+                st = NetStep()
+                st.kind = RNVP_STEP_CONV
+                st.conv = a
+                steps.append(st)
+            plan = (key, args, plan_chains(steps, sv["arena"].buf.device))
             sv["fwd_plan"] = plan
-        for a, nb, fl in plan[1]:
-            _launch("conv_fwd", nb, fl, L.conv2d, C.byref(a), s)
+        args = plan[1]
+        dt = DTYPES[sv["dtype"]][0]
+        for g in plan[2]:
+            if g[0] == "single":
+                a, nb, fl = args[g[1]]
+                _launch("conv_fwd", nb, fl, L.conv2d, C.byref(a), s)
+            else:
+                _, i0, i1, klass, grid, lds, tab = g
+                nb = sum(args[i][1] for i in range(i0, i1))
+                fl = sum(args[i][2] for i in range(i0, i1))
+                bar = chain_barrier(id(self), tab.device)
+                _launch("net_chain_fwd", nb, fl, L.net_chain, tab.data_ptr(), i1 - i0, dt, klass, grid, lds, None,
+                        bar.data_ptr(), s)
 
     def _fwd_args(self, T, sv, ws, training):
         ar = sv["arena"]
@@ -577,7 +642,8 @@ class CouplingEngine:
                 wg_flops += 2.0 * M * spec.cout * spec.ks * spec.ks * spec.cin
         return items, groups, wg_bytes, wg_flops
 
-    def backward(self, sv, gz, gl_full, gl_sample, grad_block, gx=None, side=None, after=None, zero_at_end=False):
+    def backward(self, sv, gz, gl_full, gl_sample, grad_block, gx=None, side=None, after=None, zero_at_end=False,
+                 defer=None):
         """Returns dL/dx; parameter gradients are written into grad_block
         (flat fp32, zeroed by the caller; scale/shift grads accumulate).
 
@@ -586,6 +652,10 @@ class CouplingEngine:
         never rewritten) output gradients and saved inputs, so they run as
         ONE grouped launch afterwards (partial slabs, no atomics), followed by
         the weight-norm backward that sums the slabs.
+
+        defer: a list that receives the weight-gradient closure instead of
+        running it (it must run before anything rewrites this coupling's
+        scratch, i.e. before its next backward).
 
         zero_at_end: the backward sums are zero on entry (not re-zeroed here)
         and the weight-norm backward launch leaves the forward's batch sums
@@ -638,12 +708,37 @@ class CouplingEngine:
             plan = (key, self._bwd_args(T, sv, sc, ws, training))
             sv["bwd_plan"] = plan
         items, groups, wg_bytes, wg_flops = plan[1]
-        for kind, c, nb, fl, bn in items:
-            if kind == "dgrad":
-                _launch("conv_dgrad", nb, fl, L.conv2d, C.byref(c), s)
+        if len(plan) < 3:
+            steps = []
+            for kind, c, nb, fl, bn in items:
+                st = NetStep()
+                st.dgamma_off = st.dbeta_off = -1
+                if kind == "dgrad":
+                    st.kind = RNVP_STEP_CONV
+                    st.conv = c
+                else:
+                    st.kind = RNVP_STEP_BN_BWD
+                    st.bn = c
+                    st.dgamma_off = self.layout[bn + "weight"][0]
+                    st.dbeta_off = self.layout[bn + "bias"][0]
+                steps.append(st)
+            plan = plan + (plan_chains(steps, x.device),)
+            sv["bwd_plan"] = plan
+        for g in plan[2]:
+            if g[0] == "single":
+                kind, c, nb, fl, bn = items[g[1]]
+                if kind == "dgrad":
+                    _launch("conv_dgrad", nb, fl, L.conv2d, C.byref(c), s)
+                else:
+                    c.dgamma, c.dbeta = gp(bn + "weight"), gp(bn + "bias")
+                    _launch("bn_bwd", nb, 0.0, L.bn_bwd_apply, C.byref(c), s)
             else:
-                c.dgamma, c.dbeta = gp(bn + "weight"), gp(bn + "bias")
-                _launch("bn_bwd", nb, 0.0, L.bn_bwd_apply, C.byref(c), s)
+                _, i0, i1, klass, grid, lds, tab = g
+                nb = sum(items[i][2] for i in range(i0, i1))
+                fl = sum(items[i][3] for i in range(i0, i1))
+                bar = chain_barrier(id(self), tab.device)
+                _launch("net_chain_bwd", nb, fl, L.net_chain, tab.data_ptr(), i1 - i0, dt, klass, grid, lds, gbase,
+                        bar.data_ptr(), s)
         # in_bn backward closes the critical path (dL/dx of the coupling) ...
         a.gh0, a.cs_gh0 = sar.ptr("g:h0"), chan_stride(self.P.buf_ch["h0"])
         a.in_bwd_sums = sar.ptr("in_bwd_sums")
@@ -676,7 +771,11 @@ class CouplingEngine:
             if after is not None:
                 after()
 
-        if side is None:
+        if defer is not None:
+            # the caller issues the weight gradients later (e.g. several
+            # couplings' at once on a side stream: fewer fork edges)
+            defer.append(weight_grads)
+        elif side is None:
             weight_grads()
         else:
             ev = torch.cuda.Event()

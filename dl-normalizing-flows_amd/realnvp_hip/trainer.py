@@ -22,6 +22,7 @@ MI355X-specific structure:
     (train.py:139-154, 249-250 checkpoints).
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -131,6 +132,12 @@ class FlowTrainer:
         # critical path (the forward/data-gradient chain)
         self.overlap = overlap
         self.side = torch.cuda.Stream(device=self.dev) if overlap else None
+        # side_group > 0 (single process, overlap): the weight gradients of
+        # side_group consecutive couplings are forked onto the side stream
+        # together -- one fork edge per group instead of one per coupling
+        # (each cross-stream edge of a replayed HIP graph costs a barrier
+        # packet between hardware queues)
+        self.side_group = int(os.environ.get("RNVP_SIDE_GROUP", "0")) if (overlap and process_group is None) else 0
         self._build_adam_ranges()
         self._build_buckets()
 
@@ -369,6 +376,7 @@ class FlowTrainer:
         L.prior_logprob_bwd(self.z.data_ptr(), self.g_lp.data_ptr(), gz.data_ptr(), B, self.z[0].numel(), s)
         n_coupling = sum(1 for st in self.stages if st[0] == "coupling")
         ci = n_coupling
+        pending = []
         for st in reversed(self.stages):
             if st[0] == "coupling":
                 ci -= 1
@@ -378,7 +386,9 @@ class FlowTrainer:
                     lo, hi = self.adam_ranges[ci]
                     after = (lambda lo=lo, hi=hi: self._adam_range(lo, hi))
                 eng.backward(sv, self._g(z), None, self.g_lp, block, gx=self._g(x), side=self.side, after=after,
-                             zero_at_end=True)
+                             zero_at_end=True, defer=pending if self.side_group else None)
+                if self.side_group and (len(pending) >= self.side_group or ci == 0):
+                    self._flush_side(pending)
                 if self.comm_stream is not None:
                     for lo, hi in self.bucket_after.get(n_coupling - 1 - ci, ()):
                         # the bucket's weight gradients were written on the side
@@ -408,6 +418,16 @@ class FlowTrainer:
                 _, on, off, full = st
                 L.factor_out(self._g(full).data_ptr(), self._g(on).data_ptr(), self._g(off).data_ptr(),
                              *full.shape, s)
+
+    def _flush_side(self, pending):
+        """fork the deferred weight-gradient closures onto the side stream"""
+        ev = torch.cuda.Event()
+        ev.record()
+        self.side.wait_event(ev)
+        with torch.cuda.stream(self.side):
+            for f in pending:
+                f()
+        pending.clear()
 
     def _adam_range(self, lo, hi):
         b1, b2 = self.betas
