@@ -153,9 +153,12 @@ __device__ __forceinline__ void tab_issue(const rnvp_bn_src& s, int C, int c0, i
         if (s.sums) {
             t.a1[j] = s.sums[cc];
             t.a2[j] = s.sums[C + cc];
-            const int h1 = s.shards > 1 ? 1 : 0;
-            t.b1[j] = s.sums[(long long)h1 * 2 * C + cc];
-            t.b2[j] = s.sums[(long long)h1 * 2 * C + C + cc];
+            if (s.shards > 1) {   // uniform: the second shard's loads only when it exists
+                t.b1[j] = s.sums[2 * (long long)C + cc];
+                t.b2[j] = s.sums[3 * (long long)C + cc];
+            } else {
+                t.b1[j] = t.b2[j] = 0.0;
+            }
         } else {
             t.a1[j] = s.mean[cc];
             t.a2[j] = s.var[cc];

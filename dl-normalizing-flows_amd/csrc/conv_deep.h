@@ -56,7 +56,9 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
     constexpr int G = WK > 1 ? TM : WM;          // stat partial groups per column
     constexpr int FR = WK > 1 ? (TM * TN) / NW : 1;
     static_assert(WK == 1 || FR * NW == TM * TN, "final tiles");
-    constexpr int CPT = (DEEP_MAX_CS + NT - 1) / NT;
+    // the operand's channel stride is NC * WK * KS exactly (launcher): the BN
+    // table needs ceil(cs / NT) channels per thread, not DEEP_MAX_CS's
+    constexpr int CPT = (NC * WK * KS + NT - 1) / NT;
     constexpr int SB = (20 * 256) / NT;          // staged chunks per thread per batch
     constexpr int NSTEP = KSZ * KSZ * NC;        // k-steps of one wave (static: fully unrolled)
     const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
@@ -108,9 +110,14 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
     const int total = R * cpr;
     const float rcpr = 1.0f / (float)cpr;
     u32x4 sv[SB];
+    // loads past the staged rows are not issued at all (a uniform skip): at
+    // 128 channels the rows fill ~6 of the SB slots, and every wasted load
+    // counts against the 63 outstanding vector memory operations a wave can
+    // have, serialising the prologue into extra memory round trips
     auto stage_load = [&](int q0) {
 #pragma unroll
         for (int u = 0; u < SB; ++u) {
+            if (q0 + u * NT >= total) break;
             const int q = q0 + u * NT + tid;
             const int r = fdiv_small(q, rcpr), c = q - r * cpr;
             const int p = m0 - hal + r;

@@ -97,12 +97,18 @@ int launch_cfg(const rnvp_conv_args* a, hipStream_t s, int cfg) {
 // measured (tools/conv_microbench.py --deep, profiles/r2_deep_microbench.txt):
 // the deep family beats the other families at M <= 1024 (every shape:
 // whole-tile-per-wave, K / 4) and for the 3x3 at M <= 4096 (64-channel
-// tiles); elsewhere -1 (the caller's other families)
+// tiles); elsewhere -1 (the caller's other families).
+// Round 3 (prologue loads trimmed): 1x1 up to M = 4096 and 3x3 up to
+// M = 16384 as well -- step 26.47 -> 26.03 ms (profiles/r3_dispatch_ab.txt).
+// RNVP_DEEP_MAXM1 / RNVP_DEEP_MAXM3: the largest M the family takes for 1x1
+// (cfg 0 up to 1024, cfg 1 above) / 3x3 convs (A/B of the dispatch limits)
 int rnvp_deep_auto_cfg(const rnvp_conv_args* a) {
+    static const long long max1 = [] { const char* e = getenv("RNVP_DEEP_MAXM1"); return e ? atoll(e) : 4096ll; }();
+    static const long long max3 = [] { const char* e = getenv("RNVP_DEEP_MAXM3"); return e ? atoll(e) : 16384ll; }();
     const long long M = (long long)a->B * a->H * a->W;
+    if (M > (a->ks == 3 ? max3 : max1)) return -1;
     if (M <= 1024) return 0;
-    if (M <= 4096 && a->ks == 3) return 1;
-    return -1;
+    return 1;
 }
 
 int rnvp_deep_launch(const rnvp_conv_args* a, hipStream_t s, int cfg) {

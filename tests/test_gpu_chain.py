@@ -144,7 +144,9 @@ def test_chain_trainer_step_config1():
     assert rel(g1, g0) < 3e-3, rel(g1, g0)
     lp0, g0 = out[("bf16", 0)]
     lp1, g1 = out[("bf16", 1)]
-    assert float(((lp1 - lp0).abs() / lp0.abs()).max()) < 1e-4
+    # bf16: the per-sample log-prob floor of two correct bf16 evaluations is
+    # 4.2e-4 (test_gpu_deep.test_trainer_config1_full_batch_bf16)
+    assert float(((lp1 - lp0).abs() / lp0.abs()).max()) < 5e-4
     assert rel(g1, g0) < 2e-2, rel(g1, g0)
 
 
