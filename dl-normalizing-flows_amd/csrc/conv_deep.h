@@ -106,50 +106,46 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
 
     // ---- prologue: every independent load at once (weight ring, BN-table
     // sums, activation rows), one wait, the transform into LDS ----
-    const int cpr = cs / CH;
-    const int total = R * cpr;
-    const float rcpr = 1.0f / (float)cpr;
+    // the channel stride is NC * WK * KS (launcher), so a row is CPR chunks
+    // and NT % CPR == 0: a thread's chunk column is the same in every staged
+    // row -- its BN coefficients are loaded into registers once, and its rows
+    // advance by NT / CPR per slot
+    constexpr int CPR = NC * WK * 4;
+    static_assert(NT % CPR == 0, "fixed chunk column per thread");
+    constexpr int RSTEP = NT / CPR;
+    const int cfix = tid % CPR, rbase = tid / CPR;
     u32x4 sv[SB];
     // loads past the staged rows are not issued at all (a uniform skip): at
     // 128 channels the rows fill ~6 of the SB slots, and every wasted load
     // counts against the 63 outstanding vector memory operations a wave can
     // have, serialising the prologue into extra memory round trips
-    auto stage_load = [&](int q0) {
+    auto stage_load = [&](int r0) {
 #pragma unroll
         for (int u = 0; u < SB; ++u) {
-            if (q0 + u * NT >= total) break;
-            const int q = q0 + u * NT + tid;
-            const int r = fdiv_small(q, rcpr), c = q - r * cpr;
+            if (r0 + u * RSTEP >= R) break;
+            const int r = r0 + rbase + u * RSTEP;
             const int p = m0 - hal + r;
-            const bool ok = (q < total) & (p >= 0) & (p < M);
-            sv[u] = *(const u32x4*)(X + (ok ? (long long)p * cs + c * CH : 0));
+            const bool ok = (r < R) & (p >= 0) & (p < M);
+            sv[u] = *(const u32x4*)(X + (ok ? (long long)p * cs + cfix * CH : 0));
         }
     };
-    auto stage_store = [&](int q0) {
+    float scv[CH], shv[CH];
+    auto stage_store = [&](int r0) {
 #pragma unroll
         for (int u = 0; u < SB; ++u) {
-            const int q = q0 + u * NT + tid;
-            if (q >= total) continue;
-            const int r = fdiv_small(q, rcpr), c = q - r * cpr;
+            const int r = r0 + rbase + u * RSTEP;
+            if (r >= R) continue;
             const int p = m0 - hal + r;
             u32x4 w = sv[u];
             if (PRO) {
                 float f[CH];
                 unpack(w, f, T());
-                const int c0 = c * CH;
 #pragma unroll
-                for (int e = 0; e < CH; e += 4) {
-                    const floatx4 sc = *(const floatx4*)&bnp[c0 + e];
-                    const floatx4 sh = *(const floatx4*)&bnp[cs + c0 + e];
-                    f[e] = fmaxf(f[e] * sc.x + sh.x, 0.f);
-                    f[e + 1] = fmaxf(f[e + 1] * sc.y + sh.y, 0.f);
-                    f[e + 2] = fmaxf(f[e + 2] * sc.z + sh.z, 0.f);
-                    f[e + 3] = fmaxf(f[e + 3] * sc.w + sh.w, 0.f);
-                }
+                for (int e = 0; e < CH; ++e) f[e] = fmaxf(f[e] * scv[e] + shv[e], 0.f);
                 w = pack(f, T());
             }
             const uint32_t keep = (p >= 0 && p < M) ? ~0u : 0u;
-            *(u32x4*)(act + r * pitch + c * CH) = w & u32x4{keep, keep, keep, keep};
+            *(u32x4*)(act + r * pitch + cfix * CH) = w & u32x4{keep, keep, keep, keep};
         }
     };
     DEEP_STAMP(0);
@@ -204,13 +200,19 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
     for (int c = tid * CH; c < pitch; c += NT * CH) *(u32x4*)(zrow + c) = u32x4{0u, 0u, 0u, 0u};
     __syncthreads();
     DEEP_STAMP(1);
-
+    if (PRO) {
+#pragma unroll
+        for (int e = 0; e < CH; ++e) {
+            scv[e] = bnp[cfix * CH + e];
+            shv[e] = bnp[cs + cfix * CH + e];
+        }
+    }
 
     // ---- act(x) rows [m0 - hal, m0 + BM + hal) -> LDS (transformed once) ----
     stage_store(0);
-    for (int q0 = NT * SB; q0 < total; q0 += NT * SB) {
-        stage_load(q0);
-        stage_store(q0);
+    for (int r0 = RSTEP * SB; r0 < R; r0 += RSTEP * SB) {
+        stage_load(r0);
+        stage_store(r0);
     }
     __syncthreads();
     DEEP_STAMP(2);
