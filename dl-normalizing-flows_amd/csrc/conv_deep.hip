@@ -65,7 +65,7 @@ int launch_deep(const rnvp_conv_args* a, hipStream_t s) {
         }
         return RNVP_E_UNSUPPORTED;
     }
-    if constexpr (WK == 4) {   // 3x3: whole-tile-per-wave configurations only
+    if constexpr (WK == NW) {   // 3x3: whole-tile-per-wave configurations only
         switch (nc) {
             case 1: return launch_deep_nc<T, BN, NW, WK, DK, 1, 3>(a, s);
             case 2: return launch_deep_nc<T, BN, NW, WK, DK, 2, 3>(a, s);
@@ -81,6 +81,8 @@ int launch_deep(const rnvp_conv_args* a, hipStream_t s) {
 // cfg 1                 64   4   4   6   whole 64x64 tile per wave, K / 4
 // cfg 2                 64   4   1   8   16-pixel quarters, all of K (1x1, small K)
 // cfg 3                 32   4   2   8   32-pixel halves x K / 2
+// cfg 4                 32   8   8   8   cfg 0 with 8 waves (two per SIMD: one's memory waits under the other's MFMAs)
+// cfg 5                 64   8   8   6   cfg 1 with 8 waves
 template <typename T>
 int launch_cfg(const rnvp_conv_args* a, hipStream_t s, int cfg) {
     switch (cfg) {
@@ -88,6 +90,8 @@ int launch_cfg(const rnvp_conv_args* a, hipStream_t s, int cfg) {
         case 1: return launch_deep<T, 64, 4, 4, 6>(a, s);
         case 2: return a->ks == 1 ? launch_deep<T, 64, 4, 1, 8>(a, s) : RNVP_E_UNSUPPORTED;
         case 3: return a->ks == 1 ? launch_deep<T, 32, 4, 2, 8>(a, s) : RNVP_E_UNSUPPORTED;
+        case 4: return launch_deep<T, 32, 8, 8, 8>(a, s);
+        case 5: return launch_deep<T, 64, 8, 8, 6>(a, s);
     }
     return RNVP_E_INVALID;
 }
@@ -107,8 +111,15 @@ int rnvp_deep_auto_cfg(const rnvp_conv_args* a) {
     static const long long max3 = [] { const char* e = getenv("RNVP_DEEP_MAXM3"); return e ? atoll(e) : 16384ll; }();
     const long long M = (long long)a->B * a->H * a->W;
     if (M > (a->ks == 3 ? max3 : max1)) return -1;
-    if (M <= 1024) return 0;
-    return 1;
+    // per-shape choice from tools/conv_microbench.py --deep
+    // (profiles/r3_deep_microbench_cfgs.txt): the 8-wave tiles at M <= 1024;
+    // 32-channel tiles for the data gradients above (more workgroups); the
+    // 8-wave 64-channel tile for the forward convs at 256+ channels
+    const bool dgrad = a->epi_relu_bn_bwd || (!a->pro_bn_relu && !a->out_sums);
+    const int kc = a->dtype == RNVP_F32 ? 16 : 32;   // channels per k-step
+    if (M <= 1024) return a->cs_in % (8 * kc) == 0 ? 4 : 0;
+    if (dgrad) return 0;
+    return a->cs_in % (8 * kc) == 0 ? 5 : 1;
 }
 
 int rnvp_deep_launch(const rnvp_conv_args* a, hipStream_t s, int cfg) {

@@ -332,7 +332,7 @@ DEEP_FAMILY = DEEP + [
     ("s4_3x3_ragged_m", 3, 7, 9, 256, 200, 3, dict(pro=True, stats=True)),                # M % 64 != 0, N % 64 != 0
     ("s2_1x1_64", 8, 32, 32, 64, 64, 1, dict(pro=True, residual=True, stats=True)),
 ]
-DEEP_CFGS = 4
+DEEP_CFGS = 6
 VARIANT_DEEP0 = 16
 
 

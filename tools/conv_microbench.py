@@ -161,7 +161,7 @@ def main():
     torch.manual_seed(0)
     variants = [0, 1] if "--v01" in sys.argv else [0]
     if "--deep" in sys.argv:   # the deep-scale family's configurations (RNVP_VARIANT_DEEP0 + c)
-        variants = [0] + [16 + c for c in range(4)]
+        variants = [0] + [16 + c for c in range(6)]
     only = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--case=")]
     print("%-32s %3s %9s %9s %9s" % ("case", "var", "us", "GB/s", "TFLOP/s"))
     for name, B, H, W, ci, co, ks, fl in CASES:

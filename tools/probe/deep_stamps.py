@@ -84,7 +84,7 @@ CASES = [
 
 if __name__ == "__main__":
     for name, B, H, W, ci, co, ks, fl in CASES:
-        for cfg in (0, 1, 2, 3):
+        for cfg in (0, 1, 2, 3, 4, 5):
             try:
                 case(name, B, H, W, ci, co, ks, cfg, **fl)
             except AssertionError:
