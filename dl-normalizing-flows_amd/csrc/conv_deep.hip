@@ -96,7 +96,147 @@ int launch_cfg(const rnvp_conv_args* a, hipStream_t s, int cfg) {
     return RNVP_E_INVALID;
 }
 
+// ---------------------------------------------------------------------------
+// grouped independent 1x1 convs: one launch, the convs' tiles concatenated
+// (block b -> the conv whose tile range holds b; every conv keeps its own
+// XCD-aware tile order).  Both prologue forms are compiled in.
+template <typename T, int BN, int NW, int WK, int DK, int NC>
+__global__ __launch_bounds__(64 * NW) void k_net_group(const rnvp_net_step* __restrict__ steps, int n) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    int b = blockIdx.x, c = 0;
+    while (c + 1 < n && b >= steps[c].tiles) {   // uniform scan over <= RNVP_NET_GROUP_MAX tile counts
+        b -= steps[c].tiles;
+        ++c;
+    }
+    const rnvp_net_step& st = steps[c];
+    if (st.conv.pro_bn_relu)
+        deep_tile<T, BN, 1, true, NW, WK, DK, NC>(st.conv, st.shards, st.xa, st.xb, b, st.tiles, lds);
+    else
+        deep_tile<T, BN, 1, false, NW, WK, DK, NC>(st.conv, st.shards, st.xa, st.xb, b, st.tiles, lds);
+}
+
+using GroupKernel = void (*)(const rnvp_net_step*, int);
+
+template <typename T, int BN, int NW, int WK, int DK>
+GroupKernel group_kernel_nc(int nc) {
+    switch (nc) {
+        case 1: return k_net_group<T, BN, NW, WK, DK, 1>;
+        case 2: return k_net_group<T, BN, NW, WK, DK, 2>;
+        case 4: return k_net_group<T, BN, NW, WK, DK, 4>;
+        case 8: return k_net_group<T, BN, NW, WK, DK, 8>;
+        case 16: return k_net_group<T, BN, NW, WK, DK, 16>;
+    }
+    return nullptr;
+}
+
+// the configuration table of launch_cfg (cfg 0 / 1 / 4 / 5)
+template <typename T>
+GroupKernel group_kernel_t(int cfg, int nc) {
+    switch (cfg) {
+        case 0: return group_kernel_nc<T, 32, 4, 4, 8>(nc);
+        case 1: return group_kernel_nc<T, 64, 4, 4, 6>(nc);
+        case 4: return group_kernel_nc<T, 32, 8, 8, 8>(nc);
+        case 5: return group_kernel_nc<T, 64, 8, 8, 6>(nc);
+    }
+    return nullptr;
+}
+
+// klass = cfg | nc << 4
+GroupKernel group_kernel(int dtype, int klass) {
+    const int cfg = klass & 15, nc = klass >> 4;
+    return dtype == RNVP_F32 ? group_kernel_t<float>(cfg, nc) : group_kernel_t<bf16_t>(cfg, nc);
+}
+
+struct GroupCfg { int bn, nw, wk; };
+inline GroupCfg group_cfg_shape(int cfg) {
+    switch (cfg) {
+        case 0: return {32, 4, 4};
+        case 1: return {64, 4, 4};
+        case 4: return {32, 8, 8};
+        default: return {64, 8, 8};
+    }
+}
+
 }  // namespace
+
+// Grouped 1x1 convs: the group's configuration follows the single-launch
+// choice (rnvp_deep_auto_cfg's policy, extended to M <= 16384 for 1x1)
+extern "C" int rnvp_net_group_prepare(rnvp_net_step* steps, int n, int* klass, int* grid, int* lds_bytes) {
+    if (!steps || n <= 0 || n > RNVP_NET_GROUP_MAX || !klass || !grid || !lds_bytes) return RNVP_E_INVALID;
+    const rnvp_conv_args& a0 = steps[0].conv;
+    const long long M = (long long)a0.B * a0.H * a0.W;
+    if (M <= 0 || M > 16384) return RNVP_E_UNSUPPORTED;
+    if (a0.dtype != RNVP_F32 && a0.dtype != RNVP_BF16) return RNVP_E_INVALID;
+    const int kc = a0.dtype == RNVP_F32 ? 16 : 32;   // channels per k-step
+    int cfg = -1, nc = -1;
+    long long tiles = 0;
+    size_t lds = 0;
+    for (int i = 0; i < n; ++i) {
+        rnvp_net_step& st = steps[i];
+        const rnvp_conv_args& a = st.conv;
+        if (st.kind != RNVP_STEP_CONV || a.ks != 1) return RNVP_E_UNSUPPORTED;
+        if (a.dtype != a0.dtype || a.B != a0.B || a.H != a0.H || a.W != a0.W) return RNVP_E_UNSUPPORTED;
+        if (!a.x || !a.w || !a.y || a.n <= 0 || a.cin <= 0 || (a.cs_in & 7) || (a.cs_out & 7)) return RNVP_E_INVALID;
+        if (a.cs_in < a.cin || a.cs_out < a.n || (a.kp & 63) || a.kp < a.cs_in) return RNVP_E_INVALID;
+        if (((uintptr_t)a.x & 15) || ((uintptr_t)a.w & 15)) return RNVP_E_INVALID;
+        if (a.epi_relu_bn_bwd && !a.epi_x) return RNVP_E_INVALID;
+        if (a.pro_bn_relu && a.pro.sums && a.pro.shards > 2) return RNVP_E_UNSUPPORTED;
+        if (a.epi_relu_bn_bwd && a.epi.sums && a.epi.shards > 2) return RNVP_E_UNSUPPORTED;
+        // one configuration for the whole group: the policy of its first conv
+        const rnvp_conv_args& f = steps[0].conv;
+        const bool dgrad = f.epi_relu_bn_bwd || (!f.pro_bn_relu && !f.out_sums);
+        int c;
+        if (M <= 1024) c = f.cs_in % (8 * kc) == 0 ? 4 : 0;
+        else if (dgrad) c = 0;
+        else c = f.cs_in % (8 * kc) == 0 ? 5 : 1;
+        const GroupCfg g = group_cfg_shape(c);
+        if (a.cs_in % (g.wk * kc) || a.cs_in > DEEP_MAX_CS || a.n < g.bn / 2) return RNVP_E_UNSUPPORTED;
+        const int ncv = a.cs_in / (g.wk * kc);
+        if (ncv != 1 && ncv != 2 && ncv != 4 && ncv != 8 && ncv != 16) return RNVP_E_UNSUPPORTED;
+        if (i == 0) {
+            cfg = c;
+            nc = ncv;
+        } else if (c != cfg || ncv != nc) {
+            return RNVP_E_UNSUPPORTED;
+        }
+        const size_t shm = a0.dtype == RNVP_F32
+                               ? (g.nw == 8 ? (g.bn == 32 ? deep_lds_bytes<float, 32, 8, 8>(a.cs_in, a.W, 1)
+                                                          : deep_lds_bytes<float, 64, 8, 8>(a.cs_in, a.W, 1))
+                                            : (g.bn == 32 ? deep_lds_bytes<float, 32, 4, 4>(a.cs_in, a.W, 1)
+                                                          : deep_lds_bytes<float, 64, 4, 4>(a.cs_in, a.W, 1)))
+                               : (g.nw == 8 ? (g.bn == 32 ? deep_lds_bytes<bf16_t, 32, 8, 8>(a.cs_in, a.W, 1)
+                                                          : deep_lds_bytes<bf16_t, 64, 8, 8>(a.cs_in, a.W, 1))
+                                            : (g.bn == 32 ? deep_lds_bytes<bf16_t, 32, 4, 4>(a.cs_in, a.W, 1)
+                                                          : deep_lds_bytes<bf16_t, 64, 4, 4>(a.cs_in, a.W, 1)));
+        if (shm > 160 * 1024) return RNVP_E_UNSUPPORTED;
+        if (shm > lds) lds = shm;
+        const long long gm = (M + DEEP_BM - 1) / DEEP_BM, gn = (a.n + g.bn - 1) / g.bn;
+        st.cfg = c;
+        st.nc = ncv;
+        st.shards = rnvp_stat_shards(M);
+        st.tiles = (int)(gm * gn);
+        xcd_blocks(&a, (int)gm, (int)gn, g.bn, a0.dtype == RNVP_F32 ? 4 : 2, &st.xa, &st.xb);
+        tiles += st.tiles;
+    }
+    if (tiles <= 0 || tiles >= (1ll << 31)) return RNVP_E_INVALID;
+    *klass = cfg | (nc << 4);
+    *grid = (int)tiles;
+    *lds_bytes = (int)lds;
+    return group_kernel(a0.dtype, *klass) ? RNVP_OK : RNVP_E_UNSUPPORTED;
+}
+
+extern "C" int rnvp_net_group(const rnvp_net_step* steps, int n, int dtype, int klass, int grid, int lds_bytes,
+                              void* stream) {
+    if (!steps || n <= 0 || n > RNVP_NET_GROUP_MAX || grid <= 0 || lds_bytes < 0 || lds_bytes > 160 * 1024)
+        return RNVP_E_INVALID;
+    if (dtype != RNVP_F32 && dtype != RNVP_BF16) return RNVP_E_INVALID;
+    const GroupKernel k = group_kernel(dtype, klass);
+    if (!k) return RNVP_E_INVALID;
+    const int nw = group_cfg_shape(klass & 15).nw;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(64 * nw), lds_bytes, (hipStream_t)stream, steps, n);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
 
 // measured (tools/conv_microbench.py --deep, profiles/r2_deep_microbench.txt):
 // the deep family beats the other families at M <= 1024 (every shape:

@@ -50,6 +50,7 @@ class BNBwdArgs(C.Structure):
 
 RNVP_STEP_CONV, RNVP_STEP_BN_BWD = 0, 1
 NET_CHAIN_BARRIER_BYTES = 64
+NET_GROUP_MAX = 8
 
 
 class NetStep(C.Structure):
@@ -145,6 +146,8 @@ _SIGS = {
     "rnvp_fill_f64": (i32, [vp, i64, f64, vp]),
     "rnvp_net_chain_prepare": (i32, [vp, i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]),
     "rnvp_net_chain": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, vp]),
+    "rnvp_net_group_prepare": (i32, [vp, i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]),
+    "rnvp_net_group": (i32, [vp, i32, i32, i32, i32, i32, vp]),
 }
 
 EXPORTED = sorted(_SIGS)
@@ -160,7 +163,8 @@ class _Lib:
             fn.restype = res
             fn.argtypes = args
             raw = name in ("rnvp_version", "rnvp_stat_shards", "rnvp_wgrad_slabs", "rnvp_wgrad_replicas",
-                           "rnvp_weight_norm_tiles", "rnvp_net_chain_prepare") or res is not i32
+                           "rnvp_weight_norm_tiles", "rnvp_net_chain_prepare",
+                           "rnvp_net_group_prepare") or res is not i32
             setattr(self, name[len("rnvp_"):], fn if raw else self._wrap(name, fn))
 
     def _wrap(self, name, fn):

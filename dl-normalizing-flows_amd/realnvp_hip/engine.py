@@ -20,7 +20,7 @@ import torch
 
 from . import _lib
 from ._lib import (BNBwdArgs, BNRunning, BNSrc, ConvArgs, CouplingArgs, NetStep, WgradConv, WgradGroup, WNDesc,
-                   NET_CHAIN_BARRIER_BYTES, RNVP_BF16, RNVP_F32, RNVP_STEP_BN_BWD, RNVP_STEP_CONV, WGRAD_GROUP_MAX)
+                   NET_CHAIN_BARRIER_BYTES, NET_GROUP_MAX, RNVP_BF16, RNVP_F32, RNVP_STEP_BN_BWD, RNVP_STEP_CONV, WGRAD_GROUP_MAX)
 from .net import backward_program, build_program, chan_stride, round_up
 
 BN_EPS = 1e-5
@@ -34,6 +34,9 @@ CONV_VARIANT = int(os.environ.get("RNVP_CONV_VARIANT", "0"))
 # persistent net chains (rnvp_net_chain) for runs of deep-scale net steps:
 # opt-in (RNVP_NET_CHAIN=1); measured slower than one launch per step
 NET_CHAIN = int(os.environ.get("RNVP_NET_CHAIN", "0"))
+# grouped launches of independent 1x1 convs (rnvp_net_group); RNVP_NET_GROUP=0
+# launches them one by one
+NET_GROUP = int(os.environ.get("RNVP_NET_GROUP", "1"))
 
 
 def stream_ptr():
@@ -158,18 +161,52 @@ def splitk_elems(M, nmax):
     return 8 * M * nmax if M <= 16384 else 0
 
 
-def plan_chains(steps, device):
-    """Group consecutive net steps (host NetStep structs) into persistent
-    chain launches: the longest run from each position that
-    rnvp_net_chain_prepare accepts (>= 2 steps) becomes one launch, the
-    rest stay single launches.  Returns [("chain", i0, i1, klass, grid, lds,
-    device table) | ("single", i)]."""
+def _independent(rw, members, j):
+    """step j neither reads nor writes what the group members write, and
+    writes nothing they read"""
+    rj, wj = rw[j]
+    for m in members:
+        rm, wm = rw[m]
+        if (wj & (rm | wm)) or (rj & wm):
+            return False
+    return True
+
+
+def plan_chains(steps, device, rw=None):
+    """Plan the launches of consecutive net steps (host NetStep structs):
+      * grouped launches (rnvp_net_group): a run of mutually independent 1x1
+        convs (rw[i] = (buffers read, buffers written) of step i) that
+        rnvp_net_group_prepare accepts becomes one launch;
+      * persistent chains (rnvp_net_chain, opt-in): the longest run from a
+        position that rnvp_net_chain_prepare accepts;
+      * the rest stay single launches.
+    Returns [("group" | "chain", i0, i1, klass, grid, lds, device table) |
+    ("single", i)]."""
     L = _lib.lib()
     out = []
     n = len(steps)
     i = 0
-    enabled = NET_CHAIN and CONV_VARIANT == 0 and torch.device(device).type == "cuda"
+    cuda = CONV_VARIANT == 0 and torch.device(device).type == "cuda"
+    enabled = NET_CHAIN and cuda
+    grouping = NET_GROUP and cuda and rw is not None
     while i < n:
+        if grouping:
+            members = [i]
+            best = None
+            j = i + 1
+            while j < n and len(members) < NET_GROUP_MAX and _independent(rw, members, j):
+                arr = (NetStep * (j + 1 - i))(*steps[i:j + 1])
+                k, g, lb = C.c_int(), C.c_int(), C.c_int()
+                if L.net_group_prepare(arr, j + 1 - i, C.byref(k), C.byref(g), C.byref(lb)) != 0:
+                    break
+                members.append(j)
+                best = (j + 1, arr, k.value, g.value, lb.value)
+                j += 1
+            if best is not None:
+                j, arr, k, g, lb = best
+                out.append(("group", i, j, k, g, lb, upload(bytes(arr), device)))
+                i = j
+                continue
         best = None
         j = i + 2
         while enabled and j <= n:
@@ -444,13 +481,16 @@ class CouplingEngine:
         plan = sv.get("fwd_plan")
         if plan is None or plan[0] != key:
             args = self._fwd_args(T, sv, ws, training)
-            steps = []
-            for a, _, _ in args:
+            steps, rw = [], []
+            for (a, _, _), op in zip(args, self.P.ops):
                 st = NetStep()
                 st.kind = RNVP_STEP_CONV
                 st.conv = a
                 steps.append(st)
-            plan = (key, args, plan_chains(steps, sv["arena"].buf.device))
+                reads = {op.x} | ({op.residual} if op.residual else set()) | ({op.y} if op.accumulate else set())
+                reads |= {"s:" + op.pro_bn} if op.pro_bn else set()
+                rw.append((reads, {op.y} | ({"s:" + op.stats_bn} if op.stats_bn else set())))
+            plan = (key, args, plan_chains(steps, sv["arena"].buf.device, rw))
             sv["fwd_plan"] = plan
         args = plan[1]
         dt = DTYPES[sv["dtype"]][0]
@@ -458,6 +498,11 @@ class CouplingEngine:
             if g[0] == "single":
                 a, nb, fl = args[g[1]]
                 _launch("conv_fwd", nb, fl, L.conv2d, C.byref(a), s)
+            elif g[0] == "group":
+                _, i0, i1, klass, grid, lds, tab = g
+                nb = sum(args[i][1] for i in range(i0, i1))
+                fl = sum(args[i][2] for i in range(i0, i1))
+                _launch("conv_fwd", nb, fl, L.net_group, tab.data_ptr(), i1 - i0, dt, klass, grid, lds, s)
             else:
                 _, i0, i1, klass, grid, lds, tab = g
                 nb = sum(args[i][1] for i in range(i0, i1))
@@ -709,20 +754,29 @@ class CouplingEngine:
             sv["bwd_plan"] = plan
         items, groups, wg_bytes, wg_flops = plan[1]
         if len(plan) < 3:
-            steps = []
-            for kind, c, nb, fl, bn in items:
+            steps, rw = [], []
+            bsteps = [st for st in self.steps if st.kind != "wgrad"]
+            for (kind, c, nb, fl, bn), bst in zip(items, bsteps):
                 st = NetStep()
                 st.dgamma_off = st.dbeta_off = -1
+                op = bst.op
+                dst = bst.tmp if (kind == "dgrad" and bst.tmp) else bst.gx
+                reads = ({bst.residual} if bst.residual else set()) | ({dst} if bst.accumulate else set())
                 if kind == "dgrad":
                     st.kind = RNVP_STEP_CONV
                     st.conv = c
+                    reads |= {bst.gy} | ({op.x} if op.pro_bn else set())
+                    writes = {dst} | ({"e:" + op.pro_bn} if op.pro_bn else set())
                 else:
                     st.kind = RNVP_STEP_BN_BWD
                     st.bn = c
                     st.dgamma_off = self.layout[bn + "weight"][0]
                     st.dbeta_off = self.layout[bn + "bias"][0]
+                    reads |= {bst.tmp, op.x, "e:" + bn}
+                    writes = {dst}
                 steps.append(st)
-            plan = plan + (plan_chains(steps, x.device),)
+                rw.append((reads, writes))
+            plan = plan + (plan_chains(steps, x.device, rw),)
             sv["bwd_plan"] = plan
         for g in plan[2]:
             if g[0] == "single":
@@ -732,6 +786,11 @@ class CouplingEngine:
                 else:
                     c.dgamma, c.dbeta = gp(bn + "weight"), gp(bn + "bias")
                     _launch("bn_bwd", nb, 0.0, L.bn_bwd_apply, C.byref(c), s)
+            elif g[0] == "group":
+                _, i0, i1, klass, grid, lds, tab = g
+                nb = sum(items[i][2] for i in range(i0, i1))
+                fl = sum(items[i][3] for i in range(i0, i1))
+                _launch("conv_dgrad", nb, fl, L.net_group, tab.data_ptr(), i1 - i0, dt, klass, grid, lds, s)
             else:
                 _, i0, i1, klass, grid, lds, tab = g
                 nb = sum(items[i][2] for i in range(i0, i1))

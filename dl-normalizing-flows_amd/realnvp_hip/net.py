@@ -176,13 +176,27 @@ def backward_program(P: NetProgram) -> List[BwdStep]:
         written.add(dst)
         return acc, res
 
-    for op in reversed(P.ops):
+    order = list(reversed(P.ops))
+    if "out" in P.buf_ch:
+        # skip architecture: once the out_block's backward has made d out
+        # complete, the data gradients of in_skip and every core_skips[i]
+        # (all read d out) come next -- independent of each other, so the
+        # engine runs them as one grouped launch; the blocks' chain follows
+        # and accumulates onto what they wrote
+        head = [op for op in order if op.x == "out"]
+        skips = [op for op in order if op.y == "out"]
+        order = head + skips + [op for op in order if op.x != "out" and op.y != "out"]
+    for op in order:
         gy = "g:" + op.y
         gx = "g:" + op.x
         if op.residual is not None:
+            # folded into the NEXT write of the residual's gradient (a first
+            # write or an accumulation: with the skip data gradients hoisted,
+            # g:x1_i already holds core_skips[i-1]'s part when block i's
+            # residual is registered); gy is complete by then
             gr = "g:" + op.residual
-            if gr in written:
-                raise NotImplementedError("residual into an already-written gradient")
+            if gr in pending:
+                raise NotImplementedError("two residuals into one gradient")
             pending[gr] = gy
         if op.pro_bn is not None:
             steps.append(BwdStep("dgrad", op, gy, gx=None, tmp="gtmp"))

@@ -346,6 +346,23 @@ int rnvp_net_chain_prepare(rnvp_net_step* steps_host, int n, int* klass, int* gr
 int rnvp_net_chain(const rnvp_net_step* steps_device, int n, int dtype, int klass, int grid, int lds_bytes,
                    float* grad_base, void* barrier, void* stream);
 
+/* ---- grouped 1x1 convs --------------------------------------------------
+ * Up to RNVP_NET_GROUP_MAX INDEPENDENT 1x1 convs of one net (same pixels; no
+ * conv reads what another writes) in ONE launch: the workgroups of all of
+ * them share the grid, so one conv's memory waits overlap another's MFMAs
+ * and the kernel boundaries between them disappear.  Used for the skip convs
+ * of ResidualModule (modules_realnvp.py:184-189): each core_skips[i] forward
+ * runs beside the next block's first 1x1, and the data gradients of
+ * in_skip + every core_skips[i] (all read d out) run as one launch.
+ * Steps are rnvp_net_step with kind RNVP_STEP_CONV (rnvp_conv2d semantics,
+ * with or without the BN prologue).  rnvp_net_group_prepare (host) validates
+ * and fills the derived fields (RNVP_E_UNSUPPORTED: no grouped form -- launch
+ * them one by one); rnvp_net_group launches the device copy. */
+#define RNVP_NET_GROUP_MAX 8
+int rnvp_net_group_prepare(rnvp_net_step* steps_host, int n, int* klass, int* grid, int* lds_bytes);
+int rnvp_net_group(const rnvp_net_step* steps_device, int n, int dtype, int klass, int grid, int lds_bytes,
+                   void* stream);
+
 /* misc */
 int rnvp_fill_f64(double* p, long long n, double v, void* stream);
 

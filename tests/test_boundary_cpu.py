@@ -113,6 +113,23 @@ def test_backward_program_is_well_formed():
                     if s.gx:
                         written.add(s.gx)
                 assert "g:h0" in written
+                # ... and COMPLETE: every contribution to d b (the data
+                # gradient of each op reading b, the identity path of each
+                # residual add onto b) is in before any step reads it (the skip
+                # data gradients run early, block residuals fold into later writes)
+                want = {}
+                for op in P.ops:
+                    want["g:" + op.x] = want.get("g:" + op.x, 0) + 1
+                    if op.residual:
+                        want["g:" + op.residual] = want.get("g:" + op.residual, 0) + 1
+                have = {"g:st": 0}
+                want["g:st"] = 0
+                for s in steps:
+                    for src in ([s.gy] if s.kind in ("dgrad", "wgrad") else []) + ([s.residual] if s.residual else []):
+                        assert have.get(src, 0) == want.get(src, 0), (rb, bott, skip, src, s)
+                    if s.gx and s.kind in ("dgrad", "bn_apply"):
+                        have[s.gx] = have.get(s.gx, 0) + 1 + (1 if s.residual else 0)
+                assert have["g:h0"] == want["g:h0"]
 
 
 def test_reference_train_py_import_line():

@@ -67,14 +67,14 @@ def _run_coupling(kind, cio, mid, size, B, dtype, chain, seed=0):
 
 
 DEEP = [
-    # config 1 scale-5 checkerboard (4x4, 48 channels, mid 512) and scale-4
-    # channelwise (4x4, 96 channels, mid 512): M = 1024, where the single
-    # launches run the same deep tiles (tolerance: fp64-sum order only);
-    # scale-4 checkerboard (8x8, 24 channels, mid 256): M = 4096, where the
-    # single 1x1 launches use the generic family (another fp32 summation
-    # order, so the ReLU-kink floor of the data gradient, ~1e-3, applies)
-    ("s5_ckbd", "ckbd", 48, 512, 4, 1e-5),
-    ("s4_chan", "chan", 96, 512, 4, 1e-5),
+    # config 1 scale-5 checkerboard (4x4, 48 channels, mid 512), scale-4
+    # channelwise (4x4, 96 channels, mid 512): M = 1024; scale-4 checkerboard
+    # (8x8, 24 channels, mid 256): M = 4096.  The single launches use other
+    # tile configurations than the chain (8-wave tiles, grouped skip convs:
+    # another fp32 summation order), so the ReLU-kink floor of the data
+    # gradient, ~1e-3, applies
+    ("s5_ckbd", "ckbd", 48, 512, 4, 3e-3),
+    ("s4_chan", "chan", 96, 512, 4, 3e-3),
     ("s4_ckbd", "ckbd", 24, 256, 8, 3e-3),
 ]
 
@@ -103,12 +103,14 @@ def test_chain_is_used_at_the_deep_scales():
     _, _, _, _, eng = _run_coupling("ckbd", 48, 512, 4, 64, "fp32", chain=True)
     svs = [sv for pool in eng._saved_pool.values() for sv in pool]
     assert svs, "no saved arena"
+    # (grouped launches of independent 1x1 convs are planned first; the chain
+    # takes the rest)
     fwd = svs[0]["fwd_plan"][2]
-    chains = [gr for gr in fwd if gr[0] == "chain"]
-    assert len(chains) == 1 and chains[0][2] - chains[0][1] == 18, [g[:3] for g in fwd]
+    covered = sum(gr[2] - gr[1] for gr in fwd if gr[0] in ("chain", "group"))
+    assert covered == 18 and any(gr[0] == "chain" for gr in fwd), [g[:3] for g in fwd]
     bwd = svs[0]["bwd_plan"][2]
-    nb = sum(gr[2] - gr[1] for gr in bwd if gr[0] == "chain")
-    assert nb >= 28, [g[:3] for g in bwd]
+    nb = sum(gr[2] - gr[1] for gr in bwd if gr[0] in ("chain", "group"))
+    assert nb >= 28 and any(gr[0] == "chain" for gr in bwd), [g[:3] for g in bwd]
 
 
 def test_chain_trainer_step_config1():
@@ -206,8 +208,10 @@ def test_chain_c_abi_two_convs():
 
     t0, y0, s0 = run(False)
     t1, y1, s1 = run(True)
-    assert rel(t1, t0) == 0.0
-    assert rel(s1, s0) < 1e-12
+    # the single 1x1 launch runs the 8-wave tile configuration (K split 8
+    # ways), the chain's class the 4-wave one: fp32 summation order only
+    assert rel(t1, t0) < 1e-6
+    assert rel(s1, s0) < 1e-6
     assert rel(y1, y0) < 1e-6, rel(y1, y0)
     # and against torch: relu(bn(t1)) conv 3x3
     mean = s0[0] / M
