@@ -934,45 +934,41 @@ __global__ __launch_bounds__(256) void k_conv_band(rnvp_conv_args a, int shards)
 
     // ---- band + halo loads first: in flight under the table / weight prologue
     const T* __restrict__ X = (const T*)a.x;
+    // cs <= 64 channels: a row is cpr <= 16 chunks (bf16: <= 8) and 256 % cpr
+    // == 0 (launcher), so a thread's chunk column is the same in every staged
+    // row: its BN coefficients go to registers once (no per-chunk LDS table
+    // reads or divisions), its rows advance by 256 / cpr per slot, and no
+    // load is issued past the band
     const int cpr = cs / CH;
-    const int total = R * cpr;
-    const float rcpr = 1.0f / (float)cpr;
+    const int cfix = tid % cpr, rbase = tid / cpr, rstep = 256 / cpr;
     u32x4 sv[SB];
-    auto stage_load = [&](int q0) {
+    auto stage_load = [&](int r0) {
 #pragma unroll
         for (int u = 0; u < SB; ++u) {
-            const int q = q0 + u * 256 + tid;
-            const int r = fdiv_small(q, rcpr), c = q - r * cpr;
+            if (r0 + u * rstep >= R) break;
+            const int r = r0 + rbase + u * rstep;
             const int p = m0 - hal + r;
-            const bool ok = (q < total) & (p >= 0) & (p < M);
-            sv[u] = *(const u32x4*)(X + (ok ? (long long)p * cs + c * CH : 0));
+            const bool ok = (r < R) & (p >= 0) & (p < M);
+            sv[u] = *(const u32x4*)(X + (ok ? (long long)p * cs + cfix * CH : 0));
         }
     };
-    auto stage_store = [&](int q0) {
+    float scv[CH], shv[CH];
+    auto stage_store = [&](int r0) {
 #pragma unroll
         for (int u = 0; u < SB; ++u) {
-            const int q = q0 + u * 256 + tid;
-            if (q >= total) continue;
-            const int r = fdiv_small(q, rcpr), c = q - r * cpr;
+            const int r = r0 + rbase + u * rstep;
+            if (r >= R) continue;
             const int p = m0 - hal + r;
             u32x4 w = sv[u];
             if (PRO) {
                 float f[CH];
                 unpack(w, f, T());
-                const int c0 = c * CH;
 #pragma unroll
-                for (int e = 0; e < CH; e += 4) {
-                    const floatx4 sc = *(const floatx4*)&bnp[c0 + e];
-                    const floatx4 sh = *(const floatx4*)&bnp[cs + c0 + e];
-                    f[e] = fmaxf(f[e] * sc.x + sh.x, 0.f);
-                    f[e + 1] = fmaxf(f[e + 1] * sc.y + sh.y, 0.f);
-                    f[e + 2] = fmaxf(f[e + 2] * sc.z + sh.z, 0.f);
-                    f[e + 3] = fmaxf(f[e + 3] * sc.w + sh.w, 0.f);
-                }
+                for (int e = 0; e < CH; ++e) f[e] = fmaxf(f[e] * scv[e] + shv[e], 0.f);
                 w = pack(f, T());
             }
             const uint32_t keep = (p >= 0 && p < M) ? ~0u : 0u;
-            *(u32x4*)(act + r * pitch + c * CH) = w & u32x4{keep, keep, keep, keep};
+            *(u32x4*)(act + r * pitch + cfix * CH) = w & u32x4{keep, keep, keep, keep};
         }
     };
     stage_load(0);
@@ -1009,12 +1005,19 @@ __global__ __launch_bounds__(256) void k_conv_band(rnvp_conv_args a, int shards)
         for (int c = tid * CH; c < pitch; c += 256 * CH) *(u32x4*)(zrow + c) = u32x4{0u, 0u, 0u, 0u};
     }
     __syncthreads();
+    if (PRO) {
+#pragma unroll
+        for (int e = 0; e < CH; ++e) {
+            scv[e] = bnp[cfix * CH + e];
+            shv[e] = bnp[cs + cfix * CH + e];
+        }
+    }
 
     // ---- act(x) band -> LDS (transformed once) ----
     stage_store(0);
-    for (int q0 = 256 * SB; q0 < total; q0 += 256 * SB) {
-        stage_load(q0);
-        stage_store(q0);
+    for (int r0 = rstep * SB; r0 < R; r0 += rstep * SB) {
+        stage_load(r0);
+        stage_store(r0);
     }
     __syncthreads();
 
@@ -1136,6 +1139,7 @@ bool band_ok(const rnvp_conv_args* a) {
     const long long M = (long long)a->B * a->H * a->W;
     // 3x3 only: for 1x1 the streaming kernel (no halo to share) is faster
     if (a->n > 64 || a->cs_in > 64 || a->ks != 3) return false;
+    if (256 % (a->cs_in / Mf<T>::CH) != 0) return false;   // fixed chunk column per thread
     if (M < 32768 || M >= (1ll << 21)) return false;
     return band_lds_bytes<T>(a->cs_in, a->n, a->W, a->ks) <= 150 * 1024;
 }

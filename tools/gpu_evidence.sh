@@ -15,6 +15,9 @@ export TMPDIR=/tmp
 T=${TAG:-ev}
 O=gpurun_out/$T
 mkdir -p $O
+# on exit keep the summaries and the step's kernel trace, drop the raw PMC /
+# marker traces (gpurun copies back <= 64 MiB)
+trap 'rm -rf $O/pmc_fetch $O/pmc_write $O/pmc_mfma $O/trace_fam; for f in kernel_stats kernel_trace; do [ -f $O/prof/run_$f.csv ] && cp $O/prof/run_$f.csv $O/$f.csv; done; rm -rf $O/prof' EXIT
 step() { local log=$1; shift; "$@" > $O/$log 2>&1; local rc=$?; echo "$log rc=$rc"; tail -${TAILN:-3} $O/$log; if [ $rc -ne 0 ]; then exit $rc; fi; }
 R=$GRAFT_REPO_ROOT
 if [ -z "$NOTEST" ]; then

@@ -26,10 +26,18 @@ def main():
     adam = [i for i, r in enumerate(rows) if "k_adam" in r["Kernel_Name"]]
     if len(adam) < 2:
         raise SystemExit("need two complete steps in the trace")
-    seg = rows[adam[-2] + 1: adam[-1] + 1]
-    mk = [i for i, r in enumerate(seg) if "k_marker" in r["Kernel_Name"]]
-    if len(mk) != 2 * len(fams):
-        raise SystemExit("found %d markers in the step, expected %d" % (len(mk), 2 * len(fams)))
+    # the last complete step that carries the captured markers (bench.py's
+    # instrumented eager step for the HIP-event roofline runs after the
+    # replays, without them)
+    seg, mk = None, []
+    for j in range(len(adam) - 1, 0, -1):
+        cand = rows[adam[j - 1] + 1: adam[j] + 1]
+        mk = [i for i, r in enumerate(cand) if "k_marker" in r["Kernel_Name"]]
+        if len(mk) == 2 * len(fams):
+            seg = cand
+            break
+    if seg is None:
+        raise SystemExit("no step with the %d captured markers in the trace" % (2 * len(fams)))
     agg = defaultdict(lambda: dict(launches=0, kernels=0, us=0.0))
     for f, i0, i1 in zip(fams, mk[0::2], mk[1::2]):
         a = agg[f]
