@@ -30,16 +30,22 @@
 namespace {
 
 constexpr int WT_NT = 512;     // 8 waves
+#ifndef WT_C0_DEPTH
+#define WT_C0_DEPTH 1   // 2 (per-tap B fragments, a second stage in flight) measured slower: profiles/r3_experiments.txt
+#endif
 constexpr int WT_SP = 128;     // output pixels per stage: 4 MFMA k-steps of 32
 constexpr int WT_KST = WT_SP / 32;
 
 // tile classes: (co tile, ci tile, kernel size, waves over co, waves over ci,
 template <int C> struct WtCfg;
 // tap groups, x chunks per thread per stage, stages of global loads in flight)
-template <> struct WtCfg<0> { static constexpr int TCO = 64, TCI = 64, KS = 3, WCO = 2, WCI = 4, WTG = 1, NX = 5, DEPTH = 1; };
-template <> struct WtCfg<1> { static constexpr int TCO = 128, TCI = 128, KS = 1, WCO = 2, WCI = 4, WTG = 1, NX = 4, DEPTH = 1; };
-template <> struct WtCfg<2> { static constexpr int TCO = 32, TCI = 32, KS = 3, WCO = 2, WCI = 2, WTG = 2, NX = 4, DEPTH = 2; };
-template <> struct WtCfg<3> { static constexpr int TCO = 64, TCI = 64, KS = 1, WCO = 2, WCI = 4, WTG = 1, NX = 2, DEPTH = 2; };
+// BALL: every B fragment of a k-step read before its MFMAs (one LDS wait) or
+// each tap's fragment right before that tap's MFMAs (32 fewer VGPRs for the
+// 3x3 class, spent on a second stage of global loads in flight)
+template <> struct WtCfg<0> { static constexpr int TCO = 64, TCI = 64, KS = 3, WCO = 2, WCI = 4, WTG = 1, NX = 5, DEPTH = WT_C0_DEPTH, BALL = WT_C0_DEPTH == 1; };
+template <> struct WtCfg<1> { static constexpr int TCO = 128, TCI = 128, KS = 1, WCO = 2, WCI = 4, WTG = 1, NX = 4, DEPTH = 1, BALL = 1; };
+template <> struct WtCfg<2> { static constexpr int TCO = 32, TCI = 32, KS = 3, WCO = 2, WCI = 2, WTG = 2, NX = 4, DEPTH = 2, BALL = 1; };
+template <> struct WtCfg<3> { static constexpr int TCO = 64, TCI = 64, KS = 1, WCO = 2, WCI = 4, WTG = 1, NX = 2, DEPTH = 2, BALL = 1; };
 
 __host__ __device__ inline int wt_class(int ks, int cs_in, int cs_dy) {
     if (ks == 3) return (cs_in <= 32 && cs_dy <= 32) ? 2 : 0;
@@ -272,34 +278,46 @@ __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int 
 #pragma unroll
             for (int a = 0; a < FCO; ++a)
                 af[a] = tr_pair(dyL + jl * DP + (wco * FCO * 16 + a * 16 + 4 * pp) * 2, DP);
-            // every B fragment of the k-step is read before the MFMAs (one LDS wait)
-            u32x4 bfr[FCI][TPW];
-#pragma unroll
-            for (int b = 0; b < FCI; ++b) {
+            auto bfrag = [&](int b, int t) {
                 const int col = (wci * FCI * 16 + b * 16 + 4 * pp) * 2;
-#pragma unroll
-                for (int t = 0; t < TPW; ++t) {
-                    if (wg * TPW + t >= T) continue;
-                    const i16x4 lo =
-                        __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)(xL + (plo[kk] + toff[t]) * XP + col));
-                    const i16x4 hi =
-                        __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)(xL + (phi[kk] + toff[t]) * XP + col));
-                    const uint2 l = __builtin_bit_cast(uint2, lo), h = __builtin_bit_cast(uint2, hi);
-                    bfr[b][t] = u32x4{l.x, l.y, h.x, h.y};
-                }
-            }
+                const i16x4 lo =
+                    __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)(xL + (plo[kk] + toff[t]) * XP + col));
+                const i16x4 hi =
+                    __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)(xL + (phi[kk] + toff[t]) * XP + col));
+                const uint2 l = __builtin_bit_cast(uint2, lo), h = __builtin_bit_cast(uint2, hi);
+                return u32x4{l.x, l.y, h.x, h.y};
+            };
             if (do_bias) {
 #pragma unroll
                 for (int a = 0; a < FCO; ++a) Mf<bf16_t>::step(af[a], ones, bacc[a]);
             }
+            if constexpr (Cfg::BALL) {
+                // every B fragment of the k-step is read before the MFMAs (one LDS wait)
+                u32x4 bfr[FCI][TPW];
 #pragma unroll
-            for (int b = 0; b < FCI; ++b)
+                for (int b = 0; b < FCI; ++b)
 #pragma unroll
-                for (int t = 0; t < TPW; ++t) {
-                    if (wg * TPW + t >= T) continue;
+                    for (int t = 0; t < TPW; ++t)
+                        if (wg * TPW + t < T) bfr[b][t] = bfrag(b, t);
 #pragma unroll
-                    for (int a = 0; a < FCO; ++a) Mf<bf16_t>::step(af[a], bfr[b][t], acc[a][b][t]);
-                }
+                for (int b = 0; b < FCI; ++b)
+#pragma unroll
+                    for (int t = 0; t < TPW; ++t) {
+                        if (wg * TPW + t >= T) continue;
+#pragma unroll
+                        for (int a = 0; a < FCO; ++a) Mf<bf16_t>::step(af[a], bfr[b][t], acc[a][b][t]);
+                    }
+            } else {
+#pragma unroll
+                for (int b = 0; b < FCI; ++b)
+#pragma unroll
+                    for (int t = 0; t < TPW; ++t) {
+                        if (wg * TPW + t >= T) continue;
+                        const u32x4 bf = bfrag(b, t);
+#pragma unroll
+                        for (int a = 0; a < FCO; ++a) Mf<bf16_t>::step(af[a], bf, acc[a][b][t]);
+                    }
+            }
         }
     };
 
