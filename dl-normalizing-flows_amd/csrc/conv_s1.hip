@@ -22,24 +22,23 @@ namespace {
 
 // NOPS epilogue operand streams per element (residual, previous y, the dgrad
 // epilogue's pre-BN x -- in that order, those present)
+// two waves per SIMD (<= 256 registers) unless that would spill
+template <int NT, int NKS, int NOPS>
+constexpr int s1_min_blocks() { return (NKS == 2 && (NOPS == 3 || (NT == 4 && NOPS == 2))) ? 1 : 2; }
+
 template <int NT, int NKS, int TW, int NOPS>
-__global__ __launch_bounds__(256) void k_conv_s1(rnvp_conv_args a, int shards) {
+__global__ __launch_bounds__(256, (s1_min_blocks<NT, NKS, NOPS>())) void k_conv_s1(rnvp_conv_args a, int shards) {
     constexpr int CH = 8, KS = 32;            // bf16: 8 channels per 16-B chunk, 32 per k-step
     constexpr int NC = 16 * NT;
     __shared__ double red[4][NC][2];
     __shared__ double tmp[2 * 64];
-    __shared__ float bnp[2 * 64];
+    __shared__ __attribute__((aligned(16))) float bnp[2 * 64];
     __shared__ float etab[4 * NC];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, li = lane & 15;
     const int M = a.B * a.H * a.W;             // < 2^31 (host)
     const int N = a.n, cs = a.cs_in, cso = a.cs_out;
     const bool pro = a.pro_bn_relu != 0, epi_bn = a.epi_relu_bn_bwd != 0;
     const bool has_acc = a.accumulate != 0;
-
-    // ---- tables (every thread: block-wide reductions) ----
-    if (pro) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + cs, nullptr, nullptr, tmp);
-    if (epi_bn) block_bn_table(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp);
-    __syncthreads();
 
     // ---- per-lane constants: weights, prologue coefficients, bias ----
     const bf16_t* __restrict__ Wg = (const bf16_t*)a.w;
@@ -50,15 +49,6 @@ __global__ __launch_bounds__(256) void k_conv_s1(rnvp_conv_args a, int shards) {
         for (int j = 0; j < NT; ++j) {
             const int n = j * 16 + li, k = s * KS + g * CH;
             wv[s][j] = (n < N && k < cs) ? *(const u32x4*)(Wg + (long long)n * a.kp + k) : u32x4{0u, 0u, 0u, 0u};
-        }
-    float psc[NKS][CH], psh[NKS][CH];
-#pragma unroll
-    for (int s = 0; s < NKS; ++s)
-#pragma unroll
-        for (int e = 0; e < CH; ++e) {
-            const int c = s * KS + g * CH + e;
-            psc[s][e] = (pro && c < cs) ? bnp[c] : 1.f;
-            psh[s][e] = (pro && c < cs) ? bnp[cs + c] : 0.f;
         }
     float bias[NT][4];
 #pragma unroll
@@ -120,11 +110,13 @@ __global__ __launch_bounds__(256) void k_conv_s1(rnvp_conv_args a, int shards) {
         }
     };
 
-    double s1[NT][4], s2[NT][4];
+    // per-lane partial statistics in fp32 (a lane adds TW values per tile over a
+    // few tiles); the cross-lane and cross-block sums are fp64
+    float s1[NT][4], s2[NT][4];
 #pragma unroll
     for (int j = 0; j < NT; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.0;
+        for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.f;
     bf16_t* __restrict__ Y = (bf16_t*)a.y;
 
     auto run = [&](int t, auto SLC) __attribute__((always_inline)) {
@@ -143,8 +135,14 @@ __global__ __launch_bounds__(256) void k_conv_s1(rnvp_conv_args a, int shards) {
                 if (pro) {
                     float f[CH];
                     unpack(v, f, bf16_t());
+                    // prologue coefficients from LDS (registers go to the tile ring)
+                    const int c0 = s * KS + g * CH;
+                    const float4 sa = *(const float4*)&bnp[c0], sb = *(const float4*)&bnp[c0 + 4];
+                    const float4 ha = *(const float4*)&bnp[64 + c0], hb = *(const float4*)&bnp[64 + c0 + 4];
+                    const float sc[CH] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
+                    const float sh[CH] = {ha.x, ha.y, ha.z, ha.w, hb.x, hb.y, hb.z, hb.w};
 #pragma unroll
-                    for (int e = 0; e < CH; ++e) f[e] = fmaxf(f[e] * psc[s][e] + psh[s][e], 0.f);
+                    for (int e = 0; e < CH; ++e) f[e] = fmaxf(f[e] * sc[e] + sh[e], 0.f);
                     v = pack(f, bf16_t());
                     // a pixel outside the image / a channel chunk beyond cs stays zero
                     const int m = t * (16 * TW) + i * 16 + li, k = s * KS + g * CH;
@@ -191,7 +189,7 @@ __global__ __launch_bounds__(256) void k_conv_s1(rnvp_conv_args a, int shards) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         s1[j][r] += v[r];
-                        s2[j][r] += (double)v[r] * v[r];
+                        s2[j][r] += v[r] * v[r];
                     }
                 }
 #pragma unroll
@@ -207,6 +205,13 @@ __global__ __launch_bounds__(256) void k_conv_s1(rnvp_conv_args a, int shards) {
     using I1 = std::integral_constant<int, 1>;
     int t = w0;
     if (t < ntiles) load(t, I0{});
+
+    // ---- tables (every thread: block-wide reductions), their loads in flight
+    // behind the weights and the first tile's ----
+    if (pro) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + 64, nullptr, nullptr, tmp);
+    if (epi_bn) block_bn_table(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp);
+    __syncthreads();
+
     while (t < ntiles) {
         if (t + nwaves < ntiles) load(t + nwaves, I1{});
         run(t, I0{});
@@ -224,7 +229,7 @@ __global__ __launch_bounds__(256) void k_conv_s1(rnvp_conv_args a, int shards) {
         for (int j = 0; j < NT; ++j)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const double u1 = row_sum16(s1[j][r]), u2 = row_sum16(s2[j][r]);
+                const double u1 = row_sum16((double)s1[j][r]), u2 = row_sum16((double)s2[j][r]);
                 if (li == 0) {
                     red[wid][j * 16 + 4 * g + r][0] = u1;
                     red[wid][j * 16 + 4 * g + r][1] = u2;
