@@ -899,15 +899,21 @@ size_t band_lds_bytes(int cs, int n, int W, int ks) {
            ((size_t)nc * kpl + (size_t)(R + 1) * (cs + CH)) * sizeof(T);
 }
 
-template <typename T, int NT, int KSZ, bool PRO>
-__global__ __launch_bounds__(256) void k_conv_band(rnvp_conv_args a, int shards) {
+// NH = 2: eight waves, wave pairs split the output channels (each wave 64
+// pixels x NT/2 channel tiles): two waves per SIMD when the band and the
+// weights hold the CU to one workgroup (64-channel 3x3 at 32x32)
+template <typename T, int NT, int KSZ, bool PRO, int NH>
+__global__ __launch_bounds__(256 * NH) void k_conv_band(rnvp_conv_args a, int shards) {
     constexpr int CH = Mf<T>::CH, KS = 4 * CH;
     constexpr int NC = 16 * NT;
     constexpr int TM = 4, BM = 64 * TM;        // 4 waves x 64 pixels
     constexpr int PAD = KSZ / 2;
-    constexpr int SB = 12;                     // staged 16-B chunks per thread per batch
+    constexpr int SB = 12 / NH;                // staged 16-B chunks per thread per batch
+    constexpr int NTH = 256 * NH, NTW = NT / NH;
+    static_assert(NT % NH == 0, "channel tiles split evenly");
     extern __shared__ double dsm[];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, li = lane & 15;
+    const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
+    const int wid = (tid >> 6) & 3, hf = tid >> 8;   // pixel group, channel half
     const int M = a.B * a.H * a.W, W = a.W, H = a.H;
     const int N = a.n, cs = a.cs_in;
     const int K = KSZ * KSZ * cs;
@@ -940,7 +946,7 @@ __global__ __launch_bounds__(256) void k_conv_band(rnvp_conv_args a, int shards)
     // reads or divisions), its rows advance by 256 / cpr per slot, and no
     // load is issued past the band
     const int cpr = cs / CH;
-    const int cfix = tid % cpr, rbase = tid / cpr, rstep = 256 / cpr;
+    const int cfix = tid % cpr, rbase = tid / cpr, rstep = NTH / cpr;
     u32x4 sv[SB];
     auto stage_load = [&](int r0) {
 #pragma unroll
@@ -980,12 +986,12 @@ __global__ __launch_bounds__(256) void k_conv_band(rnvp_conv_args a, int shards)
         const T* Wg = (const T*)a.w;
         const int wcpr = kpl / CH, wtot = NC * wcpr, kv = nsteps * KS;
         const float rw = 1.0f / (float)wcpr;
-        for (int q0 = 0; q0 < wtot; q0 += 4 * 256) {
+        for (int q0 = 0; q0 < wtot; q0 += 4 * NTH) {
             u32x4 v[4];
             unsigned okm = 0;
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const int q = q0 + u * 256 + tid;
+                const int q = q0 + u * NTH + tid;
                 const int r = fdiv_small(q, rw), c = q - r * wcpr;
                 const bool ok = (q < wtot) & (r < N) & (c * CH < kv);
                 v[u] = *(const u32x4*)(Wg + (ok ? (long long)r * a.kp + c * CH : 0));
@@ -993,7 +999,7 @@ __global__ __launch_bounds__(256) void k_conv_band(rnvp_conv_args a, int shards)
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const int q = q0 + u * 256 + tid;
+                const int q = q0 + u * NTH + tid;
                 if (q < wtot) {
                     const int r = fdiv_small(q, rw), c = q - r * wcpr;
                     const uint32_t keep = ((okm >> u) & 1u) ? ~0u : 0u;
@@ -1001,8 +1007,8 @@ __global__ __launch_bounds__(256) void k_conv_band(rnvp_conv_args a, int shards)
                 }
             }
         }
-        for (int n = tid; n < NC; n += 256) btab[n] = (a.bias && n < N) ? a.bias[n] : 0.f;
-        for (int c = tid * CH; c < pitch; c += 256 * CH) *(u32x4*)(zrow + c) = u32x4{0u, 0u, 0u, 0u};
+        for (int n = tid; n < NC; n += NTH) btab[n] = (a.bias && n < N) ? a.bias[n] : 0.f;
+        for (int c = tid * CH; c < pitch; c += NTH * CH) *(u32x4*)(zrow + c) = u32x4{0u, 0u, 0u, 0u};
     }
     __syncthreads();
     if (PRO) {
@@ -1041,11 +1047,11 @@ __global__ __launch_bounds__(256) void k_conv_band(rnvp_conv_args a, int shards)
         tvm[i] = bits;
     }
 
-    floatx4 acc[TM][NT];
+    floatx4 acc[TM][NTW];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < NT; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < NTW; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
     // lane's K position k = s*KS + g*CH -> (tap, ci); a 16-B chunk never
     // straddles a tap (cs % CH == 0); KS / cs <= 4 wraps per step
@@ -1053,14 +1059,14 @@ __global__ __launch_bounds__(256) void k_conv_band(rnvp_conv_args a, int shards)
 #pragma unroll
     for (int w = 0; w < 4; ++w)
         if (ci >= cs) { ci -= cs; ++tap; }
-    const T* wl = Wl + li * kpl + g * CH;
+    const T* wl = Wl + (hf * NTW * 16 + li) * kpl + g * CH;
     for (int st = 0; st < nsteps; ++st) {
         const int ty = tap / KSZ;
         const int toff = ((ty - PAD) * W + (tap - ty * KSZ - PAD)) * pitch + ci;
         const int tsh = tap < KSZ * KSZ ? tap : 31;   // bit 31 of tvm is never set
-        u32x4 wv[NT], av[TM];
+        u32x4 wv[NTW], av[TM];
 #pragma unroll
-        for (int j = 0; j < NT; ++j) wv[j] = *(const u32x4*)(wl + j * 16 * kpl + st * KS);
+        for (int j = 0; j < NTW; ++j) wv[j] = *(const u32x4*)(wl + j * 16 * kpl + st * KS);
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
             const bool ok = (tvm[i] >> tsh) & 1u;
@@ -1069,7 +1075,7 @@ __global__ __launch_bounds__(256) void k_conv_band(rnvp_conv_args a, int shards)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int j = 0; j < NT; ++j) Mf<T>::step(wv[j], av[i], acc[i][j]);
+            for (int j = 0; j < NTW; ++j) Mf<T>::step(wv[j], av[i], acc[i][j]);
         ci += KS;
 #pragma unroll
         for (int w = 0; w < 4; ++w)
@@ -1078,9 +1084,9 @@ __global__ __launch_bounds__(256) void k_conv_band(rnvp_conv_args a, int shards)
 
     // ---- epilogue: lane owns channels j*16 + 4g .. +3 of its pixels ----
     const int cso = a.cs_out;
-    double s1[NT][4], s2[NT][4];
+    double s1[NTW][4], s2[NTW][4];
 #pragma unroll
-    for (int j = 0; j < NT; ++j)
+    for (int j = 0; j < NTW; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.0;
 #pragma unroll
@@ -1088,8 +1094,8 @@ __global__ __launch_bounds__(256) void k_conv_band(rnvp_conv_args a, int shards)
         const int m = m0 + wid * 64 + i * 16 + li;
         if (m >= M) continue;
 #pragma unroll
-        for (int j = 0; j < NT; ++j) {
-            const int n0 = j * 16 + 4 * g;
+        for (int j = 0; j < NTW; ++j) {
+            const int n0 = (hf * NTW + j) * 16 + 4 * g;
             if (n0 >= cso) continue;
             epi4<T>(a, (long long)m * cso + n0, acc[i][j], btab + n0, epi_bn, etab + n0, NC, s1[j], s2[j], N - n0);
         }
@@ -1097,18 +1103,19 @@ __global__ __launch_bounds__(256) void k_conv_band(rnvp_conv_args a, int shards)
     const bool want_sums = a.out_sums || (epi_bn && a.epi_sums);
     if (want_sums) {
 #pragma unroll
-        for (int j = 0; j < NT; ++j)
+        for (int j = 0; j < NTW; ++j)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const double u1 = row_sum16(s1[j][r]), u2 = row_sum16(s2[j][r]);
+                const int col = (hf * NTW + j) * 16 + 4 * g + r;
                 if (li == 0) {
-                    red[(wid * NC + j * 16 + 4 * g + r) * 2] = u1;
-                    red[(wid * NC + j * 16 + 4 * g + r) * 2 + 1] = u2;
+                    red[(wid * NC + col) * 2] = u1;
+                    red[(wid * NC + col) * 2 + 1] = u2;
                 }
             }
         __syncthreads();
         double* sums = shard_ptr(epi_bn ? a.epi_sums : a.out_sums, shards, N);
-        for (int n = tid; n < N; n += 256) {
+        for (int n = tid; n < N; n += NTH) {
             double t1 = 0.0, t2 = 0.0;
 #pragma unroll
             for (int w = 0; w < 4; ++w) {
@@ -1127,8 +1134,19 @@ int launch_band(const rnvp_conv_args* a, hipStream_t s) {
     const unsigned grid = (unsigned)((M + 255) / 256);
     const size_t shm = band_lds_bytes<T>(a->cs_in, a->n, a->W, KSZ);
     const int sh = rnvp_stat_shards(M);
-    if (a->pro_bn_relu) k_conv_band<T, NT, KSZ, true><<<grid, 256, shm, s>>>(*a, sh);
-    else k_conv_band<T, NT, KSZ, false><<<grid, 256, shm, s>>>(*a, sh);
+    // eight waves for the 64-channel 3x3 (one workgroup per CU by LDS);
+    // RNVP_BAND_NH=1 keeps four
+    static const int nh_env = [] { const char* e = getenv("RNVP_BAND_NH"); return e ? atoi(e) : 2; }();
+    if constexpr (NT == 4 && KSZ == 3) {
+        if (nh_env == 2) {
+            if (a->pro_bn_relu) k_conv_band<T, NT, KSZ, true, 2><<<grid, 512, shm, s>>>(*a, sh);
+            else k_conv_band<T, NT, KSZ, false, 2><<<grid, 512, shm, s>>>(*a, sh);
+            RNVP_LAUNCH_CHECK();
+            return RNVP_OK;
+        }
+    }
+    if (a->pro_bn_relu) k_conv_band<T, NT, KSZ, true, 1><<<grid, 256, shm, s>>>(*a, sh);
+    else k_conv_band<T, NT, KSZ, false, 1><<<grid, 256, shm, s>>>(*a, sh);
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
 }
