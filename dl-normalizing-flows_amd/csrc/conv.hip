@@ -1134,11 +1134,12 @@ int launch_band(const rnvp_conv_args* a, hipStream_t s) {
     const unsigned grid = (unsigned)((M + 255) / 256);
     const size_t shm = band_lds_bytes<T>(a->cs_in, a->n, a->W, KSZ);
     const int sh = rnvp_stat_shards(M);
-    // eight waves for the 64-channel 3x3 (one workgroup per CU by LDS);
-    // RNVP_BAND_NH=1 keeps four
+    // eight waves for the 3x3 (64 channels: 23.76 vs 24.03 ms per step; 32
+    // channels: 23.71 vs 23.79); RNVP_BAND_NH / RNVP_BAND_NH2 = 1 keep four
     static const int nh_env = [] { const char* e = getenv("RNVP_BAND_NH"); return e ? atoi(e) : 2; }();
-    if constexpr (NT == 4 && KSZ == 3) {
-        if (nh_env == 2) {
+    static const int nh2_env = [] { const char* e = getenv("RNVP_BAND_NH2"); return e ? atoi(e) : 2; }();
+    if constexpr ((NT == 4 || NT == 2) && KSZ == 3) {
+        if ((NT == 4 ? nh_env : nh2_env) == 2) {
             if (a->pro_bn_relu) k_conv_band<T, NT, KSZ, true, 2><<<grid, 512, shm, s>>>(*a, sh);
             else k_conv_band<T, NT, KSZ, false, 2><<<grid, 512, shm, s>>>(*a, sh);
             RNVP_LAUNCH_CHECK();
