@@ -243,11 +243,12 @@ extern "C" int rnvp_net_group(const rnvp_net_step* steps, int n, int dtype, int 
 // whole-tile-per-wave, K / 4) and for the 3x3 at M <= 4096 (64-channel
 // tiles); elsewhere -1 (the caller's other families).
 // Round 3 (prologue loads trimmed): 1x1 up to M = 4096 and 3x3 up to
-// M = 16384 as well -- step 26.47 -> 26.03 ms (profiles/r3_dispatch_ab.txt).
+// M = 16384 as well -- step 26.47 -> 26.03 ms (profiles/r3_dispatch_ab.txt);
+// 1x1 up to 16384 later (23.70 -> 23.64 ms, three alternating pairs).
 // RNVP_DEEP_MAXM1 / RNVP_DEEP_MAXM3: the largest M the family takes for 1x1
 // (cfg 0 up to 1024, cfg 1 above) / 3x3 convs (A/B of the dispatch limits)
 int rnvp_deep_auto_cfg(const rnvp_conv_args* a) {
-    static const long long max1 = [] { const char* e = getenv("RNVP_DEEP_MAXM1"); return e ? atoll(e) : 4096ll; }();
+    static const long long max1 = [] { const char* e = getenv("RNVP_DEEP_MAXM1"); return e ? atoll(e) : 16384ll; }();
     static const long long max3 = [] { const char* e = getenv("RNVP_DEEP_MAXM3"); return e ? atoll(e) : 16384ll; }();
     const long long M = (long long)a->B * a->H * a->W;
     if (M > (a->ks == 3 ? max3 : max1)) return -1;
