@@ -64,6 +64,8 @@ def parse():
     p.add_argument("--cpu-batch", type=int, default=64)
     p.add_argument("--cpu-steps", type=int, default=3)
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--launch-check", action="store_true",
+                   help="each rank prints its rank / world size and exits before any GPU call (tests the launcher)")
     p.add_argument("--pmc-markers", default=None,
                    help="write the instrumented step's launch families here and dispatch a marker before each "
                         "launch (for rocprofv3 --pmc passes, tools/pmc_traffic.py)")
@@ -93,11 +95,39 @@ def synthetic_pixels(B, C, S, seed):
     return torch.from_numpy((k / 255.0).astype(np.float32))
 
 
+@__import__("functools").lru_cache(maxsize=1)
+def binary_stamp():
+    """Identity of the benchmarked binary: sha256 of the loaded HIP library and
+    the git commit (RNVP_COMMIT on the GPU box, which has no .git)."""
+    import hashlib
+    from realnvp_hip import _lib
+    h = hashlib.sha256(open(_lib.LIB_PATH, "rb").read()).hexdigest()[:16]
+    commit = os.environ.get("RNVP_COMMIT")
+    if not commit and os.path.isdir(os.path.join(ROOT, ".git")):
+        import subprocess
+        try:
+            commit = subprocess.run(["git", "rev-parse", "HEAD"], cwd=ROOT, capture_output=True, text=True,
+                                    timeout=30).stdout.strip() or None
+        except (OSError, subprocess.SubprocessError):
+            commit = None
+    return dict(lib_sha256=h, commit=commit)
+
+
+STALE = []
+
+
 def _load_for(path, config):
-    """a profiles/*.json family table, if it was measured on this config"""
+    """a profiles/*.json family table, if it was measured on this config AND
+    on this binary (its stamp's library hash equals the loaded one); a table
+    of another binary is not used and is listed in the line's
+    roofline.stale_tables"""
     if path and os.path.exists(path):
         t = json.load(open(path))
         if t.get("config") == config:
+            st = t.get("stamp") or {}
+            if st.get("lib_sha256") != binary_stamp()["lib_sha256"]:
+                STALE.append(dict(table=os.path.relpath(path, ROOT), stamp=st or None))
+                return {}
             return t.get("families", {})
     return {}
 
@@ -126,7 +156,8 @@ def kernel_roofline(trainer, markers=None, traffic=None, config=None, mfma=None,
         d["launches"] += 1
     E.PROFILE = None
     if markers is not None:
-        json.dump(dict(config=config, families=E.MARKER_FAMILIES, n_params=int(trainer.param.numel()),
+        json.dump(dict(config=config, stamp=binary_stamp(), families=E.MARKER_FAMILIES,
+                       n_params=int(trainer.param.numel()),
                        alg_bytes={k: v["bytes"] / v["launches"] for k, v in fam.items()}), open(markers, "w"))
     dom = max(fam, key=lambda k: fam[k]["ms"])
     d = fam[dom]
@@ -164,6 +195,8 @@ def kernel_roofline(trainer, markers=None, traffic=None, config=None, mfma=None,
         roof["rocprof_avg_launch_us"] = rp[dom]["avg_launch_us"]
         roof["rocprof_achieved"] = round(bytes_per_launch / (rp[dom]["avg_launch_us"] * 1e-6) / 1e9, 1)
         roof["rocprof_source"] = os.path.relpath(rocprof, ROOT)
+    if STALE:
+        roof["stale_tables"] = list(STALE)
     families = {k: dict(ms=round(v["ms"], 3), launches=v["launches"],
                         gbs=round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1),
                         tflops=round(v["flops"] / max(v["ms"], 1e-9) / 1e9, 2)) for k, v in fam.items()}
@@ -302,6 +335,25 @@ def secondary(args, dev):
                           steps=5, step_roofline_frac=round(v * c["alg_bytes"] / (HBM_PEAK_GBS * 1e9), 5))
     del tr, model
     torch.cuda.empty_cache()
+
+    # BASELINE config 4's per-GPU slice (128x128x3, 6 scales, D64, 1.886 B
+    # parameters, batch 256 = the HBM-sized local batch of the 8-GPU config)
+    c = CONFIGS["c4"]
+    model = build_model(c["size"], c["res_blocks"], c["base_dim"], c["n_scales"], dev, args.seed)
+    tr = FlowTrainer(model, c["batch"], dtype="bf16", seed=1000)
+    tr.set_pixels(synthetic_pixels(c["batch"], 3, c["size"], seed=0).to(dev))
+    tr.capture(warmup=1)
+    tr.step()
+    tr.reset_metrics()
+    dt = timed(tr.step, 3, 0)
+    v = 3 * c["batch"] / dt
+    out["config4"] = dict(workload=c["label"] + ", per-GPU batch %d (one rank of the 8-GPU config), train step "
+                                                "fwd+bwd+Adam" % c["batch"],
+                          value=round(v, 2), unit="images/sec", ms_per_step=round(dt / 3 * 1e3, 3), dtype="bf16",
+                          steps=3, step_roofline_frac=round(v * c["alg_bytes"] / (HBM_PEAK_GBS * 1e9), 5),
+                          bits_per_dim=round(tr.bits_per_dim(tr.mean_logll(3)), 4))
+    del tr, model
+    torch.cuda.empty_cache()
     return out
 
 
@@ -351,14 +403,45 @@ def dp_diagnostics(tr, pg, step_s, dev):
     return out
 
 
+def launcher_command(argv, gpus, env):
+    """The rank launcher `python3 bench.py --gpus N` (N > 1) starts when it was
+    not itself started by torch.distributed.run (no WORLD_SIZE): one
+    torch.distributed.run child that spawns N ranks on this node, rendezvous
+    on 127.0.0.1.  None when this process is a rank (or N == 1) and runs the
+    benchmark itself."""
+    if gpus <= 1 or "WORLD_SIZE" in env:
+        return None
+    port = env.get("RNVP_BENCH_PORT")
+    if port is None:
+        import socket
+        with socket.socket() as s:      # a free local port for the rendezvous
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(gpus),
+            "--master-addr", "127.0.0.1", "--master-port", str(port),
+            os.path.abspath(__file__)] + list(argv)
+
+
 def main():
+    # `--gpus N` without a launcher: start the N ranks as children BEFORE any
+    # GPU call in this process (this parent has only imported torch; it never
+    # initialises HIP and never execs), pass their output through and exit
+    # with their status.  Rank 0 prints the JSON line.
     args = parse()
+    cmd = launcher_command(sys.argv[1:], args.gpus, os.environ)
+    if cmd is not None:
+        import subprocess
+        sys.stdout.flush()
+        raise SystemExit(subprocess.call(cmd))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus %d needs torch.distributed.run --nproc-per-node %d" % (args.gpus, args.gpus))
+        raise SystemExit("--gpus %d but WORLD_SIZE=%d: launch %d ranks" % (args.gpus, world, args.gpus))
+    if args.launch_check:
+        print(json.dumps(dict(rank=rank, local_rank=local, world_size=world,
+                              master=os.environ.get("MASTER_ADDR"))), flush=True)
+        return
     # RNVP_BENCH_BACKEND=gloo: a rehearsal of the multi-rank path on a box with
     # fewer GPUs than ranks (ranks share devices round-robin; eager only, as
     # gloo collectives cannot be captured).  The driver's runs use RCCL.
@@ -399,7 +482,8 @@ def main():
         if args.graph_markers:
             E.MARKERS = False
             if rank == 0:
-                json.dump(dict(config=cfg_key, families=E.MARKER_FAMILIES), open(args.graph_markers, "w"))
+                json.dump(dict(config=cfg_key, stamp=binary_stamp(), families=E.MARKER_FAMILIES),
+                          open(args.graph_markers, "w"))
 
     def barrier():
         if pg is not None:
@@ -451,6 +535,7 @@ def main():
             "roofline": roof,
             "kernel_families": fams,
             "cpu_baseline": None,
+            "binary": binary_stamp(),
         }
         if dp is not None:
             out["dp"] = dp

@@ -1188,13 +1188,11 @@ int dispatch_conv(const rnvp_conv_args* a, hipStream_t s) {
         }
     }
     const bool tuned = a->variant != 1;
-    // bf16 streaming families of the wide scales: the register-pipelined 1x1
-    // (conv_s1.hip, default; RNVP_CONV_STREAM=0 restores the round-2 stream
-    // kernel) and the 3x3 row stream (conv_s3.hip, RNVP_CONV_STREAM=3: measured
-    // slower than the band kernel at scale 1, 33 vs 28 us, so off by default)
+    // bf16 1x1 convs of the wide scales: the register-pipelined stream kernel
+    // (conv_s1.hip; RNVP_CONV_STREAM=0 restores the round-2 stream kernel)
     static const int smode = [] { const char* e = getenv("RNVP_CONV_STREAM"); return e ? atoi(e) : 1; }();
-    if (tuned && smode && a->dtype == RNVP_BF16 && (a->ks == 1 || smode == 3)) {
-        const int r = a->ks == 1 ? rnvp_conv_s1_launch(a, s) : rnvp_conv_s3_launch(a, s);
+    if (tuned && smode && a->dtype == RNVP_BF16 && a->ks == 1) {
+        const int r = rnvp_conv_s1_launch(a, s);
         if (r != RNVP_E_UNSUPPORTED) return r;
     }
     if (tuned && band_ok<T>(a)) return dispatch_band<T>(a, s);

@@ -313,7 +313,3 @@ int rnvp_wgrad_tap_launch(rnvp_wgrad_group* g, hipStream_t s);
 // register-pipelined streaming 1x1 conv (conv_s1.hip): RNVP_E_UNSUPPORTED
 // outside bf16 / 1x1 / <= 64 channels / M >= 16k
 int rnvp_conv_s1_launch(const rnvp_conv_args* a, hipStream_t s);
-
-// row-streaming 3x3 conv (conv_s3.hip): RNVP_E_UNSUPPORTED outside bf16 /
-// W in {32, 64} / <= 64 channels / M >= 16k
-int rnvp_conv_s3_launch(const rnvp_conv_args* a, hipStream_t s);

@@ -90,8 +90,20 @@ class RealNVP(nn.Module):
         return torch.tensor(weights)
 
     def _check_om(self, x, order_matrix):
-        if order_matrix is not None and tuple(order_matrix.shape) != (4 * x.shape[1], x.shape[1], 2, 2):
+        """The reference convolves with whatever 0/1 kernel it is handed
+        (flow_realnvp.py:167-193); the HIP path implements the permutation of
+        the canonical order_matrix(C) -- the only one the reference itself
+        passes (order_matrix_k, flow_realnvp.py:60-93).  Any other matrix is
+        refused rather than silently giving a different result."""
+        if order_matrix is None:
+            return
+        C = x.shape[1]
+        if tuple(order_matrix.shape) != (4 * C, C, 2, 2):
             raise ValueError("order_matrix shape does not match the input channels")
+        canon = self.order_matrix(C).to(device=order_matrix.device, dtype=order_matrix.dtype)
+        if not torch.equal(order_matrix, canon):
+            raise ValueError("factor_out / restore implement the canonical order_matrix(%d) only "
+                             "(flow_realnvp.py:139-165); got another 0/1 kernel" % C)
 
     def factor_out(self, x, order_matrix=None):
         """flow_realnvp.py:167-180 -> (on, off), each [B, 2C, H/2, W/2]."""
@@ -100,6 +112,8 @@ class RealNVP(nn.Module):
 
     def restore(self, on, off, order_matrix=None):
         """flow_realnvp.py:182-193."""
+        if order_matrix is not None:
+            self._check_om(on.new_empty(on.shape[0], on.shape[1] // 2, 1, 1), order_matrix)
         return Fn.restore(on, off)
 
     # ------------------------------------------------------------------- flow

@@ -49,7 +49,6 @@ class BNBwdArgs(C.Structure):
 
 
 RNVP_STEP_CONV, RNVP_STEP_BN_BWD = 0, 1
-NET_CHAIN_BARRIER_BYTES = 64
 NET_GROUP_MAX = 8
 
 
@@ -144,8 +143,6 @@ _SIGS = {
     "rnvp_adam_update": (i32, [vp, vp, vp, vp, i64, vp, i64, f32, f32, f32, f32, f32, vp, f32, vp]),
     "rnvp_step_increment": (i32, [vp, vp]),
     "rnvp_fill_f64": (i32, [vp, i64, f64, vp]),
-    "rnvp_net_chain_prepare": (i32, [vp, i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]),
-    "rnvp_net_chain": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, vp]),
     "rnvp_net_group_prepare": (i32, [vp, i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]),
     "rnvp_net_group": (i32, [vp, i32, i32, i32, i32, i32, vp]),
 }
@@ -163,7 +160,7 @@ class _Lib:
             fn.restype = res
             fn.argtypes = args
             raw = name in ("rnvp_version", "rnvp_stat_shards", "rnvp_wgrad_slabs", "rnvp_wgrad_replicas",
-                           "rnvp_weight_norm_tiles", "rnvp_net_chain_prepare",
+                           "rnvp_weight_norm_tiles",
                            "rnvp_net_group_prepare") or res is not i32
             setattr(self, name[len("rnvp_"):], fn if raw else self._wrap(name, fn))
 

@@ -20,7 +20,7 @@ import torch
 
 from . import _lib
 from ._lib import (BNBwdArgs, BNRunning, BNSrc, ConvArgs, CouplingArgs, NetStep, WgradConv, WgradGroup, WNDesc,
-                   NET_CHAIN_BARRIER_BYTES, NET_GROUP_MAX, RNVP_BF16, RNVP_F32, RNVP_STEP_BN_BWD, RNVP_STEP_CONV, WGRAD_GROUP_MAX)
+                   NET_GROUP_MAX, RNVP_BF16, RNVP_F32, RNVP_STEP_BN_BWD, RNVP_STEP_CONV, WGRAD_GROUP_MAX)
 from .net import backward_program, build_program, chan_stride, round_up
 
 BN_EPS = 1e-5
@@ -31,9 +31,6 @@ DTYPES = {"fp32": (RNVP_F32, 4, torch.float32), "bf16": (RNVP_BF16, 2, torch.bfl
 # conv kernel family override for A/B diagnostics (rnvp_conv_args.variant):
 # 0 = per-shape tuned dispatch, 1 = generic LDS-tiled kernels only
 CONV_VARIANT = int(os.environ.get("RNVP_CONV_VARIANT", "0"))
-# persistent net chains (rnvp_net_chain) for runs of deep-scale net steps:
-# opt-in (RNVP_NET_CHAIN=1); measured slower than one launch per step
-NET_CHAIN = int(os.environ.get("RNVP_NET_CHAIN", "0"))
 # grouped launches of independent 1x1 convs (rnvp_net_group); RNVP_NET_GROUP=0
 # launches them one by one
 NET_GROUP = int(os.environ.get("RNVP_NET_GROUP", "1"))
@@ -172,23 +169,17 @@ def _independent(rw, members, j):
     return True
 
 
-def plan_chains(steps, device, rw=None):
+def plan_launches(steps, device, rw=None):
     """Plan the launches of consecutive net steps (host NetStep structs):
-      * grouped launches (rnvp_net_group): a run of mutually independent 1x1
-        convs (rw[i] = (buffers read, buffers written) of step i) that
-        rnvp_net_group_prepare accepts becomes one launch;
-      * persistent chains (rnvp_net_chain, opt-in): the longest run from a
-        position that rnvp_net_chain_prepare accepts;
-      * the rest stay single launches.
-    Returns [("group" | "chain", i0, i1, klass, grid, lds, device table) |
-    ("single", i)]."""
+    a run of mutually independent 1x1 convs (rw[i] = (buffers read, buffers
+    written) of step i) that rnvp_net_group_prepare accepts becomes one
+    grouped launch (rnvp_net_group); the rest stay single launches.
+    Returns [("group", i0, i1, klass, grid, lds, device table) | ("single", i)]."""
     L = _lib.lib()
     out = []
     n = len(steps)
     i = 0
-    cuda = CONV_VARIANT == 0 and torch.device(device).type == "cuda"
-    enabled = NET_CHAIN and cuda
-    grouping = NET_GROUP and cuda and rw is not None
+    grouping = NET_GROUP and CONV_VARIANT == 0 and torch.device(device).type == "cuda" and rw is not None
     while i < n:
         if grouping:
             members = [i]
@@ -207,36 +198,9 @@ def plan_chains(steps, device, rw=None):
                 out.append(("group", i, j, k, g, lb, upload(bytes(arr), device)))
                 i = j
                 continue
-        best = None
-        j = i + 2
-        while enabled and j <= n:
-            arr = (NetStep * (j - i))(*steps[i:j])
-            k, g, lb = C.c_int(), C.c_int(), C.c_int()
-            if L.net_chain_prepare(arr, j - i, C.byref(k), C.byref(g), C.byref(lb)) != 0:
-                break
-            best = (j, arr, k.value, g.value, lb.value)
-            j += 1
-        if best is not None:
-            j, arr, k, g, lb = best
-            out.append(("chain", i, j, k, g, lb, upload(bytes(arr), device)))
-            i = j
-        else:
-            out.append(("single", i))
-            i += 1
+        out.append(("single", i))
+        i += 1
     return out
-
-
-_BARRIERS = {}
-
-
-def chain_barrier(key, device):
-    """Grid-barrier words of one engine's chains (zeroed once; every chain
-    leaves them reusable)."""
-    t = _BARRIERS.get((key, str(device)))
-    if t is None:
-        t = torch.zeros(NET_CHAIN_BARRIER_BYTES // 4, dtype=torch.int32, device=device)
-        _BARRIERS[(key, str(device))] = t
-    return t
 
 
 class CouplingEngine:
@@ -490,7 +454,7 @@ class CouplingEngine:
                 reads = {op.x} | ({op.residual} if op.residual else set()) | ({op.y} if op.accumulate else set())
                 reads |= {"s:" + op.pro_bn} if op.pro_bn else set()
                 rw.append((reads, {op.y} | ({"s:" + op.stats_bn} if op.stats_bn else set())))
-            plan = (key, args, plan_chains(steps, sv["arena"].buf.device, rw))
+            plan = (key, args, plan_launches(steps, sv["arena"].buf.device, rw))
             sv["fwd_plan"] = plan
         args = plan[1]
         dt = DTYPES[sv["dtype"]][0]
@@ -498,18 +462,11 @@ class CouplingEngine:
             if g[0] == "single":
                 a, nb, fl = args[g[1]]
                 _launch("conv_fwd", nb, fl, L.conv2d, C.byref(a), s)
-            elif g[0] == "group":
-                _, i0, i1, klass, grid, lds, tab = g
-                nb = sum(args[i][1] for i in range(i0, i1))
-                fl = sum(args[i][2] for i in range(i0, i1))
-                _launch("conv_fwd", nb, fl, L.net_group, tab.data_ptr(), i1 - i0, dt, klass, grid, lds, s)
             else:
                 _, i0, i1, klass, grid, lds, tab = g
                 nb = sum(args[i][1] for i in range(i0, i1))
                 fl = sum(args[i][2] for i in range(i0, i1))
-                bar = chain_barrier(id(self), tab.device)
-                _launch("net_chain_fwd", nb, fl, L.net_chain, tab.data_ptr(), i1 - i0, dt, klass, grid, lds, None,
-                        bar.data_ptr(), s)
+                _launch("conv_fwd", nb, fl, L.net_group, tab.data_ptr(), i1 - i0, dt, klass, grid, lds, s)
 
     def _fwd_args(self, T, sv, ws, training):
         ar = sv["arena"]
@@ -776,7 +733,7 @@ class CouplingEngine:
                     writes = {dst}
                 steps.append(st)
                 rw.append((reads, writes))
-            plan = plan + (plan_chains(steps, x.device, rw),)
+            plan = plan + (plan_launches(steps, x.device, rw),)
             sv["bwd_plan"] = plan
         for g in plan[2]:
             if g[0] == "single":
@@ -786,18 +743,11 @@ class CouplingEngine:
                 else:
                     c.dgamma, c.dbeta = gp(bn + "weight"), gp(bn + "bias")
                     _launch("bn_bwd", nb, 0.0, L.bn_bwd_apply, C.byref(c), s)
-            elif g[0] == "group":
-                _, i0, i1, klass, grid, lds, tab = g
-                nb = sum(items[i][2] for i in range(i0, i1))
-                fl = sum(items[i][3] for i in range(i0, i1))
-                _launch("conv_dgrad", nb, fl, L.net_group, tab.data_ptr(), i1 - i0, dt, klass, grid, lds, s)
             else:
                 _, i0, i1, klass, grid, lds, tab = g
                 nb = sum(items[i][2] for i in range(i0, i1))
                 fl = sum(items[i][3] for i in range(i0, i1))
-                bar = chain_barrier(id(self), tab.device)
-                _launch("net_chain_bwd", nb, fl, L.net_chain, tab.data_ptr(), i1 - i0, dt, klass, grid, lds, gbase,
-                        bar.data_ptr(), s)
+                _launch("conv_dgrad", nb, fl, L.net_group, tab.data_ptr(), i1 - i0, dt, klass, grid, lds, s)
         # in_bn backward closes the critical path (dL/dx of the coupling) ...
         a.gh0, a.cs_gh0 = sar.ptr("g:h0"), chan_stride(self.P.buf_ch["h0"])
         a.in_bwd_sums = sar.ptr("in_bwd_sums")

@@ -107,6 +107,10 @@ class FlowTrainer:
         self.dtype = dtype
         self.seed = seed
         self.pg = process_group
+        self.rank = 0
+        if process_group is not None:
+            import torch.distributed as dist
+            self.rank = dist.get_rank(process_group)
         model.set_precision(dtype)
         model.train()
         self._build_arenas()
@@ -122,7 +126,6 @@ class FlowTrainer:
             raise ValueError("reduce_dtype must be 'fp32' or 'bf16'")
         self.comm, self.reduce_dtype = comm, reduce_dtype
         self._reduce_pg = None
-        self._cap_pg = None
         self.comm_events = None
         self.comm_stream = None
         if self.pg is not None and comm == "overlap":
@@ -140,6 +143,7 @@ class FlowTrainer:
         self.side_group = int(os.environ.get("RNVP_SIDE_GROUP", "0")) if (overlap and process_group is None) else 0
         self._build_adam_ranges()
         self._build_buckets()
+        self._cap_pg = self._capture_group()
 
     # ----------------------------------------------------------------- arenas
     def _build_arenas(self):
@@ -279,20 +283,21 @@ class FlowTrainer:
         stream joins the graph, and an event poll on a capturing stream is a
         fatal HIP error (it aborted the world-1 test twice in round 2, when a
         warm-up all-reduce was still on the watchdog's list).  So the capture
-        uses a second group over the same ranks, created here, connected
-        eagerly (no collective) and used ONLY inside captures: its watchdog
-        list is empty by construction, and the warm-up group's stream never
-        captures.  Collectives issued while capturing are not handed to any
-        watchdog.  gloo (CPU tests) needs no second group."""
+        uses a second group over the same ranks, created at construction
+        (every rank of the trainer's group constructs its trainer; local
+        synchronisation, so a process_group that is a subgroup of a larger
+        world does not need the ranks outside it), connected eagerly (no
+        collective) and used ONLY inside captures: its watchdog list is empty
+        by construction, and the warm-up group's stream never captures.
+        Collectives issued while capturing are not handed to any watchdog.
+        gloo (CPU tests) needs no second group."""
         if self.pg is None or self.comm_stream is None:
             return None
-        if getattr(self, "_cap_pg", None) is not None:
-            return self._cap_pg
         import torch.distributed as dist
         if dist.get_backend(self.pg) != "nccl":
             return self.pg
         ranks = dist.get_process_group_ranks(self.pg)
-        g = dist.new_group(ranks=ranks, backend="nccl")
+        g = dist.new_group(ranks=ranks, backend="nccl", use_local_synchronization=True)
         g._get_backend(self.dev).eager_connect_single_device(self.dev)
         return g
 
@@ -510,7 +515,6 @@ class FlowTrainer:
         torch.cuda.synchronize()
         # the captured all-reduces go through a group of their own (see
         # _capture_group); warm-up and eager collectives stay on self.pg
-        self._cap_pg = self._capture_group()
         if before_capture is not None:
             before_capture()
         self.graph = torch.cuda.CUDAGraph()
@@ -629,8 +633,10 @@ class FlowTrainer:
     def rng_state(self):
         """The dequantisation noise stream: k_logit_fwd draws step t's noise
         from Philox(seed, counter = t), so (seed, t) is the whole RNG state
-        (the reference saves none, train.py:249-250)."""
-        return {"seed": int(self.seed), "step": int(self.step_t.item())}
+        (the reference saves none, train.py:249-250).  The
+        saving rank is recorded: data-parallel ranks draw from seeds of their
+        own."""
+        return {"seed": int(self.seed), "rank": int(self.rank), "step": int(self.step_t.item())}
 
     def state_dict(self):
         """{'model': model.state_dict(), 'optimizer': torch-Adam-format state,
@@ -645,7 +651,11 @@ class FlowTrainer:
         self.load_optimizer_state_dict(sd["optimizer"])
         rng = sd.get("rng")
         if rng is not None:
-            if int(rng["seed"]) != self.seed:
+            # a checkpoint of THIS rank resumes its noise stream exactly; one
+            # saved by another rank (usually rank 0 for all) restores only the
+            # step counter, so every replica keeps drawing its own noise
+            own = int(rng.get("rank", 0)) == self.rank
+            if own and int(rng["seed"]) != self.seed:
                 self.seed = int(rng["seed"])
                 self.drop_graph()    # the seed is a captured launch argument
             self.step_t.fill_(int(rng["step"]))

@@ -305,46 +305,20 @@ int rnvp_adam_update(float* param, float* grad, float* exp_avg, float* exp_avg_s
                      float weight_decay, const uint8_t* mask, float reg_coef, void* stream);
 int rnvp_step_increment(long long* step, void* stream);
 
-/* ---- persistent net chain -----------------------------------------------
- * A run of consecutive s/t-net steps of one coupling -- convs (rnvp_conv2d
- * semantics, deep-scale family) and BatchNorm-backward applies
- * (rnvp_bn_bwd_apply semantics) -- in ONE launch: the workgroups stay
- * resident and meet at a grid barrier between steps instead of at a kernel
- * boundary.  Replaces, for the deep scales (M = B*H*W <= 4096 pixels), the
- * chain of dependent launches ResidualModule.forward (modules_realnvp.py:
- * 175-194, via 107-114 and 64-71) and its autograd backward decompose into.
- * Each step reads what the previous one wrote (an agent-scope release /
- * acquire at the barrier); BatchNorm sums produced by a step's epilogue are
- * complete when the next step's prologue reads them.
- *   rnvp_net_chain_prepare (host): validates the host copy of the steps and
- *     fills the derived fields (cfg, nc, shards, tile order, tiles);
- *     RNVP_E_UNSUPPORTED when a step has no chain form (the caller launches
- *     that step on its own).  Returns the grid (resident workgroups) and LDS.
- *     Every conv step of one chain shares a kernel class (the deep
- *     configuration and channel chunks per wave), and the steps are all
- *     forward ones (convs, with or without the BN prologue) or all backward
- *     ones (data-gradient convs without prologue, BN-backward applies);
- *     klass names the kernel.
- *   rnvp_net_chain: launches the prepared steps (device copy of the table,
- *     klass / grid / lds_bytes as prepared).
- *     grad_base: BN-backward steps write dgamma / dbeta at grad_base +
- *     dgamma_off / dbeta_off (elements, < 0 = not written).  barrier:
- *     RNVP_NET_CHAIN_BARRIER_BYTES of device memory, zero when first used
- *     (the chain leaves it reusable); word 2 becomes non-zero if a barrier
- *     ever timed out (a non-resident grid: results invalid, no hang). */
+/* ---- net steps ------------------------------------------------------------
+ * One s/t-net step as a table entry (rnvp_net_group): a conv (rnvp_conv2d
+ * semantics) or a BatchNorm-backward apply (rnvp_bn_bwd_apply semantics).
+ * grad_base-relative dgamma_off / dbeta_off (elements, < 0 = not written)
+ * locate a BN step's affine gradients. */
 enum { RNVP_STEP_CONV = 0, RNVP_STEP_BN_BWD = 1 };
-#define RNVP_NET_CHAIN_BARRIER_BYTES 64
 typedef struct rnvp_net_step {
     int kind;
     rnvp_conv_args conv;
     rnvp_bn_bwd_args bn;
     long long dgamma_off, dbeta_off;
-    /* filled by rnvp_net_chain_prepare */
+    /* filled by rnvp_net_group_prepare */
     int cfg, nc, shards, xa, xb, tiles;
 } rnvp_net_step;
-int rnvp_net_chain_prepare(rnvp_net_step* steps_host, int n, int* klass, int* grid, int* lds_bytes);
-int rnvp_net_chain(const rnvp_net_step* steps_device, int n, int dtype, int klass, int grid, int lds_bytes,
-                   float* grad_base, void* barrier, void* stream);
 
 /* ---- grouped 1x1 convs --------------------------------------------------
  * Up to RNVP_NET_GROUP_MAX INDEPENDENT 1x1 convs of one net (same pixels; no

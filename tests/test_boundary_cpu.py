@@ -144,3 +144,62 @@ def test_reference_train_py_import_line():
     weights_init(bn)
     assert abs(float(conv.weight.std()) - 0.02) < 0.01
     assert float(bn.bias.abs().max()) == 0.0 and abs(float(bn.weight.mean()) - 1.0) < 0.02
+
+
+def test_net_group_prepare_rejections():
+    """rnvp_net_group_prepare is host-only validation (no HIP call): it groups
+    independent deep-scale 1x1 convs and refuses what has no grouped form
+    (RNVP_E_UNSUPPORTED = -2: the engine then launches them one by one) or is
+    malformed (RNVP_E_INVALID = -1).  Pointers are never dereferenced here."""
+    from realnvp_hip import _lib
+    from realnvp_hip._lib import ConvArgs, NetStep
+    L = _lib.lib()
+    fake = 1 << 20     # 16-B aligned, never dereferenced
+
+    def step(B=64, H=4, W=4, cs=512, n=512, ks=1, dtype=0, kind=0, x=fake):
+        st = NetStep()
+        st.kind = kind
+        a = st.conv
+        a.dtype, a.B, a.H, a.W, a.ks = dtype, B, H, W, ks
+        a.x, a.cs_in, a.cin, a.w, a.kp = x, cs, cs, fake, (ks * ks * cs + 63) // 64 * 64
+        a.y, a.cs_out, a.n = fake, n, n
+        return st
+
+    def prep(*steps):
+        arr = (NetStep * len(steps))(*steps)
+        k, g, lb = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        rc = L.net_group_prepare(arr, len(steps), ctypes.byref(k), ctypes.byref(g), ctypes.byref(lb))
+        return rc, k.value, g.value, lb.value, arr
+
+    rc, k, g, lb, arr = prep(step(), step())
+    assert rc == 0 and g == 2 * arr[0].tiles and 0 < lb <= 160 * 1024
+    assert rc == 0 and arr[0].tiles == arr[1].tiles > 0
+    assert prep(step(), step(ks=3))[0] == -2                     # a 3x3 member
+    assert prep(step(), step(kind=1))[0] == -2                   # a BN-backward step
+    assert prep(step(), step(B=32))[0] == -2                     # other pixels
+    assert prep(step(B=64, H=32, W=32), step(B=64, H=32, W=32))[0] == -2   # M = 65536 > 16384
+    assert prep(step(), step(dtype=1))[0] == -2                  # mixed dtypes
+    assert prep(step(), step(x=fake + 4))[0] == -1               # misaligned operand
+    assert prep(step(), step(x=0))[0] == -1                      # NULL operand
+    assert prep(*[step() for _ in range(_lib.NET_GROUP_MAX + 1)])[0] == -1   # too many members
+
+
+def test_factor_out_refuses_non_canonical_order_matrix():
+    """factor_out / restore implement order_matrix(C)'s permutation; another
+    0/1 kernel (which the reference would convolve with,
+    flow_realnvp.py:167-193) is refused instead of silently differing"""
+    import flow_realnvp
+    m = flow_realnvp.RealNVP(3, 16, torch.distributions.Normal(torch.tensor(0.), torch.tensor(1.)), _hp(4, 1))
+    x = torch.zeros(2, 3, 16, 16)
+    bad = m.order_matrix_1.clone()
+    bad[0, 0, 0, 0], bad[0, 0, 1, 1] = 0.0, 1.0
+    with pytest.raises(ValueError, match="canonical"):
+        m.factor_out(x, bad)
+    half = torch.zeros(2, 6, 8, 8)
+    with pytest.raises(ValueError, match="canonical"):
+        m.restore(half, half, bad)
+    with pytest.raises(ValueError, match="shape"):
+        m.factor_out(x, m.order_matrix(6))
+    # the canonical matrix passes the check (then the CPU tensor is refused)
+    with pytest.raises(RuntimeError, match="HIP device"):
+        m.factor_out(x, m.order_matrix_1)

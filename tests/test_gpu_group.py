@@ -1,0 +1,155 @@
+"""Grouped launches of independent 1x1 convs (rnvp_net_group, csrc/conv_deep.hip)
+against the same convs launched one by one (RNVP_NET_GROUP=0).
+
+The engine groups each core_skips[i] forward with the next block's first 1x1
+and the data gradients of in_skip + every core_skips[i]
+(modules_realnvp.py:175-194).  A grouped tile runs the same deep_tile body as
+the single launch with the same configuration (rnvp_net_group_prepare takes
+every member's single-launch choice), so forward outputs, the data gradient
+and every parameter gradient must agree up to the order of the fp64
+BatchNorm-sum atomics: checked on bottleneck+skip couplings at M = 256, 1024,
+4096 and 16384 pixels (both sides of the 8-wave / 4-wave boundary at 1024 and
+the group's 16384-pixel limit), fp32 and bf16, and through the C ABI.
+"""
+import ctypes as C
+
+import pytest
+import torch
+
+from formula_init import formula_state
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel(a, b):
+    a, b = a.double().flatten(), b.double().flatten()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+def _run_coupling(kind, cio, mid, size, B, dtype, group, seed=0):
+    import modules_realnvp as MR
+    import utils
+    from realnvp_hip import engine
+    old = engine.NET_GROUP
+    engine.NET_GROUP = int(group)
+    try:
+        torch.manual_seed(seed)
+        hp = utils.Hyperparameters(32, 4, True, True, True, True)
+        mod = MR.CheckerboardAffineCoupling(cio, mid, size, 1.0, hp) if kind == "ckbd" else \
+            MR.ChannelwiseAffineCoupling(cio, mid, 0.0, hp)
+        mod.load_state_dict(formula_state(mod, style="chirp"))
+        mod = mod.to(DEV).train()
+        mod.compute_dtype = dtype
+        g = torch.Generator().manual_seed(seed + 1)
+        x = torch.randn(B, cio, size, size, generator=g).to(DEV).requires_grad_(True)
+        gy = torch.randn(B, cio, size, size, generator=g).to(DEV)
+        gl = torch.randn(B, cio, size, size, generator=g).to(DEV)
+        y, ldj = mod(x)
+        (y * gy + ldj * gl).sum().backward()
+        torch.cuda.synchronize()
+        grads = {n: p.grad.clone() for n, p in mod.named_parameters() if p.grad is not None}
+        return y.detach(), ldj.detach(), x.grad.clone(), grads, mod.engine()
+    finally:
+        engine.NET_GROUP = old
+
+
+CASES = [
+    # name, kind, in_out_dim, mid, size, batch: M = batch * size^2
+    ("s5_ckbd_m256", "ckbd", 48, 512, 4, 16),
+    ("s5_ckbd_m1024", "ckbd", 48, 512, 4, 64),
+    ("s4_chan_m1024", "chan", 96, 512, 4, 64),
+    ("s4_ckbd_m4096", "ckbd", 24, 256, 8, 64),
+    ("s3_ckbd_m16384", "ckbd", 12, 128, 16, 64),
+]
+
+
+def _plans(eng):
+    svs = [sv for pool in eng._saved_pool.values() for sv in pool]
+    assert svs, "no saved arena"
+    return svs[0]["fwd_plan"][2], svs[0]["bwd_plan"][2]
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_grouped_matches_single_launches(case, dtype):
+    _, kind, cio, mid, size, B = case
+    y0, l0, gx0, g0, e0 = _run_coupling(kind, cio, mid, size, B, dtype, group=False)
+    y1, l1, gx1, g1, e1 = _run_coupling(kind, cio, mid, size, B, dtype, group=True)
+    f0, b0 = _plans(e0)
+    f1, b1 = _plans(e1)
+    assert all(p[0] == "single" for p in f0 + b0)
+    # grouping really happened: R = 4 skip convs -> 3 forward groups (skip i
+    # beside block i+1's first 1x1), one backward group (in_skip + 4 skips)
+    assert sum(p[0] == "group" for p in f1) >= 3, [p[:3] for p in f1]
+    assert any(p[0] == "group" and p[2] - p[1] >= 5 for p in b1), [p[:3] for p in b1]
+    # same tiles, same per-tile arithmetic: only the fp64 batch-sum order
+    # differs (fp32: exact up to it; bf16: one rounding of bf16 outputs can flip)
+    fw = 1e-6 if dtype == "fp32" else 2e-3
+    bw = 1e-5 if dtype == "fp32" else 1e-2
+    assert rel(y1, y0) < fw and rel(l1, l0) < fw, (rel(y1, y0), rel(l1, l0))
+    assert rel(gx1, gx0) < bw, rel(gx1, gx0)
+    # biases of convs that feed only a BatchNorm have a zero gradient in exact
+    # arithmetic: errors are measured against the largest gradient norm
+    gmax = max(float(g0[n].norm()) for n in g0)
+    worst = max((float((g1[n] - g0[n]).norm()) / (float(g0[n].norm()) + 1e-3 * gmax), n) for n in g0)
+    assert worst[0] < 10 * bw, worst
+
+
+def test_group_c_abi_two_skip_convs():
+    """two independent 1x1 convs (one with a BN+ReLU prologue) through
+    rnvp_net_group_prepare / rnvp_net_group against two rnvp_conv2d launches
+    and torch"""
+    from realnvp_hip import _lib
+    from realnvp_hip._lib import BNSrc, ConvArgs, NetStep
+    from realnvp_hip.engine import stat_shards, upload
+    L = _lib.lib()
+    B, H, W, Cc = 64, 4, 4, 512
+    M = B * H * W
+    torch.manual_seed(3)
+    x = torch.randn(M, Cc, device=DEV)
+    w1 = torch.randn(Cc, Cc, device=DEV) * 0.05
+    w2 = torch.randn(Cc, Cc, device=DEV) * 0.05
+    sh = stat_shards(M)
+    bsum = torch.zeros(sh, 2, Cc, device=DEV, dtype=torch.float64)
+    bsum[0, 0] = x.double().sum(0)
+    bsum[0, 1] = (x.double() ** 2).sum(0)
+    gam = torch.rand(Cc, device=DEV) + 0.5
+    bet = torch.randn(Cc, device=DEV) * 0.1
+    s = torch.cuda.current_stream().cuda_stream
+
+    def run(grouped):
+        y1 = torch.zeros(M, Cc, device=DEV)
+        y2 = torch.zeros(M, Cc, device=DEV)
+        a1 = ConvArgs()
+        a1.dtype, a1.B, a1.H, a1.W, a1.ks = 0, B, H, W, 1
+        a1.x, a1.cs_in, a1.cin, a1.w, a1.kp = x.data_ptr(), Cc, Cc, w1.data_ptr(), Cc
+        a1.y, a1.cs_out, a1.n = y1.data_ptr(), Cc, Cc
+        a2 = ConvArgs()
+        a2.dtype, a2.B, a2.H, a2.W, a2.ks = 0, B, H, W, 1
+        a2.x, a2.cs_in, a2.cin, a2.w, a2.kp = x.data_ptr(), Cc, Cc, w2.data_ptr(), Cc
+        a2.y, a2.cs_out, a2.n = y2.data_ptr(), Cc, Cc
+        a2.pro_bn_relu = 1
+        a2.pro = BNSrc(bsum.data_ptr(), float(M), None, None, gam.data_ptr(), bet.data_ptr(), 1e-5, sh)
+        if grouped:
+            steps = (NetStep * 2)()
+            for st, a in zip(steps, (a1, a2)):
+                st.kind, st.conv, st.dgamma_off, st.dbeta_off = 0, a, -1, -1
+            k, g, lb = C.c_int(), C.c_int(), C.c_int()
+            assert L.net_group_prepare(steps, 2, C.byref(k), C.byref(g), C.byref(lb)) == 0
+            tab = upload(bytes(steps), DEV)
+            L.net_group(tab.data_ptr(), 2, 0, k.value, g.value, lb.value, s)
+        else:
+            L.conv2d(C.byref(a1), s)
+            L.conv2d(C.byref(a2), s)
+        torch.cuda.synchronize()
+        return y1, y2
+
+    y1s, y2s = run(False)
+    y1g, y2g = run(True)
+    assert rel(y1g, y1s) < 1e-6 and rel(y2g, y2s) < 1e-6
+    mean = bsum[0, 0] / M
+    var = bsum[0, 1] / M - mean * mean
+    act = torch.relu((x - mean.float()) / torch.sqrt(var.float() + 1e-5) * gam + bet)
+    assert rel(y1g, x @ w1.t()) < 1e-5
+    assert rel(y2g, act @ w2.t()) < 1e-5

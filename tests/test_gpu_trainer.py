@@ -371,7 +371,7 @@ def test_checkpoint_carries_the_noise_stream():
     for _ in range(2):
         ta.step()
     sd = ta.state_dict()
-    assert sd["rng"] == {"seed": 1234, "step": 2}
+    assert sd["rng"] == {"seed": 1234, "rank": 0, "step": 2}
     tb = FlowTrainer(make_model(32, 8, 1), 4, dtype="fp32", seed=7)
     tb.load_state_dict(sd)
     assert tb.seed == 1234 and int(tb.step_t.item()) == 2
@@ -383,6 +383,63 @@ def test_checkpoint_carries_the_noise_stream():
     np.testing.assert_allclose(tb.mean_logll(1), ta.mean_logll(1), rtol=1e-6)
     assert torch.equal(tb.xl, ta.xl)    # the same noise was drawn
     assert float((tb.param - ta.param).abs().max()) <= 2 * ta.lr * 1.01
+
+
+def _resume_rank(rank, port, ckpt, out):
+    """world-2 (gloo) rank: rank 0 saves after one step, every rank resumes
+    from rank 0's checkpoint and takes one more step"""
+    import torch.distributed as dist
+    from realnvp_hip.dist import rank_seed
+    from realnvp_hip.trainer import FlowTrainer
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        tr = FlowTrainer(make_model(32, 8, 1), 4, dtype="fp32", seed=rank_seed(1000, rank),
+                         process_group=dist.group.WORLD, comm="split")
+        tr.set_pixels(pixels(4, 3, 32, seed=5).to(DEV))     # the same pixels on both ranks
+        tr.step()
+        if rank == 0:
+            torch.save(tr.state_dict(), ckpt)
+        dist.barrier()
+        tb = FlowTrainer(make_model(32, 8, 1), 4, dtype="fp32", seed=rank_seed(1000, rank),
+                         process_group=dist.group.WORLD, comm="split")
+        tb.load_state_dict(torch.load(ckpt, weights_only=True))
+        tb.set_pixels(pixels(4, 3, 32, seed=5).to(DEV))
+        tb.step()
+        torch.cuda.synchronize()
+        torch.save({"seed": tb.seed, "step": int(tb.step_t.item()), "xl": tb.xl.cpu()}, out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_resume_from_rank0_checkpoint_keeps_per_rank_noise(tmp_path):
+    """data-parallel ranks resumed from rank 0's checkpoint keep
+    their own dequantisation seeds (only the step counter is restored), so
+    the replicas still draw different noise"""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ckpt = str(tmp_path / "ckpt.pt")
+    outs = [str(tmp_path / ("rank%d.pt" % r)) for r in range(2)]
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_resume_rank, args=(r, port, ckpt, outs[r])) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+            p.join()
+    assert [p.exitcode for p in procs] == [0, 0]
+    r0, r1 = [torch.load(o, weights_only=True) for o in outs]
+    from realnvp_hip.dist import rank_seed
+    assert r0["seed"] == rank_seed(1000, 0) and r1["seed"] == rank_seed(1000, 1)
+    assert r0["step"] == r1["step"] == 2
+    assert not torch.equal(r0["xl"], r1["xl"])     # different noise on the same pixels
 
 
 def test_dropin_backward_between_trainer_steps():

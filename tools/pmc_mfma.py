@@ -46,7 +46,7 @@ def main():
     for f in fams:
         agg[f]["launches"] += 1
     adam = [(n, v) for _, n, v in dispatches(d, "SQ_VALU_MFMA_BUSY_CYCLES") if re.search(r"\bk_adam", n)]
-    out = dict(config=meta.get("config"), formula="100 * MFMA_BUSY / (GRBM_GUI_ACTIVE / 8 * 1024)", families={})
+    out = dict(config=meta.get("config"), stamp=meta.get("stamp"), formula="100 * MFMA_BUSY / (GRBM_GUI_ACTIVE / 8 * 1024)", families={})
     for f, a in sorted(agg.items(), key=lambda kv: -kv[1]["GRBM_GUI_ACTIVE"]):
         cyc = a["GRBM_GUI_ACTIVE"] / XCDS
         util = 100.0 * a["SQ_VALU_MFMA_BUSY_CYCLES"] / max(cyc * SIMDS, 1.0)

@@ -83,7 +83,7 @@ def main():
         a["kernels"] += len(f)
         a["read"] += sum(v for _, v in f) * 1024.0 * 2.0
         a["write"] += sum(v for _, v in w) * 1024.0
-    res = dict(config=meta.get("config"), correction="bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024", families={},
+    res = dict(config=meta.get("config"), stamp=meta.get("stamp"), correction="bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024", families={},
                adam_calibration=dict(measured=adam, n_params=meta.get("n_params")))
     alg = meta.get("alg_bytes", {})
     for fam, a in sorted(agg.items(), key=lambda kv: -kv[1]["read"] - kv[1]["write"]):

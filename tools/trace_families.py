@@ -45,7 +45,7 @@ def main():
         for r in seg[i0 + 1:i1]:
             a["kernels"] += 1
             a["us"] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-    out = dict(config=meta.get("config"), source="rocprofv3 kernel trace, graph-replayed step", families={})
+    out = dict(config=meta.get("config"), stamp=meta.get("stamp"), source="rocprofv3 kernel trace, graph-replayed step", families={})
     for f, a in sorted(agg.items(), key=lambda kv: -kv[1]["us"]):
         out["families"][f] = dict(launches=a["launches"], kernels=a["kernels"], total_ms=round(a["us"] / 1e3, 3),
                                   avg_launch_us=round(a["us"] / a["launches"], 2))
