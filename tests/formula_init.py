@@ -102,3 +102,35 @@ def pixels(batch, channels, size, seed=0):
 def uniform_noise(batch, channels, size, seed=1):
     rng = np.random.Generator(np.random.PCG64(seed))
     return torch.from_numpy(rng.random((batch, channels, size, size)).astype(np.float32))
+
+
+# ---------------------------------------------------------------------------
+# gradient projection checksums: <g, r_k> / |r_k| for K closed-form vectors
+# r_k[i] = cos(2 pi frac((i + 1) * PHI_k) + k), quasi-random and regenerated on
+# any box from the element index alone.  A permuted, mis-scattered or
+# sign-flipped gradient with the right norm moves its projections by
+# ~|g| / sqrt(n) each, like an error of its own size would.
+PROJ_PHI = (0.6180339887498949, 0.4142135623730951, 0.7320508075688772, 0.2360679774997898)
+
+
+def projections(g):
+    """[K] float64 projection checksums of one gradient tensor (any device)."""
+    t = g.detach().reshape(-1).double()
+    i = torch.arange(1, t.numel() + 1, dtype=torch.float64, device=t.device)
+    out = []
+    for k, phi in enumerate(PROJ_PHI):
+        r = torch.cos(2.0 * np.pi * torch.frac(i * phi) + k)
+        out.append(float(torch.dot(t, r) / r.norm()))
+    return np.array(out)
+
+
+def projection_matrix(grads):
+    """[n_tensors, K] projections of a list of gradient tensors"""
+    return np.stack([projections(g) for g in grads])
+
+
+def largest(names, sizes, n=10):
+    """the n largest tensors (by element count; ties by name order): those
+    whose full gradients the trainer tests compare element by element"""
+    order = sorted(range(len(names)), key=lambda i: (-sizes[i], i))
+    return [names[i] for i in sorted(order[:n])]

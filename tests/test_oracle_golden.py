@@ -173,3 +173,25 @@ def test_trainer_trajectory(case):
     with torch.no_grad():
         lp = O.log_prob(S, spec, torch.from_numpy(g["x"]), training=False)
     np.testing.assert_allclose(lp.numpy(), g["traj_eval_logprob_after"], rtol=1e-4)
+
+
+def test_oracle_gradient_values_at_config1():
+    """The oracle's fp32 training step at the benchmarked configuration
+    (config 1, B = 64, formula weights) against the reference's gradient
+    VALUES (tools/make_goldens.py:grads_golden): projection checksums of every
+    tensor as close to the float64 truth as the reference's own (x3), with the
+    same per-tensor tail rule the GPU trainer test applies."""
+    from formula_init import projection_matrix
+    from realnvp_bf16emu import run
+    from test_gpu_deep import check_projections_vs_truth, model_inputs
+    v = load_golden("grads_m64_d32_r4_b64.npz")
+    spec = O.FlowSpec(3, 64, O.HP(32, 4))
+    entries = O.flow_spec_entries(spec)
+    train = O.trainable_names(entries)
+    assert train == list(v["grad_names"])
+    x, ld = model_inputs(64, 64)
+    grads = run(O.build_state(entries, formula_value), spec, train, x, ld, None, full=True)[4]
+    P = projection_matrix([grads[n] for n in train])
+    check_projections_vs_truth(P, v["ref_grad_proj"], v["truth_grad_proj"])
+    # the stored oracle projections are this very computation (another host)
+    assert np.linalg.norm(P - v["oracle_grad_proj"]) / np.linalg.norm(v["oracle_grad_proj"]) < 1e-3

@@ -1,5 +1,6 @@
 """bf16-faithful golden for the benchmarked path (test infrastructure, CPU).
 
+The emulation itself lives in oracle/realnvp_bf16emu.py (the GPU test re-runs it).
 The bench line times the bf16 s/t-network step of config 1 (64x64x3, R4, D32,
 B=64).  Against the fp32 reference that step is ~0.3 off in gradient (the
 precision of bf16 activations through 28 batch-statistic couplings), which
@@ -40,119 +41,10 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
-import torch.nn.functional as F  # noqa: E402
 
 import realnvp_oracle as O  # noqa: E402
-from formula_init import chirp_value, pixels, uniform_noise  # noqa: E402
-
-
-class _R(torch.autograd.Function):
-    """bf16 storage of a value and of the gradient flowing back into it."""
-    @staticmethod
-    def forward(ctx, t):
-        return t.bfloat16().float()
-
-    @staticmethod
-    def backward(ctx, g):
-        return g.bfloat16().float()
-
-
-class _RF(torch.autograd.Function):
-    """bf16 operand in the forward only (packed weights)."""
-    @staticmethod
-    def forward(ctx, t):
-        return t.bfloat16().float()
-
-    @staticmethod
-    def backward(ctx, g):
-        return g
-
-
-class Emu:
-    """The oracle's residual module with the engine's bf16 rounding points;
-    wide=True accumulates every conv in fp64 (the summation-order variant)."""
-
-    def __init__(self, wide):
-        self.wide = wide
-
-    def conv_raw(self, S, p, x):
-        w = _RF.apply(O.wn_weight(S, p + "conv."))
-        b = S.get(p + "conv.bias")
-        pad = w.shape[-1] // 2
-        if self.wide:
-            return _Wide.apply(x, w, pad) + (b.view(1, -1, 1, 1) if b is not None else 0.0)
-        return F.conv2d(x, w, b, padding=pad)
-
-    def operand(self, S, p, x, training):
-        """ReLU(BN(x)) as the MFMA operand (rounded when packed)."""
-        return _R.apply(F.relu(O.batch_norm(S, p, x, training)))
-
-    def block(self, S, p, x, training, bottleneck, skip_in, skip_p):
-        r = p + "res_block."
-        h = self.operand(S, p + "in_block.0.", x, training)
-        if bottleneck:
-            h = _R.apply(self.conv_raw(S, r + "0.", h))
-            h = self.operand(S, r + "1.", h, training)
-            h = _R.apply(self.conv_raw(S, r + "3.", h))
-            h = self.operand(S, r + "4.", h, training)
-            y = _R.apply(self.conv_raw(S, r + "6.", h) + x)       # residual in the epilogue
-        else:
-            h = _R.apply(self.conv_raw(S, r + "0.", h))
-            h = self.operand(S, r + "1.", h, training)
-            y = _R.apply(self.conv_raw(S, r + "3.", h) + x)
-        out = None
-        if skip_in is not None:
-            out = _R.apply(skip_in + self.conv_raw(S, skip_p, y))  # skip accumulation
-        return y, out
-
-    def module(self, S, p, h0, training, hp):
-        assert hp.res_blocks > 0 and hp.skip, "config-1 net (skip, res_blocks > 0)"
-        x = _R.apply(self.conv_raw(S, p + "in_block.", h0))
-        out = _R.apply(self.conv_raw(S, p + "in_skip.", x))
-        for i in range(hp.res_blocks):
-            x, out = self.block(S, p + "core_block.%d." % i, x, training, hp.bottleneck, out,
-                                p + "core_skips.%d." % i)
-        h = self.operand(S, p + "out_block.0.", out, training)
-        return _R.apply(self.conv_raw(S, p + "out_block.2.", h))
-
-
-class _Wide(torch.autograd.Function):
-    """conv2d accumulated in fp64, result rounded to fp32 (forward and both
-    backward products): an fp32-grade conv with a different summation."""
-    @staticmethod
-    def forward(ctx, x, w, pad):
-        ctx.save_for_backward(x, w)
-        ctx.pad = pad
-        return F.conv2d(x.double(), w.double(), padding=pad).float()
-
-    @staticmethod
-    def backward(ctx, g):
-        x, w = ctx.saved_tensors
-        gd = g.double()
-        gx = torch.nn.grad.conv2d_input(x.shape, w.double(), gd, padding=ctx.pad).float()
-        gw = torch.nn.grad.conv2d_weight(x.double(), w.shape, gd, padding=ctx.pad).float()
-        return gx, gw, None
-
-
-def run(S0, spec, train, x, ld, emu):
-    S = {k: v.clone() for k, v in S0.items()}
-    for n in train:
-        S[n].requires_grad_(True)
-    saved = O.residual_module
-    if emu is not None:
-        def rm(S_, p, h, training, res_blocks, bottleneck, skip):
-            return emu.module(S_, p, _R.apply(h), training, spec.hp)
-        O.residual_module = rm
-    try:
-        lp = O.log_prob(S, spec, x.clone(), training=True)
-        names = O.param_names(O.flow_spec_entries(spec))
-        ws = O.weight_scale(S, names, lambda n: n in train)
-        loss = -(lp + ld).mean() + 5e-5 * ws
-        grads = torch.autograd.grad(loss, [S[n] for n in train], allow_unused=True)
-    finally:
-        O.residual_module = saved
-    norms = np.array([float(g.double().norm()) if g is not None else 0.0 for g in grads])
-    return lp.detach().numpy().astype(np.float64), float(loss), norms
+from formula_init import chirp_value, largest, pixels, uniform_noise  # noqa: E402
+from realnvp_bf16emu import Emu, run  # noqa: E402
 
 
 def model_inputs(B, size):
@@ -176,10 +68,11 @@ def main():
     S0 = O.build_state(entries, chirp_value)
     train = O.trainable_names(entries)
     x, ld = model_inputs(a.batch, a.size)
-    res = {}
+    res, full = {}, {}
     for tag, emu in (("fp32", None), ("emu", Emu(False)), ("emu_wide", Emu(True))):
         t0 = time.time()
-        res[tag] = run(S0, spec, train, x, ld, emu)
+        r = run(S0, spec, train, x, ld, emu, full=True)
+        res[tag], full[tag] = r[:4], r[4:]
         print("%-9s loss %.6f  (%.1f s)" % (tag, res[tag][1], time.time() - t0), flush=True)
 
     def rel(u, v):
@@ -192,10 +85,30 @@ def main():
         float(np.max(np.abs(res["emu"][0] - res["emu_wide"][0]) / np.abs(res["emu_wide"][0]))),
         rel(res["emu"][2], res["emu_wide"][2]), abs(res["emu"][1] - res["emu_wide"][1]) / abs(res["emu_wide"][1])))
     out = dict(grad_names=np.array(train))
-    for t, (lp, loss, norms) in res.items():
+    for t, (lp, loss, norms, proj) in res.items():
         out[t + "_logprob"] = lp
         out[t + "_loss"] = np.float64(loss)
         out[t + "_grad_norms"] = norms
+        out[t + "_grad_proj"] = proj
+    # element-wise floors of the 10 largest tensors and of dL/dx: the largest
+    # relative L2 distance between any two of the three CPU references (the
+    # GPU test recomputes the "emu" tensors with this same emulation and
+    # holds the HIP step to 3x these floors)
+    sizes = [full["fp32"][0][n].numel() for n in train]
+    big = largest(train, sizes)
+    out["full_names"] = np.array(big)
+    tags = list(full)
+
+    def trel(a, b):
+        a, b = a.double(), b.double()
+        return float((a - b).norm() / b.norm())
+    pairs = [("emu", "emu_wide"), ("emu", "fp32"), ("emu_wide", "fp32")]
+    out["full_pairs"] = np.array(["%s~%s" % p for p in pairs])
+    out["full_floor"] = np.array([[trel(full[a][0][n], full[b][0][n]) for a, b in pairs] for n in big])
+    out["grad_x_floor"] = np.array([trel(full[a][1], full[b][1]) for a, b in pairs])
+    for n, f in zip(big, out["full_floor"]):
+        print("full-tensor floor %-60s" % n, np.round(f, 4))
+    print("dL/dx floor", np.round(out["grad_x_floor"], 4))
     out["config"] = np.array([a.size, a.base_dim, a.res_blocks, a.batch])
     np.savez_compressed(a.out, **out)
     print("wrote", a.out)

@@ -333,9 +333,72 @@ def model_goldens():
         print(name, "took %.1fs" % (time.time() - t0))
 
 
+def grads_golden(name="m64_d32_r4_b64", size=64, bd=32, rb=4, B=64):
+    """Gradient VALUES of the benchmarked configuration (config 1, B=64,
+    formula weights, the lite golden's batch and loss): per-tensor projection
+    checksums (tests/formula_init.py:projections) of the reference's fp32
+    gradients and of the oracle's float64 truth, and for the 10 largest
+    tensors and dL/dx the element-wise fp32 error floors (relative L2 against
+    the truth) of the reference and of the fp32 oracle, which the GPU test
+    re-runs to compare those tensors element by element."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import realnvp_oracle as O
+    from formula_init import formula_value, largest, projection_matrix
+    t0 = time.time()
+    prior = D.Normal(torch.tensor(0.0), torch.tensor(1.0), validate_args=False)
+    model = flow_realnvp.RealNVP(3, size, prior, hps(bd, rb))
+    model.load_state_dict(formula_state(model))
+    _, _, x_in, logdet = model_inputs(B, size)
+    model.train()
+    xr = x_in.clone().requires_grad_(True)
+    lp, ws = model(xr)
+    (-(lp + logdet).mean() + 5e-5 * ws).backward()
+    names = [n for n, p in model.named_parameters() if p.grad is not None]
+    params = dict(model.named_parameters())
+    ref = {n: params[n].grad.detach().clone() for n in names}
+    ref_gx = xr.grad.detach().clone()
+    print(name, "reference step %.1fs" % (time.time() - t0), flush=True)
+
+    def oracle(dtype):
+        spec = O.FlowSpec(3, size, O.HP(bd, rb))
+        entries = O.flow_spec_entries(spec)
+        S = {k: (v.to(dtype) if v.is_floating_point() else v) for k, v in O.build_state(entries, formula_value).items()}
+        train = O.trainable_names(entries)
+        assert train == names
+        for n in train:
+            S[n].requires_grad_(True)
+        x = x_in.clone().to(dtype).requires_grad_(True)
+        lpo = O.log_prob(S, spec, x, training=True)
+        wso = O.weight_scale(S, O.param_names(entries), lambda n: n in set(train))
+        loss = -(lpo + logdet.to(dtype)).mean() + O.SCALE_REG * wso
+        g = torch.autograd.grad(loss, [x] + [S[n] for n in train])
+        return dict(zip(train, g[1:])), g[0]
+    truth, truth_gx = oracle(torch.float64)
+    o32, o32_gx = oracle(torch.float32)
+    print(name, "oracle fp64 + fp32 %.1fs" % (time.time() - t0), flush=True)
+
+    def trel(a, b):
+        a, b = a.double(), b.double()
+        return float((a - b).norm() / b.norm())
+    big = largest(names, [ref[n].numel() for n in names])
+    d = dict(grad_names=np.array(names), ref_grad_proj=projection_matrix([ref[n] for n in names]),
+             truth_grad_proj=projection_matrix([truth[n] for n in names]),
+             oracle_grad_proj=projection_matrix([o32[n] for n in names]),
+             full_names=np.array(big),
+             ref_full_err=np.array([trel(ref[n], truth[n]) for n in big]),
+             oracle_full_err=np.array([trel(o32[n], truth[n]) for n in big]),
+             ref_grad_x_err=np.float64(trel(ref_gx, truth_gx)), oracle_grad_x_err=np.float64(trel(o32_gx, truth_gx)),
+             oracle_vs_ref_full=np.array([trel(o32[n], ref[n]) for n in big]))
+    print("full-tensor errors vs fp64: reference", np.round(d["ref_full_err"], 5), "oracle",
+          np.round(d["oracle_full_err"], 5), "dL/dx", float(d["ref_grad_x_err"]), float(d["oracle_grad_x_err"]))
+    save("grads_%s.npz" % name, d)
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     which = sys.argv[1:2] or ["index", "logit", "coupling", "model"]
+    if "grads" in which:
+        grads_golden()
     if "index" in which:
         index_maps()
     if "logit" in which:
