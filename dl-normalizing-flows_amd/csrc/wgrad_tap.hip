@@ -47,7 +47,7 @@ template <> struct WtCfg<1> { static constexpr int TCO = 128, TCI = 128, KS = 1,
 template <> struct WtCfg<2> { static constexpr int TCO = 32, TCI = 32, KS = 3, WCO = 2, WCI = 2, WTG = 2, NX = 4, DEPTH = 2, BALL = 1; };
 template <> struct WtCfg<3> { static constexpr int TCO = 64, TCI = 64, KS = 1, WCO = 2, WCI = 4, WTG = 1, NX = 2, DEPTH = 2, BALL = 1; };
 
-__host__ __device__ inline int wt_class(int ks, int cs_in, int cs_dy) {
+inline int wt_class_base(int ks, int cs_in, int cs_dy) {
     if (ks == 3) return (cs_in <= 32 && cs_dy <= 32) ? 2 : 0;
     return (cs_in <= 64 && cs_dy <= 64) ? 3 : 1;
 }
@@ -381,7 +381,11 @@ __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int 
 }
 
 // block -> (conv, slab, co tile, ci tile); consecutive tasks (one slab's tiles,
-// which share the slab's pixels through L2) go to one XCD
+// which share the slab's pixels through L2) go to one XCD.  One kernel per
+// tile class (every conv of the launch has class CLS): each class gets its
+// own register allocation (the 1x1 classes fit more waves per SIMD than the
+// 3x3 ones; one kernel over all classes took the largest class's 207 VGPRs)
+template <int CLS>
 __global__ __launch_bounds__(WT_NT) void k_wgrad_tap(rnvp_wgrad_group g) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int nb = gridDim.x, b = blockIdx.x;
@@ -392,18 +396,50 @@ __global__ __launch_bounds__(WT_NT) void k_wgrad_tap(rnvp_wgrad_group g) {
     const rnvp_wgrad_conv& gc = g.conv[c];
     const WtConv cv{gc.x, gc.dy, gc.ws, gc.wsb, gc.pro, gc.cs_in, gc.cin, gc.cs_dy, gc.n, gc.kp, gc.pro_bn_relu,
                     gc.nz, gc.nrep, g.B, g.H, g.W, gc.m_per_slab};
-    const int cls = wt_class(gc.ks, gc.cs_in, gc.cs_dy);
-    const int tco = (gc.n + wt_tco(cls) - 1) / wt_tco(cls), tci = gc.tk;
+    const int tco = (gc.n + wt_tco(CLS) - 1) / wt_tco(CLS), tci = gc.tk;
     const int local = t - gc.task0;
     const int per = tco * tci;
     const int z = local / per, rr = local - z * per;
     const int cot = rr / tci, cit = rr - cot * tci;
+    wt_body<CLS>(cv, cot, cit, z, lds);
+}
+
+using WtKernel = void (*)(rnvp_wgrad_group);
+WtKernel wt_kernel(int cls) {
     switch (cls) {
-        case 0: wt_body<0>(cv, cot, cit, z, lds); break;
-        case 1: wt_body<1>(cv, cot, cit, z, lds); break;
-        case 2: wt_body<2>(cv, cot, cit, z, lds); break;
-        default: wt_body<3>(cv, cot, cit, z, lds); break;
+        case 0: return k_wgrad_tap<0>;
+        case 1: return k_wgrad_tap<1>;
+        case 2: return k_wgrad_tap<2>;
+        default: return k_wgrad_tap<3>;
     }
+}
+
+// x staging of a 3x3 class fits its NX chunks per thread
+bool wt_stage_fits(int cls, int H, int W) {
+    if (wt_ks(cls) != 3) return true;
+    const int npr = wt_npr(WT_SP / W, H);
+    const int cpi = wt_tci(cls) / 8;
+    const int nx = cls == 0 ? WtCfg<0>::NX : WtCfg<2>::NX;   // class 0: W = 128 (config 4 scale 1) falls back
+    return (long long)npr * (W + 2) * cpi <= (long long)nx * WT_NT;
+}
+
+long long wt_tasks(const rnvp_wgrad_conv& v, int cls) {
+    return (long long)v.nz * ((v.n + wt_tco(cls) - 1) / wt_tco(cls)) * ((v.cs_in + wt_tci(cls) - 1) / wt_tci(cls));
+}
+
+// tile class of a conv: the widest tiles (fewest operand re-reads) unless
+// they leave the GPU short of workgroups -- the deep scales' convs (M <= 16k
+// pixels, nz <= 8 slabs) then take the 32 x 32 (3x3) / 64 x 64 (1x1) tiles:
+// 4x the workgroups.  RNVP_WT_POLICY=0 keeps the channel-count rule only.
+int wt_class(const rnvp_wgrad_conv& v, int H, int W) {
+    static const int policy = [] { const char* e = getenv("RNVP_WT_POLICY"); return e ? atoi(e) : 1; }();
+    const int c = wt_class_base(v.ks, v.cs_in, v.cs_dy);
+    if (policy == 0) return c;
+    const int small = v.ks == 3 ? 2 : 3;
+    if (c != small && wt_tasks(v, c) < 256 && wt_stage_fits(small, H, W) &&
+        wt_lds_bytes(small, H, W) <= 160 * 1024)
+        return small;
+    return c;
 }
 
 }  // namespace
@@ -417,33 +453,38 @@ int rnvp_wgrad_tap_launch(rnvp_wgrad_group* g, hipStream_t s) {
     const int H = g->H, W = g->W;
     if (W > WT_SP || WT_SP % W) return RNVP_E_UNSUPPORTED;            // stages are whole rows
     if ((long long)g->B * (H + 2) >= (1ll << 22) || M >= (1ll << 31)) return RNVP_E_UNSUPPORTED;
-    long long tasks = 0;
-    size_t shm = 0;
+    // validate every conv and pick its class before launching anything
     for (int c = 0; c < g->n_conv; ++c) {
         rnvp_wgrad_conv& v = g->conv[c];
-        const int cls = wt_class(v.ks, v.cs_in, v.cs_dy);
         // 32-bit buffer offsets (bytes)
         if (M * v.cs_in * 2 >= (1ll << 31) || M * v.cs_dy * 2 >= (1ll << 31)) return RNVP_E_UNSUPPORTED;
-        const size_t lb = wt_lds_bytes(cls, H, W);
-        if (lb > 160 * 1024) return RNVP_E_UNSUPPORTED;
-        if (wt_ks(cls) == 3) {
-            const int npr = wt_npr(WT_SP / W, H);
-            const int cpi = wt_tci(cls) / 8;
-            const int nx = cls == 0 ? WtCfg<0>::NX : WtCfg<2>::NX;   // class 0: W = 128 (config 4 scale 1) falls back
-            if ((long long)npr * (W + 2) * cpi > (long long)nx * WT_NT) return RNVP_E_UNSUPPORTED;
-        }
-        if (lb > shm) shm = lb;
+        const int cls = wt_class(v, H, W);
+        if (wt_lds_bytes(cls, H, W) > 160 * 1024 || !wt_stage_fits(cls, H, W)) return RNVP_E_UNSUPPORTED;
         // slabs of whole stages; the slab count must stay v.nz (the replica
         // workspace and the weight-norm backward are sized by it)
         const long long stages = (M + WT_SP - 1) / WT_SP;
         v.m_per_slab = ((stages + v.nz - 1) / v.nz) * WT_SP;
         if ((M + v.m_per_slab - 1) / v.m_per_slab != v.nz) return RNVP_E_UNSUPPORTED;
+        v.cls = cls;
         v.tk = (v.cs_in + wt_tci(cls) - 1) / wt_tci(cls);
-        v.task0 = (int)tasks;
-        tasks += (long long)v.nz * ((v.n + wt_tco(cls) - 1) / wt_tco(cls)) * v.tk;
+        if (wt_tasks(v, cls) <= 0 || wt_tasks(v, cls) > (1ll << 28)) return RNVP_E_INVALID;
     }
-    if (tasks <= 0 || tasks > (1ll << 30)) return RNVP_E_INVALID;
-    k_wgrad_tap<<<(unsigned)tasks, WT_NT, shm, s>>>(*g);
-    RNVP_LAUNCH_CHECK();
+    // one launch per class present, its convs' tasks concatenated
+    for (int cls = 0; cls < 4; ++cls) {
+        rnvp_wgrad_group sub = *g;
+        sub.n_conv = 0;
+        long long tasks = 0;
+        for (int c = 0; c < g->n_conv; ++c) {
+            if (g->conv[c].cls != cls) continue;
+            rnvp_wgrad_conv v = g->conv[c];
+            v.task0 = (int)tasks;
+            tasks += wt_tasks(v, cls);
+            sub.conv[sub.n_conv++] = v;
+        }
+        if (sub.n_conv == 0) continue;
+        if (tasks > (1ll << 30)) return RNVP_E_INVALID;
+        hipLaunchKernelGGL(wt_kernel(cls), dim3((unsigned)tasks), dim3(WT_NT), wt_lds_bytes(cls, H, W), s, sub);
+        RNVP_LAUNCH_CHECK();
+    }
     return RNVP_OK;
 }

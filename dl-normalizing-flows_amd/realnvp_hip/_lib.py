@@ -72,7 +72,7 @@ class WgradConv(C.Structure):
     _fields_ = [("x", vp), ("dy", vp), ("ws", vp), ("wsb", vp), ("pro", BNSrc),
                 ("cs_in", i32), ("cin", i32), ("ks", i32), ("cs_dy", i32), ("n", i32), ("kp", i32),
                 ("pro_bn_relu", i32), ("nz", i32), ("nrep", i32), ("m_per_slab", i64), ("task0", i32),
-                ("tk", i32)]
+                ("tk", i32), ("cls", i32)]
 
 
 class WgradGroup(C.Structure):

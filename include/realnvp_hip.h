@@ -164,7 +164,7 @@ typedef struct rnvp_wgrad_conv {
     rnvp_bn_src pro;
     int cs_in, cin, ks, cs_dy, n, kp, pro_bn_relu, nz, nrep;
     long long m_per_slab;               /* filled by the library */
-    int task0, tk;                      /* filled by the library */
+    int task0, tk, cls;                 /* filled by the library */
 } rnvp_wgrad_conv;
 typedef struct rnvp_wgrad_group {
     int dtype, B, H, W, n_conv;
