@@ -182,10 +182,9 @@ extern "C" int rnvp_net_group_prepare(rnvp_net_step* steps, int n, int* klass, i
         if (a.epi_relu_bn_bwd && !a.epi_x) return RNVP_E_INVALID;
         if (a.pro_bn_relu && a.pro.sums && a.pro.shards > 2) return RNVP_E_UNSUPPORTED;
         if (a.epi_relu_bn_bwd && a.epi.sums && a.epi.shards > 2) return RNVP_E_UNSUPPORTED;
-        // one configuration for the whole group: every member's single-launch
-        // choice (rnvp_deep_auto_cfg, incl. its RNVP_DEEP_MAXM1 limit) must
-        // agree, else the group is refused and the convs launch one by one
-        const int c = rnvp_deep_auto_cfg(&a);
+        // one configuration for the whole group: the single-launch choice of
+        // its first conv (rnvp_deep_auto_cfg, incl. its RNVP_DEEP_MAXM1 limit)
+        const int c = rnvp_deep_auto_cfg(&steps[0].conv);
         if (c < 0) return RNVP_E_UNSUPPORTED;
         const GroupCfg g = group_cfg_shape(c);
         if (a.cs_in % (g.wk * kc) || a.cs_in > DEEP_MAX_CS || a.n < g.bn / 2) return RNVP_E_UNSUPPORTED;

@@ -228,10 +228,11 @@ __global__ __launch_bounds__(256) void k_out1(rnvp_coupling_args a, int TP, int 
     const Geo g = geo(a);
     const Tile t = tile_of(g, TP);
     const int lane = threadIdx.x & 63;
-    double* red = dsm;                          // [2*Cb] (+ pad to 16 B)
+    double* red = dsm;                          // [4*Cb] (+ pad to 16 B): out_bn sums | next_sums
     __shared__ float redl[16];
-    T* st = (T*)(dsm + 2 * ((g.Cb + 1) / 2 * 2));   // [tp][cs_st]
-    lds_zero(red, 2 * g.Cb);
+    T* st = (T*)(dsm + 4 * ((g.Cb + 1) / 2 * 2));   // [tp][cs_st]
+    const bool nxt = a.next_sums != nullptr && g.kind == 0;
+    lds_zero(red, 4 * g.Cb);
     tile_copy_in<T>(a.st, t.m0, t.tp, a.cs_st, st);
     __syncthreads();
     const float sc = a.scale[0], ss = a.scale_shift[0];
@@ -259,6 +260,13 @@ __global__ __launch_bounds__(256) void k_out1(rnvp_coupling_args a, int TP, int 
             atomicAdd(&red[cb], s1);
             atomicAdd(&red[g.Cb + cb], s2);
         }
+        if (nxt) {   // uniform: the transformed positions' share, for the next coupling's in_bn
+            const double t1 = seg_sum(tr ? (double)u : 0.0, seg), t2 = seg_sum(tr ? (double)u * u : 0.0, seg);
+            if (ok && (lane & (seg - 1)) == 0) {
+                atomicAdd(&red[2 * g.Cb + cb], t1);
+                atomicAdd(&red[3 * g.Cb + cb], t2);
+            }
+        }
     }
     const float dl = block_sum(sl, redl);   // (barriers also publish red)
     if (threadIdx.x == 0 && dl != 0.f) atomicAdd(&a.ldj_sample[t.b], dl);
@@ -266,6 +274,163 @@ __global__ __launch_bounds__(256) void k_out1(rnvp_coupling_args a, int TP, int 
         double* dst = cshard(a.out_sums, 2 * g.Cb);
         for (int c = threadIdx.x; c < 2 * g.Cb; c += blockDim.x) atomicAdd(&dst[c], red[c]);
     }
+    if (nxt) {
+        double* dst = cshard(a.next_sums, 2 * g.Cb);
+        for (int c = threadIdx.x; c < 2 * g.Cb; c += blockDim.x) atomicAdd(&dst[c], red[2 * g.Cb + c]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// chained couplings, forward: z of coupling a AND the in part of coupling nx
+// (nx->x == a->z, same kind and shape, opposite mask) in one pass
+// ---------------------------------------------------------------------------
+// a's out_bn batch statistics of channel cb (fp64) and the closed-form in_bn
+// sums of nx over the positions nx's in_bn reads (= a's transformed ones,
+// where z = (u - mean_f) * rstd_f with the fp32 mean / rstd k_out2 applies)
+__device__ __forceinline__ void chain_in_sums(const rnvp_coupling_args& a, const Geo& g, int cb, float& mean_f,
+                                              float& rstd_f, float& hlv, double& D1, double& D2) {
+    const double cnt = (double)g.B * g.HW;
+    const double o1 = csum(a.out_sums, 2 * g.Cb, cb), o2 = csum(a.out_sums, 2 * g.Cb, g.Cb + cb);
+    const double mean = o1 / cnt;
+    double var = o2 / cnt - mean * mean;
+    if (var < 0) var = 0;
+    mean_f = (float)mean;
+    rstd_f = (float)(1.0 / sqrt(var + (double)a.eps));
+    hlv = (float)(0.5 * log(var + (double)a.eps));
+    double S1, S2, n;
+    if (g.kind == 0) {   // the transformed squares only
+        S1 = csum(a.next_sums, 2 * g.Cb, cb);
+        S2 = csum(a.next_sums, 2 * g.Cb, g.Cb + cb);
+        n = (double)g.B * n_transformed(g);
+    } else {             // the whole transformed half
+        S1 = o1;
+        S2 = o2;
+        n = cnt;
+    }
+    const double m = (double)mean_f, r = (double)rstd_f;
+    D1 = r * (S1 - n * m);
+    D2 = r * r * (S2 - 2.0 * m * S1 + n * m * m);
+    if (D2 < 0) D2 = 0;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_out2_in(rnvp_coupling_args a, rnvp_coupling_args nx, int TP, int main_grid) {
+    extern __shared__ double dsm[];
+    if ((int)blockIdx.x >= main_grid) {
+        // extra workgroups: one s/t-net BatchNorm running-stat update each (as k_out2)
+        const rnvp_bn_running r = a.net_running[blockIdx.x - main_grid];
+        double* tmp = dsm;   // [2*C]
+        block_shard_sums(r.sums, r.C, r.shards, 0, r.C, tmp, tmp + r.C);
+        const float mom = a.momentum;
+        for (int c = threadIdx.x; c < r.C; c += blockDim.x) {
+            double mean = tmp[c] / r.count;
+            double var = tmp[r.C + c] / r.count - mean * mean;
+            if (var < 0) var = 0;
+            double unb = r.count > 1 ? var * r.count / (r.count - 1) : var;
+            r.rmean[c] = (1.f - mom) * r.rmean[c] + mom * (float)mean;
+            r.rvar[c] = (1.f - mom) * r.rvar[c] + mom * (float)unb;
+        }
+        if (threadIdx.x == 0 && r.nbt) r.nbt[0] += 1;
+        return;
+    }
+    const Geo g = geo(a), gn = geo(nx);
+    const Tile t = tile_of(g, TP);
+    const int Cb = g.Cb, Cr = (Cb + 3) / 4 * 4;
+    float* ot = (float*)dsm;                     // a's out_bn: mean | rstd | half log var [Cr each]
+    float* it = ot + 3 * Cr;                     // nx's in_bn: scale | shift [Cr each]
+    T* h = (T*)(it + 2 * Cr);                    // nx's h0 tile [tp][cs_h0] (16-B aligned: 20*Cr B)
+    const int cs = nx.cs_h0;
+    const double cnt = (double)g.B * g.HW;
+    for (int cb = threadIdx.x; cb < Cb; cb += blockDim.x) {
+        float mf, rf, hl;
+        double D1, D2;
+        chain_in_sums(a, g, cb, mf, rf, hl, D1, D2);
+        ot[cb] = mf;
+        ot[Cr + cb] = rf;
+        ot[2 * Cr + cb] = hl;
+        // nx's in_bn from the closed-form sums, as bn_affine forms it
+        const double mean = D1 / cnt;
+        double var = D2 / cnt - mean * mean;
+        if (var < 0) var = 0;
+        const float rstd = (float)(1.0 / sqrt(var + (double)nx.eps));
+        const float gam = nx.in_gamma ? nx.in_gamma[cb] : 1.f, bet = nx.in_beta ? nx.in_beta[cb] : 0.f;
+        it[cb] = gam * rstd;
+        it[Cr + cb] = bet - (float)mean * gam * rstd;
+        if (blockIdx.x == 0) {
+            // a's out_bn running stats (as k_out2); nx's in_bn sums (shard 0) and running stats (as k_in_apply)
+            const double o1 = csum(a.out_sums, 2 * Cb, cb), o2 = csum(a.out_sums, 2 * Cb, Cb + cb);
+            const double om = o1 / cnt;
+            double ov = o2 / cnt - om * om;
+            if (ov < 0) ov = 0;
+            const double unb = cnt > 1 ? ov * cnt / (cnt - 1) : ov;
+            if (a.out_rmean) {
+                a.out_rmean[cb] = (1.f - a.momentum) * a.out_rmean[cb] + a.momentum * (float)om;
+                a.out_rvar[cb] = (1.f - a.momentum) * a.out_rvar[cb] + a.momentum * (float)unb;
+            }
+            nx.in_sums[cb] = D1;
+            nx.in_sums[Cb + cb] = D2;
+            if (nx.in_rmean) {
+                const double iu = cnt > 1 ? var * cnt / (cnt - 1) : var;
+                nx.in_rmean[cb] = (1.f - nx.momentum) * nx.in_rmean[cb] + nx.momentum * (float)mean;
+                nx.in_rvar[cb] = (1.f - nx.momentum) * nx.in_rvar[cb] + nx.momentum * (float)iu;
+            }
+        }
+    }
+    // nx's padding / mask channels of the h0 tile
+    for (int e = threadIdx.x; e < t.tp * cs; e += blockDim.x) {
+        const int pl = e / cs, ch = e - pl * cs;
+        if (ch >= 2 * Cb) {
+            float out = 0.f;
+            if (gn.kind == 0 && ch == 2 * Cb) out = (float)ckbd_m(gn, t.p0 + pl);
+            stv(&h[pl * cs + ch], out);
+        }
+    }
+    __syncthreads();
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) {
+            if (a.out_nbt) a.out_nbt[0] += 1;
+            if (nx.in_nbt) nx.in_nbt[0] += 1;
+        }
+        // per-sample constant of a: -sum_c 0.5*log(var_c+eps) * (#transformed positions per channel)
+        float k = 0.f;
+        for (int cb = 0; cb < Cb; ++cb) k += ot[2 * Cr + cb];
+        k = -k * (float)n_transformed(g);
+        for (int b = threadIdx.x; b < g.B; b += blockDim.x) a.ldj_sample[b] += k;
+    }
+    const int total = g.C * t.tp;
+    for (int e = threadIdx.x; e < total; e += blockDim.x) {
+        const int c = e / t.tp, pl = e - c * t.tp, p = t.p0 + pl;
+        const long long idx = ((long long)t.b * g.C + c) * g.HW + p;
+        bool tr;
+        int cb;
+        if (g.kind == 0) {
+            tr = !ckbd_m(g, p);
+            cb = c;
+        } else {
+            tr = c >= g.on_base && c < g.on_base + Cb;
+            cb = c - g.on_base;
+        }
+        const float u = a.u[idx];
+        const float zv = tr ? (u - ot[cb]) * ot[Cr + cb] : u;
+        a.z[idx] = zv;
+        // nx's in part: masked input (checkerboard: every channel at nx's kept
+        // squares; channelwise: nx's conditioning half = a's transformed half)
+        int cn;
+        float xm;
+        if (gn.kind == 0) {
+            cn = c;
+            xm = ckbd_m(gn, p) ? zv : 0.f;
+        } else {
+            if (c < gn.off_base || c >= gn.off_base + Cb) continue;
+            cn = c - gn.off_base;
+            xm = zv;
+        }
+        const float xa = xm * it[cn] + it[Cr + cn];
+        stv(&h[pl * cs + cn], fmaxf(xa, 0.f));
+        stv(&h[pl * cs + Cb + cn], fmaxf(-xa, 0.f));
+    }
+    __syncthreads();
+    tile_copy_out<T>(h, t.m0, t.tp, cs, nx.h0);
 }
 
 // z = out_bn(u) on transformed positions; ldj var term; running stats.
@@ -588,14 +753,22 @@ __global__ __launch_bounds__(256) void k_in_bwd_red(rnvp_coupling_args a, int TP
     for (int c = threadIdx.x; c < 2 * g.Cb; c += blockDim.x) atomicAdd(&dst[c], red[c]);
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void k_in_bwd_apply(rnvp_coupling_args a, int TP, int seg) {
+template <typename T, bool CHAIN>
+__global__ __launch_bounds__(256) void k_in_bwd_apply(rnvp_coupling_args a, rnvp_coupling_args pv, int TP, int seg) {
     extern __shared__ double dsm[];
     const Geo g = geo(a);
     const Tile t = tile_of(g, TP);
-    float* tab = (float*)dsm;                            // sc | sf | mean | rstd | coef | k1 | k2 [Cb each]
-    const int tabn = 8 * ((g.Cb + 3) / 4 * 4);
-    T* gh = (T*)(tab + tabn);
+    const int lane = threadIdx.x & 63;
+    float* tab = (float*)dsm;                            // sc | sf | mean | rstd | coef | k1 | k2 | pm | pr [Cb each]
+    const int tabn = 12 * ((g.Cb + 3) / 4 * 4);
+    double* pred = (double*)(tab + tabn);                // CHAIN: prev's A | B | G [Cb each]
+    T* gh = (T*)(pred + (CHAIN ? 3 * ((g.Cb + 1) / 2 * 2) : 0));
+    if (CHAIN) {
+        lds_zero(pred, 3 * g.Cb);
+        const Geo gp = geo(pv);
+        for (int cb = threadIdx.x; cb < g.Cb; cb += blockDim.x)
+            out_bn_stats(pv, gp, cb, tab[7 * g.Cb + cb], tab[8 * g.Cb + cb]);
+    }
     in_bn_table(a, g, tab);
     const double cnt = (double)g.B * g.HW;
     for (int cb = threadIdx.x; cb < g.Cb; cb += blockDim.x) {
@@ -630,14 +803,45 @@ __global__ __launch_bounds__(256) void k_in_bwd_apply(rnvp_coupling_args a, int 
     tile_copy_in<T>(a.gh0, t.m0, t.tp, a.cs_gh0, gh);
     __syncthreads();
     const int total = g.Cb * t.tp;
-    for (int e = threadIdx.x; e < total; e += blockDim.x) {
-        const int cb = e / t.tp, pl = e - cb * t.tp, p = t.p0 + pl;
-        float gxa, xh;
-        in_bwd_vals<T>(a, g, t, gh, tab, cb, pl, gxa, xh);
-        float gxm = tab[4 * g.Cb + cb] * (gxa - tab[5 * g.Cb + cb] - xh * tab[6 * g.Cb + cb]);
-        if (g.kind == 0 && !ckbd_m(g, p)) gxm = 0.f;   // xm = x * mask
+    for (int e0 = 0; e0 < total; e0 += blockDim.x) {
+        const int e = e0 + threadIdx.x;
+        const bool ok = e < total;
+        const int cb = ok ? e / t.tp : 0, pl = ok ? e - cb * t.tp : 0, p = t.p0 + pl;
         const int c = (g.kind == 0) ? cb : g.off_base + cb;
-        a.gx[((long long)t.b * g.C + c) * g.HW + p] += gxm;
+        const long long idx = ((long long)t.b * g.C + c) * g.HW + p;
+        float gfin = 0.f;
+        bool ptr = false;   // a transformed position of prev (= kept square / conditioning half of a)
+        if (ok) {
+            float gxa, xh;
+            in_bwd_vals<T>(a, g, t, gh, tab, cb, pl, gxa, xh);
+            float gxm = tab[4 * g.Cb + cb] * (gxa - tab[5 * g.Cb + cb] - xh * tab[6 * g.Cb + cb]);
+            const bool kept = g.kind != 0 || ckbd_m(g, p);
+            if (!kept) gxm = 0.f;   // xm = x * mask
+            gfin = a.gx[idx] + gxm;
+            a.gx[idx] = gfin;
+            ptr = kept;
+        }
+        if (CHAIN) {
+            // prev's k_out_bwd_red over its transformed positions, from the
+            // final gradient of z_prev = x_a (every lane takes part in seg_sum)
+            float vA = 0.f, vB = 0.f, vG = 0.f;
+            if (ptr) {
+                vA = gfin;
+                vB = gfin * (pv.u[idx] - tab[7 * g.Cb + cb]) * tab[8 * g.Cb + cb];
+                vG = pv.gl_sample ? pv.gl_sample[t.b] : 0.f;
+            }
+            const double dA = seg_sum((double)vA, seg), dB = seg_sum((double)vB, seg), dG = seg_sum((double)vG, seg);
+            if (ok && (lane & (seg - 1)) == 0) {
+                atomicAdd(&pred[cb], dA);
+                atomicAdd(&pred[g.Cb + cb], dB);
+                atomicAdd(&pred[2 * g.Cb + cb], dG);
+            }
+        }
+    }
+    if (CHAIN) {
+        __syncthreads();
+        double* dst = cshard(pv.bwd_sums, 3 * g.Cb);
+        for (int c = threadIdx.x; c < 3 * g.Cb; c += blockDim.x) atomicAdd(&dst[c], pred[c]);
     }
 }
 
@@ -712,7 +916,7 @@ extern "C" int rnvp_coupling_out_fwd(const rnvp_coupling_args* a, void* stream) 
     hipStream_t s = (hipStream_t)stream;
     const TileCfg tc = tile_cfg(a);
     const int esz = a->dtype == RNVP_F32 ? 4 : 2;
-    const size_t shm1 = 16 * ((Cb + 1) / 2 * 2) + (size_t)tc.TP * a->cs_st * esz;
+    const size_t shm1 = 32 * ((Cb + 1) / 2 * 2) + (size_t)tc.TP * a->cs_st * esz;
     if (a->dtype == RNVP_F32) k_out1<float><<<tc.grid, 256, shm1, s>>>(*a, tc.TP, tc.seg);
     else k_out1<bf16_t><<<tc.grid, 256, shm1, s>>>(*a, tc.TP, tc.seg);
     RNVP_LAUNCH_CHECK();
@@ -756,7 +960,7 @@ extern "C" int rnvp_coupling_out_bwd(const rnvp_coupling_args* a, void* stream) 
     hipStream_t s = (hipStream_t)stream;
     const TileCfg tc = tile_cfg(a);
     const int esz = a->dtype == RNVP_F32 ? 4 : 2;
-    if (stats) {
+    if (stats && !a->bwd_sums_ready) {
         k_out_bwd_red<<<tc.grid, 256, 24 * Cb + 8 * Cb, s>>>(*a, tc.TP, tc.seg);
         RNVP_LAUNCH_CHECK();
     }
@@ -787,9 +991,70 @@ extern "C" int rnvp_coupling_in_bwd(const rnvp_coupling_args* a, void* stream) {
         else k_in_bwd_red<bf16_t><<<tc.grid, 256, shm, s>>>(*a, tc.TP, tc.seg);
         RNVP_LAUNCH_CHECK();
     }
-    const size_t shm = 32 * r4(Cb) + gsh;
-    if (a->dtype == RNVP_F32) k_in_bwd_apply<float><<<tc.grid, 256, shm, s>>>(*a, tc.TP, tc.seg);
-    else k_in_bwd_apply<bf16_t><<<tc.grid, 256, shm, s>>>(*a, tc.TP, tc.seg);
+    const size_t shm = 48 * r4(Cb) + gsh;
+    if (a->dtype == RNVP_F32) k_in_bwd_apply<float, false><<<tc.grid, 256, shm, s>>>(*a, *a, tc.TP, tc.seg);
+    else k_in_bwd_apply<bf16_t, false><<<tc.grid, 256, shm, s>>>(*a, *a, tc.TP, tc.seg);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+namespace {
+// a and b chain: b consumes a's output (same kind / shape, the opposite mask)
+int chain_check(const rnvp_coupling_args* a, const rnvp_coupling_args* b) {
+    if (check(a) || check(b)) return RNVP_E_INVALID;
+    if (a->kind != b->kind || a->B != b->B || a->C != b->C || a->H != b->H || a->W != b->W || a->dtype != b->dtype)
+        return RNVP_E_INVALID;
+    if ((a->mask_config ? 1 : 0) == (b->mask_config ? 1 : 0)) return RNVP_E_INVALID;
+    if (!a->training || !b->training || !a->coupling_bn) return RNVP_E_INVALID;
+    return RNVP_OK;
+}
+}  // namespace
+
+extern "C" int rnvp_coupling_out_in_fwd(const rnvp_coupling_args* a, const rnvp_coupling_args* nx, void* stream) {
+    if (!a || !nx || chain_check(a, nx)) return RNVP_E_INVALID;
+    if (!a->st || !a->u || !a->z || !a->ldj_sample || !a->scale || !a->scale_shift || !a->out_sums || a->ldj_full)
+        return RNVP_E_INVALID;
+    if (a->kind == 0 && !a->next_sums) return RNVP_E_INVALID;
+    if (!nx->h0 || !nx->in_sums || nx->x != a->z) return RNVP_E_INVALID;
+    const int Cb = cb_of(a);
+    if (a->cs_st < 2 * Cb || nx->cs_h0 < (nx->kind == 0 ? 2 * Cb + 1 : 2 * Cb)) return RNVP_E_INVALID;
+    if (a->B == 0) return RNVP_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const TileCfg tc = tile_cfg(a);
+    const int esz = a->dtype == RNVP_F32 ? 4 : 2;
+    const size_t shm1 = 32 * ((Cb + 1) / 2 * 2) + (size_t)tc.TP * a->cs_st * esz;
+    if (a->dtype == RNVP_F32) k_out1<float><<<tc.grid, 256, shm1, s>>>(*a, tc.TP, tc.seg);
+    else k_out1<bf16_t><<<tc.grid, 256, shm1, s>>>(*a, tc.TP, tc.seg);
+    RNVP_LAUNCH_CHECK();
+    const TileCfg tn = tile_cfg(nx);
+    const int nrun = a->net_running ? a->n_net_running : 0;
+    if (nrun < 0 || (nrun > 0 && a->net_running_cmax <= 0)) return RNVP_E_INVALID;
+    size_t shm = 20 * (size_t)r4(Cb) + (size_t)tn.TP * nx->cs_h0 * esz;
+    if (nrun > 0 && 16 * (size_t)a->net_running_cmax > shm) shm = 16 * (size_t)a->net_running_cmax;
+    if (a->dtype == RNVP_F32) k_out2_in<float><<<tn.grid + nrun, 256, shm, s>>>(*a, *nx, tn.TP, tn.grid);
+    else k_out2_in<bf16_t><<<tn.grid + nrun, 256, shm, s>>>(*a, *nx, tn.TP, tn.grid);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+extern "C" int rnvp_coupling_in_bwd_chain(const rnvp_coupling_args* a, const rnvp_coupling_args* pv, void* stream) {
+    if (!a || !pv || chain_check(pv, a)) return RNVP_E_INVALID;
+    if (!a->gh0 || !a->gx || !a->in_sums || !a->in_bwd_sums) return RNVP_E_INVALID;
+    if (!pv->u || !pv->out_sums || !pv->bwd_sums || pv->gl_full) return RNVP_E_INVALID;
+    const int Cb = cb_of(a);
+    if (a->cs_gh0 < 2 * Cb) return RNVP_E_INVALID;
+    if (a->B == 0) return RNVP_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const TileCfg tc = tile_cfg(a);
+    const int esz = a->dtype == RNVP_F32 ? 4 : 2;
+    const size_t gsh = (size_t)tc.TP * a->cs_gh0 * esz;
+    const size_t shm0 = 16 * Cb + 16 * r4(Cb) + gsh;
+    if (a->dtype == RNVP_F32) k_in_bwd_red<float><<<tc.grid, 256, shm0, s>>>(*a, tc.TP, tc.seg);
+    else k_in_bwd_red<bf16_t><<<tc.grid, 256, shm0, s>>>(*a, tc.TP, tc.seg);
+    RNVP_LAUNCH_CHECK();
+    const size_t shm = 48 * r4(Cb) + 24 * ((Cb + 1) / 2 * 2) + gsh;
+    if (a->dtype == RNVP_F32) k_in_bwd_apply<float, true><<<tc.grid, 256, shm, s>>>(*a, *pv, tc.TP, tc.seg);
+    else k_in_bwd_apply<bf16_t, true><<<tc.grid, 256, shm, s>>>(*a, *pv, tc.TP, tc.seg);
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
 }

@@ -99,7 +99,7 @@ class CouplingArgs(C.Structure):
                 ("gh0", vp), ("cs_gh0", i32),
                 ("in_bwd_sums", vp), ("g_in_gamma", vp), ("g_in_beta", vp),
                 ("net_running", vp), ("n_net_running", i32), ("net_running_cmax", i32),
-                ("gscale_part", vp)]
+                ("gscale_part", vp), ("next_sums", vp), ("bwd_sums_ready", i32)]
 
 
 class TensorRef(C.Structure):
@@ -137,6 +137,8 @@ _SIGS = {
     "rnvp_coupling_reverse": (i32, [C.POINTER(CouplingArgs), vp]),
     "rnvp_coupling_out_bwd": (i32, [C.POINTER(CouplingArgs), vp]),
     "rnvp_coupling_in_bwd": (i32, [C.POINTER(CouplingArgs), vp]),
+    "rnvp_coupling_out_in_fwd": (i32, [C.POINTER(CouplingArgs), C.POINTER(CouplingArgs), vp]),
+    "rnvp_coupling_in_bwd_chain": (i32, [C.POINTER(CouplingArgs), C.POINTER(CouplingArgs), vp]),
     "rnvp_sumsq_multi": (i32, [vp, i32, vp, vp]),
     "rnvp_sumsq_bwd_multi": (i32, [vp, i32, vp, f32, vp]),
     "rnvp_adam_step": (i32, [vp, vp, vp, vp, i64, vp, f32, f32, f32, f32, f32, vp, f32, vp]),

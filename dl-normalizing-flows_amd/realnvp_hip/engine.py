@@ -305,6 +305,7 @@ class CouplingEngine:
         ar.add("u", B * self.C * H * W * 4)
         ar.add("in_sums", COUPLING_SHARDS * 2 * self.Cb * 8)
         ar.add("out_sums", COUPLING_SHARDS * 2 * self.Cb * 8)
+        ar.add("next_sums", COUPLING_SHARDS * 2 * self.Cb * 8)   # chained couplings (rnvp_coupling_out_in_fwd)
         sh = stat_shards(M)
         for bn, spec in self.P.bns.items():
             ar.add("s:" + bn, sh * 2 * spec.c * 8)
@@ -501,13 +502,24 @@ class CouplingEngine:
         return out
 
     # ---------------------------------------------------------------- forward
+    def chains_into(self, nxt):
+        """True when coupling `nxt` can consume this coupling's output through
+        the chained kernels (rnvp_coupling_out_in_fwd / _in_bwd_chain): same
+        kind, the opposite mask, out_bn with batch statistics."""
+        return (nxt.kind == self.kind and nxt.C == self.C and nxt.cfg != self.cfg and
+                bool(self.hp.coupling_bn))
+
     def forward(self, x, training, dtype, full_ldj, saved=None, prepare=True, ldj_sample=None, z_out=None,
-                zero_sums=True):
+                zero_sums=True, chain_next=None, in_done=False):
         """x: [B,C,H,W] fp32 device tensor.  Returns (z, ldj, saved) where ldj
         is the elementwise log_diag_J [B,C,H,W] (full_ldj) or this coupling's
         per-sample sum [B] (accumulated into ldj_sample when given).
         zero_sums=False: the batch-statistic sums of `saved` are already zero
-        (the previous step's backward left them so: backward(zero_at_end=True))."""
+        (the previous step's backward left them so: backward(zero_at_end=True)).
+        chain_next = (engine, saved arena) of the coupling that consumes z
+        (chains_into): its in part (h0, in_bn sums and running stats) is
+        produced by this coupling's out launch; that coupling's forward then
+        runs with in_done=True."""
         L = _lib.lib()
         B, Cc, H, W = x.shape
         assert Cc == self.C, "channel mismatch"
@@ -527,7 +539,8 @@ class CouplingEngine:
         a = self._coupling_args(T, x, B, H, W, dtype, training)
         a.in_sums = ar.ptr("in_sums")
         a.h0 = ar.ptr("h0")
-        L.coupling_in_fwd(C.byref(a), s)
+        if not in_done:
+            L.coupling_in_fwd(C.byref(a), s)
         self._net_forward(T, sv, ws, training, s)
         if training and "bn_table" in sv:
             # the net BNs' running-stat updates ride on the out launch
@@ -538,7 +551,15 @@ class CouplingEngine:
         a.out_sums = ar.ptr("out_sums")
         a.ldj_sample = ldj_sample.data_ptr()
         a.ldj_full = ldj_full.data_ptr() if full_ldj else None
-        L.coupling_out_fwd(C.byref(a), s)
+        if chain_next is not None:
+            neng, nsv = chain_next
+            nx = neng._coupling_args(neng._tensors(), z, B, H, W, dtype, training)
+            nx.in_sums = nsv["arena"].ptr("in_sums")
+            nx.h0 = nsv["arena"].ptr("h0")
+            a.next_sums = ar.ptr("next_sums")
+            L.coupling_out_in_fwd(C.byref(a), C.byref(nx), s)
+        else:
+            L.coupling_out_fwd(C.byref(a), s)
         sv["x"] = x
         return z, (ldj_full if full_ldj else ldj_sample), sv
 
@@ -645,9 +666,14 @@ class CouplingEngine:
         return items, groups, wg_bytes, wg_flops
 
     def backward(self, sv, gz, gl_full, gl_sample, grad_block, gx=None, side=None, after=None, zero_at_end=False,
-                 defer=None):
+                 defer=None, chain_prev=None, sums_ready=False):
         """Returns dL/dx; parameter gradients are written into grad_block
         (flat fp32, zeroed by the caller; scale/shift grads accumulate).
+
+        chain_prev = (engine, saved arena) of the coupling whose output this
+        one consumed (its chains_into): this coupling's in backward also
+        reduces that coupling's out_bn backward sums (rnvp_coupling_in_bwd_chain),
+        and that coupling's backward then runs with sums_ready=True.
 
         The data-gradient chain (dgrad -> BN apply per conv) runs first; the
         weight gradients of all the net's convs only need their (complete,
@@ -699,6 +725,7 @@ class CouplingEngine:
         a.bwd_sums = sar.ptr("bwd_sums")
         a.g_scale, a.g_scale_shift = gp("scale"), gp("scale_shift")
         a.gscale_part = sar.ptr("gscale_part")
+        a.bwd_sums_ready = int(bool(sums_ready))
         L.coupling_out_bwd(C.byref(a), s)
 
         # the net's data-gradient chain and grouped weight gradients: argument
@@ -752,7 +779,15 @@ class CouplingEngine:
         a.gh0, a.cs_gh0 = sar.ptr("g:h0"), chan_stride(self.P.buf_ch["h0"])
         a.in_bwd_sums = sar.ptr("in_bwd_sums")
         a.g_in_gamma, a.g_in_beta = gp("in_bn.weight"), gp("in_bn.bias")
-        L.coupling_in_bwd(C.byref(a), s)
+        if chain_prev is not None:
+            peng, psv = chain_prev
+            pv = peng._coupling_args(peng._tensors(), psv["x"], B, H, W, dtype, training)
+            pv.u, pv.out_sums = psv["arena"].ptr("u"), psv["arena"].ptr("out_sums")
+            pv.bwd_sums = peng.scratch(B, H, W, dtype, x.device)["arena"].ptr("bwd_sums")
+            pv.gl_sample = gl_sample.data_ptr() if gl_sample is not None else None
+            L.coupling_in_bwd_chain(C.byref(a), C.byref(pv), s)
+        else:
+            L.coupling_in_bwd(C.byref(a), s)
 
         # ... while the weight gradients (grouped wgrad + weight-norm backward)
         # only feed the optimizer: on a side stream they overlap the backward

@@ -30,6 +30,10 @@ import torch
 from . import _lib
 from .engine import stream_ptr
 
+# chained consecutive couplings (rnvp_coupling_out_in_fwd / _in_bwd_chain):
+# RNVP_CHAIN_COUPLING=0 launches every coupling's in and out parts on their own
+CHAIN_COUPLING = int(os.environ.get("RNVP_CHAIN_COUPLING", "1"))
+
 
 def wn_table(engines, dtype, dev):
     """One weight-norm descriptor table over the convs of several couplings
@@ -213,6 +217,16 @@ class FlowTrainer:
             self.stages.append(("restore", cur, off, full))
             cur = full
         self.z = cur
+        # chained couplings: chain[i] = the coupling stage that consumes stage
+        # i's output directly (engine.chains_into), else None
+        self.chain = {}
+        for i, st in enumerate(self.stages):
+            if st[0] != "coupling":
+                continue
+            nx = self.stages[i + 1] if i + 1 < len(self.stages) else None
+            ok = (CHAIN_COUPLING and nx is not None and nx[0] == "coupling" and nx[3] is st[4] and
+                  st[2].chains_into(nx[2]))
+            self.chain[i] = nx if ok else None
         # backward buffers: a gradient buffer per forward tensor
         self.gbuf = {}
         self._build_wn_table()
@@ -350,14 +364,16 @@ class FlowTrainer:
             for t in self.wn_tables:
                 self._wn_fwd(t)
         ci = 0
-        for st in self.stages:
+        for i, st in enumerate(self.stages):
             if st[0] == "coupling":
                 if ci == self.wn_split and late_ready is not None:
                     torch.cuda.current_stream().wait_event(late_ready)
                 ci += 1
                 _, mod, eng, x, z, sv, _ = st
+                nxt = self.chain[i]
                 eng.forward(x, True, self.dtype, False, saved=sv, prepare=False, ldj_sample=self.ldj, z_out=z,
-                            zero_sums=False)
+                            zero_sums=False, in_done=self.chain.get(i - 1) is not None,
+                            chain_next=None if nxt is None else (nxt[2], nxt[5]))
             elif st[0] == "squeeze":
                 _, a, b = st
                 L.squeeze(a.data_ptr(), b.data_ptr(), *a.shape, s)
@@ -382,7 +398,8 @@ class FlowTrainer:
         n_coupling = sum(1 for st in self.stages if st[0] == "coupling")
         ci = n_coupling
         pending = []
-        for st in reversed(self.stages):
+        for i in reversed(range(len(self.stages))):
+            st = self.stages[i]
             if st[0] == "coupling":
                 ci -= 1
                 _, mod, eng, x, z, sv, block = st
@@ -390,8 +407,11 @@ class FlowTrainer:
                 if self.adam_ranges is not None:
                     lo, hi = self.adam_ranges[ci]
                     after = (lambda lo=lo, hi=hi: self._adam_range(lo, hi))
+                prv = self.stages[i - 1] if self.chain.get(i - 1) is not None else None
                 eng.backward(sv, self._g(z), None, self.g_lp, block, gx=self._g(x), side=self.side, after=after,
-                             zero_at_end=True, defer=pending if self.side_group else None)
+                             zero_at_end=True, defer=pending if self.side_group else None,
+                             chain_prev=None if prv is None else (prv[2], prv[5]),
+                             sums_ready=self.chain[i] is not None)
                 if self.side_group and (len(pending) >= self.side_group or ci == 0):
                     self._flush_side(pending)
                 if self.comm_stream is not None:

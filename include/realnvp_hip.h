@@ -270,12 +270,42 @@ typedef struct rnvp_coupling_args {
      * workgroup on one address); rnvp_coupling_in_bwd folds them into
      * g_scale / g_scale_shift (+=) and leaves them zero */
     double* gscale_part;
+    /* optional, chained couplings (see rnvp_coupling_out_in_fwd /
+     * rnvp_coupling_in_bwd_chain): [RNVP_COUPLING_SHARDS][2*Cb] fp64 sums of
+     * u and u^2 over the transformed positions (checkerboard; zeroed on entry),
+     * and bwd_sums_ready = 1 when bwd_sums were already reduced by the next
+     * coupling's chained in backward (rnvp_coupling_out_bwd then skips its
+     * reduction pass) */
+    double* next_sums;
+    int bwd_sums_ready;
 } rnvp_coupling_args;
 int rnvp_coupling_in_fwd(const rnvp_coupling_args* a, void* stream);   /* in_sums must be zeroed */
 int rnvp_coupling_out_fwd(const rnvp_coupling_args* a, void* stream);  /* out_sums must be zeroed */
 int rnvp_coupling_reverse(const rnvp_coupling_args* a, void* stream);  /* z = inverse(x) */
 int rnvp_coupling_out_bwd(const rnvp_coupling_args* a, void* stream);  /* bwd_sums zeroed; writes gx, gst */
 int rnvp_coupling_in_bwd(const rnvp_coupling_args* a, void* stream);   /* in_bwd_sums zeroed; gx += */
+
+/* Chained couplings: coupling `next` directly consumes coupling a's output
+ * (next->x == a->z; same kind and shape, the opposite mask -- the order
+ * RealNVP.checkerboard_combo / channelwise_combo build, flow_realnvp.py:98-116).
+ * Then next's input BatchNorm statistics are a closed form of a's out_bn
+ * statistics: next's in_bn reads exactly the positions a transformed (its
+ * kept checkerboard squares / its conditioning half = a's transformed half),
+ * where z = (u - mean) * rstd, so sum z = rstd (S1 - n mean) and sum z^2 =
+ * rstd^2 (S2 - 2 mean S1 + n mean^2) over those n positions (S1, S2: the sums
+ * of u there; a's out_bn sums for channelwise, a->next_sums for checkerboard).
+ *   rnvp_coupling_out_in_fwd = rnvp_coupling_out_fwd(a) + rnvp_coupling_in_fwd(next)
+ *     in two launches instead of four: a's out part, then one pass writing
+ *     z, a's log-det terms and running stats AND next's h0, next's in_bn
+ *     running stats and next->in_sums (shard 0 = the closed-form sums; the
+ *     other shards must be zero).  Requires training, coupling_bn, no ldj_full.
+ *   rnvp_coupling_in_bwd_chain = rnvp_coupling_in_bwd(a) that also reduces
+ *     the out_bn backward sums of the coupling `prev` whose output a consumed
+ *     (prev->bwd_sums, zeroed on entry) from the final gradient it leaves in
+ *     a->gx (= prev's gz); prev's rnvp_coupling_out_bwd then runs with
+ *     bwd_sums_ready = 1.  Requires gl_full == NULL (per-sample gl). */
+int rnvp_coupling_out_in_fwd(const rnvp_coupling_args* a, const rnvp_coupling_args* next, void* stream);
+int rnvp_coupling_in_bwd_chain(const rnvp_coupling_args* a, const rnvp_coupling_args* prev, void* stream);
 
 /* ---- regulariser and optimizer ------------------------------------------
  * weight_scale = sum over tensors of sum p^2  (flow_realnvp.py:362-369);

@@ -4,10 +4,10 @@ against the same convs launched one by one (RNVP_NET_GROUP=0).
 The engine groups each core_skips[i] forward with the next block's first 1x1
 and the data gradients of in_skip + every core_skips[i]
 (modules_realnvp.py:175-194).  A grouped tile runs the same deep_tile body as
-the single launch with the same configuration (rnvp_net_group_prepare takes
-every member's single-launch choice), so forward outputs, the data gradient
-and every parameter gradient must agree up to the order of the fp64
-BatchNorm-sum atomics: checked on bottleneck+skip couplings at M = 256, 1024,
+the single launch, in the configuration its first conv would get alone
+(rnvp_deep_auto_cfg, so the dispatch knobs reach groups too), so forward
+outputs, the data gradient and every parameter gradient must agree up to
+summation order: checked on bottleneck+skip couplings at M = 256, 1024,
 4096 and 16384 pixels (both sides of the 8-wave / 4-wave boundary at 1024 and
 the group's 16384-pixel limit), fp32 and bf16, and through the C ABI.
 """
@@ -83,10 +83,13 @@ def test_grouped_matches_single_launches(case, dtype):
     # beside block i+1's first 1x1), one backward group (in_skip + 4 skips)
     assert sum(p[0] == "group" for p in f1) >= 3, [p[:3] for p in f1]
     assert any(p[0] == "group" and p[2] - p[1] >= 5 for p in b1), [p[:3] for p in b1]
-    # same tiles, same per-tile arithmetic: only the fp64 batch-sum order
-    # differs (fp32: exact up to it; bf16: one rounding of bf16 outputs can flip)
-    fw = 1e-6 if dtype == "fp32" else 2e-3
-    bw = 1e-5 if dtype == "fp32" else 1e-2
+    # a group runs its first conv's tile configuration for every member, so
+    # a member can sum K in another order than its single launch: fp32
+    # rounding, amplified in the backward by ReLU-kink decisions (~1e-3 per
+    # flip, tests/test_gpu_deep.py); bf16: flipped bf16 roundings of stored
+    # activations
+    fw = 1e-5 if dtype == "fp32" else 5e-3
+    bw = 3e-3 if dtype == "fp32" else 5e-2
     assert rel(y1, y0) < fw and rel(l1, l0) < fw, (rel(y1, y0), rel(l1, l0))
     assert rel(gx1, gx0) < bw, rel(gx1, gx0)
     # biases of convs that feed only a BatchNorm have a zero gradient in exact

@@ -388,7 +388,11 @@ def test_checkpoint_carries_the_noise_stream():
 def _resume_rank(rank, port, ckpt, out):
     """world-2 (gloo) rank: rank 0 saves after one step, every rank resumes
     from rank 0's checkpoint and takes one more step"""
+    import os
+    import sys
     import torch.distributed as dist
+    from conftest import PKG
+    sys.path.insert(0, PKG)
     from realnvp_hip.dist import rank_seed
     from realnvp_hip.trainer import FlowTrainer
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -467,3 +471,60 @@ def test_dropin_backward_between_trainer_steps():
     def d(a, b):
         return float((a - b).norm() / b.norm())
     assert d(g2, g0) < max(1e-4, 8 * d(g1, g0)), (d(g2, g0), d(g1, g0))
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("shape", [(32, 8, 1, 4), (64, 32, 4, 16)], ids=["m32_d8_r1_b4", "m64_d32_r4_b16"])
+def test_chained_couplings_match_unchained(shape, dtype):
+    """Consecutive couplings chained (rnvp_coupling_out_in_fwd: one launch
+    writes z and the next coupling's h0 from closed-form in_bn statistics;
+    rnvp_coupling_in_bwd_chain: the next coupling's in backward reduces this
+    one's out_bn backward sums) against every in / out part launched on its
+    own: the same step up to fp64 summation order -- per-sample log-prob,
+    the whole gradient arena, BN running statistics and the next step."""
+    from realnvp_hip import trainer as TM
+    from realnvp_hip.trainer import FlowTrainer
+    size, bd, rb, B = shape
+    out = {}
+    for chain in (0, 1):
+        old = TM.CHAIN_COUPLING
+        TM.CHAIN_COUPLING = chain
+        try:
+            model = make_model(size, bd, rb)
+            tr = FlowTrainer(model, B, dtype=dtype)
+            n_chained = sum(v is not None for v in tr.chain.values())
+            assert (n_chained > 0) == bool(chain), n_chained
+            tr.set_pixels(pixels(B, 3, size, seed=3).to(DEV))
+            tr.step()
+            g1 = tr.grad.clone()
+            lp1 = tr.lp.clone()
+            tr.step()
+            torch.cuda.synchronize()
+            bufs = torch.cat([b.detach().double().flatten() for n, b in model.named_buffers() if "running" in n])
+            out[chain] = (lp1, g1, tr.lp.clone(), tr.grad.clone(), tr.param.clone(), bufs)
+        finally:
+            TM.CHAIN_COUPLING = old
+
+    def d(a, b):
+        return float((a.double() - b.double()).norm() / b.double().norm())
+    (a0, g0, b0, h0, p0, r0), (a1, g1, b1, h1, p1, r1) = out[0], out[1]
+    assert d(r1, r0) < 1e-5, d(r1, r0)
+    assert float((p1 - p0).abs().max()) <= 4 * 5e-4
+    if dtype == "fp32":
+        assert float(((a1 - a0).abs() / a0.abs()).max()) < 1e-6
+        assert float(((b1 - b0).abs() / b0.abs()).max()) < 1e-5
+        assert d(g1, g0) < 1e-4, d(g1, g0)
+        assert d(h1, h0) < 1e-3, d(h1, h0)
+        return
+    # bf16: the closed-form in_bn statistics differ from the summed ones by
+    # fp32 rounding (~1e-7), enough to flip a few bf16 roundings of h0, and
+    # bf16 gradients amplify such flips elementwise (two valid bf16 steps
+    # differ by ~0.6 relative L2 in their largest tensors,
+    # tests/golden/bf16emu_model_m64_d32_r4_b64.npz "full_floor"): per-sample
+    # log-prob and per-tensor gradient norms are the comparable quantities
+    assert float(((a1 - a0).abs() / a0.abs()).max()) < 1e-3
+    sizes = [p.numel() for p in make_model(size, bd, rb).parameters()]
+    offs = np.cumsum([0] + sizes)
+    n0 = np.array([float(g0[o:o + k].double().norm()) for o, k in zip(offs[:-1], sizes)])
+    n1 = np.array([float(g1[o:o + k].double().norm()) for o, k in zip(offs[:-1], sizes)])
+    assert np.linalg.norm(n1 - n0) / np.linalg.norm(n0) < 2e-2

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 O=gpurun_out/${TAG:-r4b}
 mkdir -p $O
 step() { local log=$1; shift; "$@" > $O/$log 2>&1; local rc=$?; echo "$log rc=$rc"; tail -${TAILN:-4} $O/$log; if [ $rc -ne 0 ]; then exit $rc; fi; }
-step pytest_new.log timeout -k 10 900 python -u -m pytest tests/test_gpu_group.py tests/test_gpu_trainer.py tests/test_gpu_deep.py tests/test_gpu_c4.py -m gpu -v -rf --timeout 300 --timeout-method thread
+step pytest_new.log timeout -k 10 1000 python -u -m pytest tests/test_gpu_group.py tests/test_gpu_trainer.py tests/test_gpu_deep.py tests/test_gpu_c4.py tests/test_gpu_parity.py -m gpu -v -rf --timeout 300 --maxfail 10 --timeout-method thread
 step smoke.log timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()"
 step gloo2.log env RNVP_BENCH_BACKEND=gloo timeout -k 10 400 python3 -u bench.py --gpus 2 --steps 3 --warmup 1 --no-secondary --no-cpu-baseline
 step mb_wt1.txt timeout -k 10 300 python3 -u tools/conv_microbench.py --case=wgrad
