@@ -1195,7 +1195,12 @@ int dispatch_conv(const rnvp_conv_args* a, hipStream_t s) {
         const int r = rnvp_conv_s1_launch(a, s);
         if (r != RNVP_E_UNSUPPORTED) return r;
     }
-    if (tuned && band_ok<T>(a)) return dispatch_band<T>(a, s);
+    if (tuned && band_ok<T>(a)) {
+        // the persistent band kernel (conv_band.hip) where it applies
+        const int r = rnvp_conv_band2_launch(a, s);
+        if (r != RNVP_E_UNSUPPORTED) return r;
+        return dispatch_band<T>(a, s);
+    }
     if (stream_ok<T>(a)) return dispatch_stream<T>(a, s);
     if (tuned && halo_ok<T>(a)) return dispatch_halo<T>(a, s);
     // largest tile that still gives >= 512 workgroups (2 per CU); small grids

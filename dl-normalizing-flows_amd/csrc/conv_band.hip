@@ -1,0 +1,407 @@
+// Persistent band kernel for the wide-scale 3x3 convs (cs_in <= 64, 32 or 64
+// outputs, M = 32k .. 2M pixels: scales 1-2 of the 64x64 flow).
+// WeightNormConv2d (modules_realnvp.py:64-71) with the fused BN+ReLU
+// prologue and the bias / residual / skip / next-BN-statistics (or dgrad
+// ReLU/BN-backward) epilogue, as rnvp_conv2d's other families.
+//
+// One workgroup per CU walks a contiguous run of pixel bands (BM = 64*TM
+// pixels, whole image rows at 64x64 / 32x32):
+//   * the packed weights, the BatchNorm tables and the bias go to LDS ONCE per
+//     workgroup (the one-band-per-workgroup kernel, conv.hip k_conv_band,
+//     reloaded its 19-75 KB of weights for every band, in dependent rounds);
+//   * bands are double buffered: band k+1's rows + halo are loaded into
+//     registers before band k's MFMAs and written (BN+ReLU'd) into the other
+//     LDS buffer after them -- no band load waits alone;
+//   * band k's epilogue operands (residual, the previous skip sum, the dgrad
+//     epilogue's pre-BN x) are loaded before its MFMAs;
+//   * BatchNorm batch statistics accumulate in registers over all the
+//     workgroup's bands: one fp64 atomic per channel and workgroup.
+// MFMA: transposed product D[n][m] (a lane owns 4 consecutive output
+// channels of one pixel), eight waves = 4 pixel groups x 2 channel halves.
+#include "common.h"
+#include "conv_common.h"
+
+namespace {
+
+template <typename T, int NT, int TM>
+struct BandGeo {
+    static constexpr int CH = Mf<T>::CH, KS = 4 * CH;
+    static constexpr int NC = 16 * NT;          // output channels (padded)
+    static constexpr int BM = 64 * TM;          // band pixels: 4 pixel groups x 16*TM
+};
+
+template <typename T>
+__host__ __device__ inline int band2_kpl(int cs) {
+    constexpr int CH = Mf<T>::CH, KS = 4 * CH;
+    const int nsteps = (9 * cs + KS - 1) / KS;
+    return nsteps * KS + CH;   // weight row pitch (+16 B)
+}
+
+template <typename T, int NT, int TM>
+size_t band2_lds_bytes(int cs, int W) {
+    using G = BandGeo<T, NT, TM>;
+    const int ntmp = cs > G::NC ? cs : G::NC;
+    const int R = G::BM + 2 * (W + 1);
+    const int pitch = cs + G::CH;
+    return 16 * (size_t)ntmp + 8 * (size_t)cs + 20 * (size_t)G::NC + 64 * (size_t)G::NC +
+           ((size_t)G::NC * band2_kpl<T>(cs) + (size_t)pitch + 2 * (size_t)R * pitch) * sizeof(T);
+}
+
+// raw epilogue operand of 4 channels (bf16: 8 B, f32: 16 B) and its unpack
+template <typename T> struct Raw4;
+template <> struct Raw4<bf16_t> {
+    using type = uint2;
+    __device__ static __forceinline__ void cvt(const uint2 u, float* f) {
+        f[0] = __uint_as_float(u.x << 16); f[1] = __uint_as_float(u.x & 0xffff0000u);
+        f[2] = __uint_as_float(u.y << 16); f[3] = __uint_as_float(u.y & 0xffff0000u);
+    }
+};
+template <> struct Raw4<float> {
+    using type = u32x4;
+    __device__ static __forceinline__ void cvt(const u32x4 u, float* f) {
+        f[0] = __uint_as_float(u.x); f[1] = __uint_as_float(u.y); f[2] = __uint_as_float(u.z); f[3] = __uint_as_float(u.w);
+    }
+};
+
+// NOPS epilogue operand streams (residual, previous y for the skip
+// accumulation, the dgrad epilogue's pre-BN x -- in that order, those present)
+template <typename T, int NT, int TM, bool PRO, int NOPS>
+__global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards, int per) {
+    using RT = typename Raw4<T>::type;
+    using G = BandGeo<T, NT, TM>;
+    constexpr int CH = G::CH, KS = G::KS, NC = G::NC, BM = G::BM;
+    constexpr int NTW = NT / 2;                 // channel tiles per wave (two channel halves)
+    constexpr int NTH = 512;
+    constexpr int SB = 8;                       // staged 16-B chunks per thread per band (checked by the launcher)
+    constexpr int WB = 10;                      // weight chunks per thread (launcher: NC * kpl / CH <= WB * NTH)
+    static_assert(NT % 2 == 0, "two channel halves");
+    extern __shared__ double dsm[];
+    const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
+    const int wid = (tid >> 6) & 3, hf = tid >> 8;   // pixel group, channel half
+    const int M = a.B * a.H * a.W, W = a.W, H = a.H;
+    const int N = a.n, cs = a.cs_in;
+    const int K = 9 * cs;
+    const int nsteps = (K + KS - 1) / KS;
+    const int kpl = nsteps * KS + CH;
+    const bool epi_bn = a.epi_relu_bn_bwd != 0;
+    const int ntmp = cs > NC ? cs : NC;
+    const int hal = W + 1, R = BM + 2 * hal;
+    const int pitch = cs + CH;                  // band row pitch (+16 B)
+    const int nbands = (M + BM - 1) / BM;
+    const int b0 = blockIdx.x * per, b1 = min(nbands, b0 + per);
+    if (b0 >= b1) return;                       // (uniform: whole workgroup)
+
+    double* tmp = dsm;
+    float* bnp = (float*)(dsm + 2 * ntmp);      // scale | shift [cs each]
+    float* etab = bnp + 2 * cs;                 // scale | shift | mean | rstd [NC each]
+    float* btab = etab + 4 * NC;                // bias [NC]
+    double* red = (double*)(btab + NC);         // [4 pixel groups][NC][2]
+    T* Wl = (T*)(red + 8 * NC);                 // [NC][kpl]
+    T* zrow = Wl + NC * kpl;                    // [pitch] zeros
+    T* act0 = zrow + pitch;                     // [2][R][pitch]
+
+    const T* __restrict__ X = (const T*)a.x;
+    // cs <= 64: a row is cpr <= 16 chunks and NTH % cpr == 0 (launcher), so a
+    // thread's chunk column is fixed: its BN coefficients live in registers
+    const int cpr = cs / CH;
+    const int cfix = tid % cpr, rbase = tid / cpr, rstep = NTH / cpr;
+    u32x4 sv[SB];
+    auto stage_load = [&](int band) {
+        const int m0 = band * BM;
+#pragma unroll
+        for (int u = 0; u < SB; ++u) {
+            if (u * rstep >= R) break;          // uniform: no thread has a row left
+            const int r = rbase + u * rstep;
+            const int p = m0 - hal + r;
+            const bool ok = (r < R) & (p >= 0) & (p < M);
+            sv[u] = *(const u32x4*)(X + (ok ? (long long)p * cs + cfix * CH : 0));
+        }
+    };
+    float scv[CH], shv[CH];
+    auto stage_store = [&](int band, T* act) {
+        const int m0 = band * BM;
+#pragma unroll
+        for (int u = 0; u < SB; ++u) {
+            if (u * rstep >= R) break;
+            const int r = rbase + u * rstep;
+            if (r >= R) continue;
+            const int p = m0 - hal + r;
+            u32x4 w = sv[u];
+            if (PRO) {
+                float f[CH];
+                unpack(w, f, T());
+#pragma unroll
+                for (int e = 0; e < CH; ++e) f[e] = fmaxf(f[e] * scv[e] + shv[e], 0.f);
+                w = pack(f, T());
+            }
+            const uint32_t keep = (p >= 0 && p < M) ? ~0u : 0u;
+            *(u32x4*)(act + r * pitch + cfix * CH) = w & u32x4{keep, keep, keep, keep};
+        }
+    };
+
+    // ---- prologue: first band, all weights in flight; tables meanwhile ----
+    stage_load(b0);
+    const T* Wg = (const T*)a.w;
+    const int wcpr = kpl / CH, wtot = NC * wcpr, kv = nsteps * KS;
+    const float rw = 1.0f / (float)wcpr;
+    u32x4 wv[WB];
+#pragma unroll
+    for (int u = 0; u < WB; ++u) {
+        const int q = u * NTH + tid;
+        const int r = fdiv_small(q, rw), c = q - r * wcpr;
+        const bool ok = (q < wtot) & (r < N) & (c * CH < kv);
+        wv[u] = *(const u32x4*)(Wg + (ok ? (long long)r * a.kp + c * CH : 0));
+        if (!ok) wv[u] = u32x4{0u, 0u, 0u, 0u};
+    }
+    if (PRO) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + cs, nullptr, nullptr, tmp);
+    if (epi_bn) block_bn_table(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp);
+#pragma unroll
+    for (int u = 0; u < WB; ++u) {
+        const int q = u * NTH + tid;
+        if (q < wtot) {
+            const int r = fdiv_small(q, rw), c = q - r * wcpr;
+            *(u32x4*)(Wl + r * kpl + c * CH) = wv[u];
+        }
+    }
+    for (int n = tid; n < NC; n += NTH) btab[n] = (a.bias && n < N) ? a.bias[n] : 0.f;
+    for (int c = tid * CH; c < pitch; c += NTH * CH) *(u32x4*)(zrow + c) = u32x4{0u, 0u, 0u, 0u};
+    __syncthreads();
+    if (PRO) {
+#pragma unroll
+        for (int e = 0; e < CH; ++e) {
+            scv[e] = bnp[cfix * CH + e];
+            shv[e] = bnp[cs + cfix * CH + e];
+        }
+    }
+    stage_store(b0, act0);
+    __syncthreads();
+
+    const float rW = 1.0f / (float)W, rH = 1.0f / (float)H;
+    const int cso = a.cs_out;
+    // epilogue streams: role 0 residual, 1 previous y (skip accumulation), 2 pre-BN x
+    const bool p0 = a.residual != nullptr, p1 = a.accumulate != 0;
+    int role[3];
+    role[0] = p0 ? 0 : (p1 ? 1 : 2);
+    role[1] = (p0 && p1) ? 1 : 2;
+    role[2] = 2;
+    const T* opsrc[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+        opsrc[q] = role[q] == 0 ? (const T*)a.residual : (role[q] == 1 ? (const T*)a.y : (const T*)a.epi_x);
+    T* __restrict__ Y = (T*)a.y;
+    double s1[NTW][4], s2[NTW][4];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.0;
+
+    for (int band = b0; band < b1; ++band) {
+        const int cur = (band - b0) & 1;
+        const T* act = act0 + cur * R * pitch;
+        const bool more = band + 1 < b1;
+        if (more) stage_load(band + 1);
+        const int m0 = band * BM;
+        // epilogue operands of this band, in flight under the MFMAs
+        RT pre[NOPS > 0 ? NOPS : 1][TM][NTW];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < NTW; ++j) {
+                const int m = m0 + wid * 16 * TM + i * 16 + li;
+                const int n0 = (hf * NTW + j) * 16 + 4 * g;
+                const long long o = (m < M && n0 < cso) ? (long long)m * cso + n0 : 0;
+#pragma unroll
+                for (int q = 0; q < NOPS; ++q) pre[q][i][j] = *(const RT*)(opsrc[q] + o);
+            }
+        // per-lane pixel state: LDS row of the pixel, in-image taps
+        int rowoff[TM];
+        unsigned tvm[TM];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int lp = wid * 16 * TM + i * 16 + li, m = m0 + lp;
+            rowoff[i] = (lp + hal) * pitch;
+            const int mm = m < M ? m : 0;
+            const int row = fdiv_small(mm, rW);
+            const int x = mm - row * W, y = row - fdiv_small(row, rH) * H;
+            unsigned bits = 0;
+#pragma unroll
+            for (int tp = 0; tp < 9; ++tp) {
+                const int yy = y + tp / 3 - 1, xx = x + tp % 3 - 1;
+                bits |= (unsigned)((m < M) & (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W)) << tp;
+            }
+            tvm[i] = bits;
+        }
+        floatx4 acc[TM][NTW];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < NTW; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        // lane's K position k = s*KS + g*CH -> (tap, ci); a chunk never
+        // straddles a tap (cs % CH == 0); KS / cs <= 4 wraps per step
+        int tap = 0, ci = g * CH;
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+            if (ci >= cs) { ci -= cs; ++tap; }
+        const T* wl = Wl + (hf * NTW * 16 + li) * kpl + g * CH;
+        for (int st = 0; st < nsteps; ++st) {
+            const int ty = tap / 3;
+            const int toff = ((ty - 1) * W + (tap - ty * 3 - 1)) * pitch + ci;
+            const int tsh = tap < 9 ? tap : 31;   // bit 31 of tvm is never set
+            u32x4 wf[NTW], av[TM];
+#pragma unroll
+            for (int j = 0; j < NTW; ++j) wf[j] = *(const u32x4*)(wl + j * 16 * kpl + st * KS);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const bool ok = (tvm[i] >> tsh) & 1u;
+                av[i] = *(const u32x4*)(ok ? act + rowoff[i] + toff : zrow);
+            }
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < NTW; ++j) Mf<T>::step(wf[j], av[i], acc[i][j]);
+            ci += KS;
+#pragma unroll
+            for (int w = 0; w < 4; ++w)
+                if (ci >= cs) { ci -= cs; ++tap; }
+        }
+        // epilogue: lane owns channels j*16 + 4g .. +3 of its pixels
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int m = m0 + wid * 16 * TM + i * 16 + li;
+            if (m >= M) continue;
+#pragma unroll
+            for (int j = 0; j < NTW; ++j) {
+                const int n0 = (hf * NTW + j) * 16 + 4 * g;
+                if (n0 >= cso) continue;
+                float v[4], xv[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + btab[n0 + r];
+#pragma unroll
+                for (int q = 0; q < NOPS; ++q) {
+                    float f[4];
+                    Raw4<T>::cvt(pre[q][i][j], f);
+                    if (role[q] == 2) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) xv[r] = f[r];
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) v[r] += f[r];
+                    }
+                }
+                if (epi_bn) {
+                    const float* et = etab + n0;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        if (xv[r] * et[r] + et[NC + r] <= 0.f) v[r] = 0.f;
+                        s1[j][r] += v[r];
+                        s2[j][r] += v[r] * (xv[r] - et[2 * NC + r]) * et[3 * NC + r];
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        s1[j][r] += v[r];
+                        s2[j][r] += (double)v[r] * v[r];
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (n0 + r >= N) v[r] = 0.f;
+                st4(Y + (long long)m * cso + n0, v);
+            }
+        }
+        if (more) stage_store(band + 1, act0 + (cur ^ 1) * R * pitch);
+        __syncthreads();
+    }
+
+    // ---- batch statistics: DPP row sums, LDS across pixel groups, sharded fp64 atomics ----
+    const bool want_sums = a.out_sums || (epi_bn && a.epi_sums);
+    if (want_sums) {
+#pragma unroll
+        for (int j = 0; j < NTW; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double u1 = row_sum16(s1[j][r]), u2 = row_sum16(s2[j][r]);
+                const int col = (hf * NTW + j) * 16 + 4 * g + r;
+                if (li == 0) {
+                    red[(wid * NC + col) * 2] = u1;
+                    red[(wid * NC + col) * 2 + 1] = u2;
+                }
+            }
+        __syncthreads();
+        double* sums = shard_ptr(epi_bn ? a.epi_sums : a.out_sums, shards, N);
+        for (int n = tid; n < N; n += NTH) {
+            double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                t1 += red[(w * NC + n) * 2];
+                t2 += red[(w * NC + n) * 2 + 1];
+            }
+            atomicAdd(&sums[n], t1);
+            atomicAdd(&sums[N + n], t2);
+        }
+    }
+}
+
+template <typename T, int NT, int TM>
+int launch_band2(const rnvp_conv_args* a, hipStream_t s) {
+    using G = BandGeo<T, NT, TM>;
+    const long long M = (long long)a->B * a->H * a->W;
+    const size_t shm = band2_lds_bytes<T, NT, TM>(a->cs_in, a->W);
+    if (shm > 160 * 1024) return RNVP_E_UNSUPPORTED;
+    // every staged row of a band in SB chunks per thread, every weight chunk in WB
+    const int cpr = a->cs_in / G::CH;
+    const int R = G::BM + 2 * (a->W + 1);
+    if ((long long)R * cpr > 8LL * 512) return RNVP_E_UNSUPPORTED;
+    if ((long long)G::NC * (band2_kpl<T>(a->cs_in) / G::CH) > 10LL * 512) return RNVP_E_UNSUPPORTED;
+    const long long nbands = (M + G::BM - 1) / G::BM;
+    const long long grid = nbands < 256 ? nbands : 256;
+    const int per = (int)((nbands + grid - 1) / grid);
+    const unsigned ng = (unsigned)((nbands + per - 1) / per);
+    const int sh = rnvp_stat_shards(M);
+    const int nops = (a->residual ? 1 : 0) + (a->accumulate ? 1 : 0) + (a->epi_relu_bn_bwd ? 1 : 0);
+    if (a->pro_bn_relu) {
+        switch (nops) {
+            case 0: k_conv_band2<T, NT, TM, true, 0><<<ng, 512, shm, s>>>(*a, sh, per); break;
+            case 1: k_conv_band2<T, NT, TM, true, 1><<<ng, 512, shm, s>>>(*a, sh, per); break;
+            case 2: k_conv_band2<T, NT, TM, true, 2><<<ng, 512, shm, s>>>(*a, sh, per); break;
+            default: return RNVP_E_UNSUPPORTED;
+        }
+    } else {
+        switch (nops) {
+            case 0: k_conv_band2<T, NT, TM, false, 0><<<ng, 512, shm, s>>>(*a, sh, per); break;
+            case 1: k_conv_band2<T, NT, TM, false, 1><<<ng, 512, shm, s>>>(*a, sh, per); break;
+            case 2: k_conv_band2<T, NT, TM, false, 2><<<ng, 512, shm, s>>>(*a, sh, per); break;
+            default: k_conv_band2<T, NT, TM, false, 3><<<ng, 512, shm, s>>>(*a, sh, per); break;
+        }
+    }
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+template <typename T>
+int dispatch_band2(const rnvp_conv_args* a, hipStream_t s) {
+    const long long M = (long long)a->B * a->H * a->W;
+    const long long b256 = (M + 255) / 256;
+    // 32 outputs (bf16): 256-pixel bands while that leaves >= 2 bands per
+    // workgroup; otherwise 128-pixel bands (64 outputs: registers)
+    if (a->n <= 32) {
+        if (sizeof(T) == 2 && b256 >= 512) return launch_band2<T, 2, 4>(a, s);
+        return launch_band2<T, 2, 2>(a, s);
+    }
+    return launch_band2<T, 4, 2>(a, s);
+}
+
+}  // namespace
+
+// 3x3, 17..64 outputs, cs_in <= 64 with a fixed chunk column per thread,
+// 32k <= M < 2^21: the persistent band kernel (RNVP_E_UNSUPPORTED otherwise)
+int rnvp_conv_band2_launch(const rnvp_conv_args* a, hipStream_t s) {
+    static const int mode = [] { const char* e = getenv("RNVP_BAND2"); return e ? atoi(e) : 1; }();
+    if (!mode) return RNVP_E_UNSUPPORTED;
+    const long long M = (long long)a->B * a->H * a->W;
+    if (a->ks != 3 || a->n <= 16 || a->n > 64 || a->cs_in > 64 || a->cs_out > 64) return RNVP_E_UNSUPPORTED;
+    if (M < 32768 || M >= (1ll << 21)) return RNVP_E_UNSUPPORTED;
+    const int ch = a->dtype == RNVP_F32 ? 4 : 8;
+    if (a->cs_in % ch || 512 % (a->cs_in / ch) != 0) return RNVP_E_UNSUPPORTED;
+    return a->dtype == RNVP_F32 ? dispatch_band2<float>(a, s) : dispatch_band2<bf16_t>(a, s);
+}

@@ -313,3 +313,7 @@ int rnvp_wgrad_tap_launch(rnvp_wgrad_group* g, hipStream_t s);
 // register-pipelined streaming 1x1 conv (conv_s1.hip): RNVP_E_UNSUPPORTED
 // outside bf16 / 1x1 / <= 64 channels / M >= 16k
 int rnvp_conv_s1_launch(const rnvp_conv_args* a, hipStream_t s);
+
+// persistent band kernel for the wide-scale 3x3 convs (conv_band.hip):
+// RNVP_E_UNSUPPORTED outside 3x3 / 17..64 outputs / cs_in <= 64 / 32k <= M < 2^21
+int rnvp_conv_band2_launch(const rnvp_conv_args* a, hipStream_t s);

@@ -88,7 +88,7 @@ def test_grouped_matches_single_launches(case, dtype):
     # rounding, amplified in the backward by ReLU-kink decisions (~1e-3 per
     # flip, tests/test_gpu_deep.py); bf16: flipped bf16 roundings of stored
     # activations
-    fw = 1e-5 if dtype == "fp32" else 5e-3
+    fw = 1e-5 if dtype == "fp32" else 1e-2
     bw = 3e-3 if dtype == "fp32" else 5e-2
     assert rel(y1, y0) < fw and rel(l1, l0) < fw, (rel(y1, y0), rel(l1, l0))
     assert rel(gx1, gx0) < bw, rel(gx1, gx0)

@@ -480,8 +480,11 @@ def test_chained_couplings_match_unchained(shape, dtype):
     writes z and the next coupling's h0 from closed-form in_bn statistics;
     rnvp_coupling_in_bwd_chain: the next coupling's in backward reduces this
     one's out_bn backward sums) against every in / out part launched on its
-    own: the same step up to fp64 summation order -- per-sample log-prob,
-    the whole gradient arena, BN running statistics and the next step."""
+    own: one training step agrees up to summation order -- per-sample
+    log-prob, the whole gradient arena and every BN running statistic.  (Only
+    one step: Adam turns the rounding noise of zero-expectation gradients,
+    e.g. the biases that feed a BatchNorm, into +-lr steps, so later steps
+    are no longer comparable element by element.)"""
     from realnvp_hip import trainer as TM
     from realnvp_hip.trainer import FlowTrainer
     size, bd, rb, B = shape
@@ -496,33 +499,29 @@ def test_chained_couplings_match_unchained(shape, dtype):
             assert (n_chained > 0) == bool(chain), n_chained
             tr.set_pixels(pixels(B, 3, size, seed=3).to(DEV))
             tr.step()
-            g1 = tr.grad.clone()
-            lp1 = tr.lp.clone()
-            tr.step()
             torch.cuda.synchronize()
             bufs = torch.cat([b.detach().double().flatten() for n, b in model.named_buffers() if "running" in n])
-            out[chain] = (lp1, g1, tr.lp.clone(), tr.grad.clone(), tr.param.clone(), bufs)
+            out[chain] = (tr.lp.clone(), tr.grad.clone(), bufs)
         finally:
             TM.CHAIN_COUPLING = old
 
     def d(a, b):
         return float((a.double() - b.double()).norm() / b.double().norm())
-    (a0, g0, b0, h0, p0, r0), (a1, g1, b1, h1, p1, r1) = out[0], out[1]
-    assert d(r1, r0) < 1e-5, d(r1, r0)
-    assert float((p1 - p0).abs().max()) <= 4 * 5e-4
+    (a0, g0, r0), (a1, g1, r1) = out[0], out[1]
     if dtype == "fp32":
         assert float(((a1 - a0).abs() / a0.abs()).max()) < 1e-6
-        assert float(((b1 - b0).abs() / b0.abs()).max()) < 1e-5
         assert d(g1, g0) < 1e-4, d(g1, g0)
-        assert d(h1, h0) < 1e-3, d(h1, h0)
+        assert d(r1, r0) < 1e-6, d(r1, r0)
         return
     # bf16: the closed-form in_bn statistics differ from the summed ones by
     # fp32 rounding (~1e-7), enough to flip a few bf16 roundings of h0, and
     # bf16 gradients amplify such flips elementwise (two valid bf16 steps
     # differ by ~0.6 relative L2 in their largest tensors,
     # tests/golden/bf16emu_model_m64_d32_r4_b64.npz "full_floor"): per-sample
-    # log-prob and per-tensor gradient norms are the comparable quantities
+    # log-prob, per-tensor gradient norms and the running statistics are the
+    # comparable quantities
     assert float(((a1 - a0).abs() / a0.abs()).max()) < 1e-3
+    assert d(r1, r0) < 1e-3, d(r1, r0)
     sizes = [p.numel() for p in make_model(size, bd, rb).parameters()]
     offs = np.cumsum([0] + sizes)
     n0 = np.array([float(g0[o:o + k].double().norm()) for o, k in zip(offs[:-1], sizes)])
