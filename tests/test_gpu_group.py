@@ -94,8 +94,11 @@ def test_grouped_matches_single_launches(case, dtype):
     assert rel(gx1, gx0) < bw, rel(gx1, gx0)
     # biases of convs that feed only a BatchNorm have a zero gradient in exact
     # arithmetic: errors are measured against the largest gradient norm
+    # (bf16: flipped roundings make those zero-expectation gradients noise of
+    # ~1 % of the largest norm)
     gmax = max(float(g0[n].norm()) for n in g0)
-    worst = max((float((g1[n] - g0[n]).norm()) / (float(g0[n].norm()) + 1e-3 * gmax), n) for n in g0)
+    floor = 1e-3 if dtype == "fp32" else 3e-2
+    worst = max((float((g1[n] - g0[n]).norm()) / (float(g0[n].norm()) + floor * gmax), n) for n in g0)
     assert worst[0] < 10 * bw, worst
 
 
