@@ -539,8 +539,12 @@ class CouplingEngine:
         a = self._coupling_args(T, x, B, H, W, dtype, training)
         a.in_sums = ar.ptr("in_sums")
         a.h0 = ar.ptr("h0")
+        n_el, esz = x.numel(), DTYPES[dtype][1]
+        cs_h0, cs_st = chan_stride(self.P.buf_ch["h0"]), chan_stride(self.P.buf_ch["st"])
         if not in_done:
-            L.coupling_in_fwd(C.byref(a), s)
+            # algorithmic bytes: x read by the stats and the apply pass, h0 written
+            _launch("coupling", (8 if training else 4) * n_el + esz * B * H * W * cs_h0, 0.0, L.coupling_in_fwd,
+                    C.byref(a), s)
         self._net_forward(T, sv, ws, training, s)
         if training and "bn_table" in sv:
             # the net BNs' running-stat updates ride on the out launch
@@ -557,9 +561,11 @@ class CouplingEngine:
             nx.in_sums = nsv["arena"].ptr("in_sums")
             nx.h0 = nsv["arena"].ptr("h0")
             a.next_sums = ar.ptr("next_sums")
-            L.coupling_out_in_fwd(C.byref(a), C.byref(nx), s)
+            # x, u (w + r), z; st read; the next coupling's h0 written
+            _launch("coupling", 16 * n_el + esz * B * H * W * (cs_st + cs_h0), 0.0, L.coupling_out_in_fwd,
+                    C.byref(a), C.byref(nx), s)
         else:
-            L.coupling_out_fwd(C.byref(a), s)
+            _launch("coupling", 16 * n_el + esz * B * H * W * cs_st, 0.0, L.coupling_out_fwd, C.byref(a), s)
         sv["x"] = x
         return z, (ldj_full if full_ldj else ldj_sample), sv
 
@@ -726,7 +732,11 @@ class CouplingEngine:
         a.g_scale, a.g_scale_shift = gp("scale"), gp("scale_shift")
         a.gscale_part = sar.ptr("gscale_part")
         a.bwd_sums_ready = int(bool(sums_ready))
-        L.coupling_out_bwd(C.byref(a), s)
+        n_el, esz = x.numel(), DTYPES[dtype][1]
+        cs_st = chan_stride(self.P.buf_ch["st"])
+        # (reduction: gz, u) + apply: gz, u, x read, gx written; st read, gst written
+        _launch("coupling", (0 if sums_ready else 8 * n_el) + 16 * n_el + esz * B * H * W * 2 * cs_st, 0.0,
+                L.coupling_out_bwd, C.byref(a), s)
 
         # the net's data-gradient chain and grouped weight gradients: argument
         # structs cached per (saved arena, scratch, weight set); only the
@@ -785,9 +795,11 @@ class CouplingEngine:
             pv.u, pv.out_sums = psv["arena"].ptr("u"), psv["arena"].ptr("out_sums")
             pv.bwd_sums = peng.scratch(B, H, W, dtype, x.device)["arena"].ptr("bwd_sums")
             pv.gl_sample = gl_sample.data_ptr() if gl_sample is not None else None
-            L.coupling_in_bwd_chain(C.byref(a), C.byref(pv), s)
+            # reduction: x, gh0; apply: x, gx (r + w), gh0, and the previous coupling's u
+            _launch("coupling", 20 * n_el + 2 * esz * B * H * W * a.cs_gh0, 0.0, L.coupling_in_bwd_chain,
+                    C.byref(a), C.byref(pv), s)
         else:
-            L.coupling_in_bwd(C.byref(a), s)
+            _launch("coupling", 16 * n_el + 2 * esz * B * H * W * a.cs_gh0, 0.0, L.coupling_in_bwd, C.byref(a), s)
 
         # ... while the weight gradients (grouped wgrad + weight-norm backward)
         # only feed the optimizer: on a side stream they overlap the backward
