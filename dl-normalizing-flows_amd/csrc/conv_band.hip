@@ -23,6 +23,17 @@
 
 namespace {
 
+// phase stamps for tools/probe/band_stamps.hip (compiled out of the product):
+// [wg][16]: 0 start, 1 tables + weights in LDS, 2 first band in LDS, then per
+// band k < 6: 3+2k MFMAs done, 4+2k epilogue done; 15 end
+#ifdef RNVP_BAND_STAMPS
+__device__ unsigned long long* g_band_stamps;
+#define BAND_STAMP(i) \
+    do { if (threadIdx.x == 0 && (i) < 16) g_band_stamps[blockIdx.x * 16 + (i)] = wall_clock64(); } while (0)
+#else
+#define BAND_STAMP(i) do {} while (0)
+#endif
+
 template <typename T, int NT, int TM>
 struct BandGeo {
     static constexpr int CH = Mf<T>::CH, KS = 4 * CH;
@@ -140,6 +151,7 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
     };
 
     // ---- prologue: first band, all weights in flight; tables meanwhile ----
+    BAND_STAMP(0);
     stage_load(b0);
     const T* Wg = (const T*)a.w;
     const int wcpr = kpl / CH, wtot = NC * wcpr, kv = nsteps * KS;
@@ -166,6 +178,7 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
     for (int n = tid; n < NC; n += NTH) btab[n] = (a.bias && n < N) ? a.bias[n] : 0.f;
     for (int c = tid * CH; c < pitch; c += NTH * CH) *(u32x4*)(zrow + c) = u32x4{0u, 0u, 0u, 0u};
     __syncthreads();
+    BAND_STAMP(1);
     if (PRO) {
 #pragma unroll
         for (int e = 0; e < CH; ++e) {
@@ -175,6 +188,7 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
     }
     stage_store(b0, act0);
     __syncthreads();
+    BAND_STAMP(2);
 
     const float rW = 1.0f / (float)W, rH = 1.0f / (float)H;
     const int cso = a.cs_out;
@@ -264,6 +278,7 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
             for (int w = 0; w < 4; ++w)
                 if (ci >= cs) { ci -= cs; ++tap; }
         }
+        if ((band - b0) < 6) BAND_STAMP(3 + 2 * (band - b0));
         // epilogue: lane owns channels j*16 + 4g .. +3 of its pixels
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
@@ -309,6 +324,7 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
                 st4(Y + (long long)m * cso + n0, v);
             }
         }
+        if ((band - b0) < 6) BAND_STAMP(4 + 2 * (band - b0));
         if (more) stage_store(band + 1, act0 + (cur ^ 1) * R * pitch);
         __syncthreads();
     }
@@ -340,6 +356,7 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
             atomicAdd(&sums[N + n], t2);
         }
     }
+    BAND_STAMP(15);
 }
 
 template <typename T, int NT, int TM>
@@ -396,7 +413,7 @@ int dispatch_band2(const rnvp_conv_args* a, hipStream_t s) {
 // 3x3, 17..64 outputs, cs_in <= 64 with a fixed chunk column per thread,
 // 32k <= M < 2^21: the persistent band kernel (RNVP_E_UNSUPPORTED otherwise)
 int rnvp_conv_band2_launch(const rnvp_conv_args* a, hipStream_t s) {
-    static const int mode = [] { const char* e = getenv("RNVP_BAND2"); return e ? atoi(e) : 1; }();
+    static const int mode = [] { const char* e = getenv("RNVP_BAND2"); return e ? atoi(e) : 0; }();
     if (!mode) return RNVP_E_UNSUPPORTED;
     const long long M = (long long)a->B * a->H * a->W;
     if (a->ks != 3 || a->n <= 16 || a->n > 64 || a->cs_in > 64 || a->cs_out > 64) return RNVP_E_UNSUPPORTED;

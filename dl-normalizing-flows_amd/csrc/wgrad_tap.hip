@@ -396,12 +396,22 @@ __global__ __launch_bounds__(WT_NT) void k_wgrad_tap(rnvp_wgrad_group g) {
     const rnvp_wgrad_conv& gc = g.conv[c];
     const WtConv cv{gc.x, gc.dy, gc.ws, gc.wsb, gc.pro, gc.cs_in, gc.cin, gc.cs_dy, gc.n, gc.kp, gc.pro_bn_relu,
                     gc.nz, gc.nrep, g.B, g.H, g.W, gc.m_per_slab};
-    const int tco = (gc.n + wt_tco(CLS) - 1) / wt_tco(CLS), tci = gc.tk;
+    const int cls = CLS >= 0 ? CLS : gc.cls;
+    const int tco = (gc.n + wt_tco(cls) - 1) / wt_tco(cls), tci = gc.tk;
     const int local = t - gc.task0;
     const int per = tco * tci;
     const int z = local / per, rr = local - z * per;
     const int cot = rr / tci, cit = rr - cot * tci;
-    wt_body<CLS>(cv, cot, cit, z, lds);
+    if constexpr (CLS >= 0) {
+        wt_body<CLS>(cv, cot, cit, z, lds);
+    } else {
+        switch (cls) {
+            case 0: wt_body<0>(cv, cot, cit, z, lds); break;
+            case 1: wt_body<1>(cv, cot, cit, z, lds); break;
+            case 2: wt_body<2>(cv, cot, cit, z, lds); break;
+            default: wt_body<3>(cv, cot, cit, z, lds); break;
+        }
+    }
 }
 
 using WtKernel = void (*)(rnvp_wgrad_group);
@@ -427,12 +437,13 @@ long long wt_tasks(const rnvp_wgrad_conv& v, int cls) {
     return (long long)v.nz * ((v.n + wt_tco(cls) - 1) / wt_tco(cls)) * ((v.cs_in + wt_tci(cls) - 1) / wt_tci(cls));
 }
 
-// tile class of a conv: the widest tiles (fewest operand re-reads) unless
-// they leave the GPU short of workgroups -- the deep scales' convs (M <= 16k
-// pixels, nz <= 8 slabs) then take the 32 x 32 (3x3) / 64 x 64 (1x1) tiles:
-// 4x the workgroups.  RNVP_WT_POLICY=0 keeps the channel-count rule only.
+// tile class of a conv: by channel count (the widest tiles, fewest operand
+// re-reads).  RNVP_WT_POLICY=1: the deep scales' convs (M <= 16k pixels,
+// nz <= 8 slabs) take the 32 x 32 (3x3) / 64 x 64 (1x1) tiles when the wide
+// ones leave a conv under 256 workgroups (faster alone, slower in the
+// grouped step launch: profiles/r4_wgrad_ab.txt).
 int wt_class(const rnvp_wgrad_conv& v, int H, int W) {
-    static const int policy = [] { const char* e = getenv("RNVP_WT_POLICY"); return e ? atoi(e) : 1; }();
+    static const int policy = [] { const char* e = getenv("RNVP_WT_POLICY"); return e ? atoi(e) : 0; }();
     const int c = wt_class_base(v.ks, v.cs_in, v.cs_dy);
     if (policy == 0) return c;
     const int small = v.ks == 3 ? 2 : 3;
@@ -469,7 +480,24 @@ int rnvp_wgrad_tap_launch(rnvp_wgrad_group* g, hipStream_t s) {
         v.tk = (v.cs_in + wt_tci(cls) - 1) / wt_tci(cls);
         if (wt_tasks(v, cls) <= 0 || wt_tasks(v, cls) > (1ll << 28)) return RNVP_E_INVALID;
     }
-    // one launch per class present, its convs' tasks concatenated
+    // one launch per class present, its convs' tasks concatenated (each class
+    // kernel with its own register budget); RNVP_WT_SPLIT=0: one launch of
+    // the all-class kernel (the largest class's 207 VGPRs for every task)
+    static const int split = [] { const char* e = getenv("RNVP_WT_SPLIT"); return e ? atoi(e) : 1; }();
+    if (!split) {
+        long long tasks = 0;
+        size_t shm = 0;
+        for (int c = 0; c < g->n_conv; ++c) {
+            rnvp_wgrad_conv& v = g->conv[c];
+            v.task0 = (int)tasks;
+            tasks += wt_tasks(v, v.cls);
+            shm = wt_lds_bytes(v.cls, H, W) > shm ? wt_lds_bytes(v.cls, H, W) : shm;
+        }
+        if (tasks > (1ll << 30)) return RNVP_E_INVALID;
+        k_wgrad_tap<-1><<<(unsigned)tasks, WT_NT, shm, s>>>(*g);
+        RNVP_LAUNCH_CHECK();
+        return RNVP_OK;
+    }
     for (int cls = 0; cls < 4; ++cls) {
         rnvp_wgrad_group sub = *g;
         sub.n_conv = 0;
