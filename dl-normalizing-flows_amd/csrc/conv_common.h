@@ -314,6 +314,11 @@ int rnvp_wgrad_tap_launch(rnvp_wgrad_group* g, hipStream_t s);
 // outside bf16 / 1x1 / <= 64 channels / M >= 16k
 int rnvp_conv_s1_launch(const rnvp_conv_args* a, hipStream_t s);
 
+// fan-out groups of 1x1 convs sharing one input at the wide scales (conv_s1.hip):
+// the M > 16k branch of rnvp_net_group_prepare / rnvp_net_group (klass bit 12)
+int rnvp_s1_fanout_prepare(rnvp_net_step* steps, int n, int* klass, int* grid, int* lds_bytes);
+int rnvp_s1_fanout_launch(const rnvp_net_step* steps, int n, int klass, int grid, int lds_bytes, hipStream_t s);
+
 // persistent band kernel for the wide-scale 3x3 convs (conv_band.hip):
 // RNVP_E_UNSUPPORTED outside 3x3 / 17..64 outputs / cs_in <= 64 / 32k <= M < 2^21
 int rnvp_conv_band2_launch(const rnvp_conv_args* a, hipStream_t s);

@@ -165,7 +165,9 @@ extern "C" int rnvp_net_group_prepare(rnvp_net_step* steps, int n, int* klass, i
     if (!steps || n <= 0 || n > RNVP_NET_GROUP_MAX || !klass || !grid || !lds_bytes) return RNVP_E_INVALID;
     const rnvp_conv_args& a0 = steps[0].conv;
     const long long M = (long long)a0.B * a0.H * a0.W;
-    if (M <= 0 || M > 16384) return RNVP_E_UNSUPPORTED;
+    // wide scales: convs sharing one input run as a fan-out (conv_s1.hip)
+    if (M > 16384) return rnvp_s1_fanout_prepare(steps, n, klass, grid, lds_bytes);
+    if (M <= 0) return RNVP_E_UNSUPPORTED;
     if (a0.dtype != RNVP_F32 && a0.dtype != RNVP_BF16) return RNVP_E_INVALID;
     const int kc = a0.dtype == RNVP_F32 ? 16 : 32;   // channels per k-step
     int cfg = -1, nc = -1;
@@ -227,6 +229,10 @@ extern "C" int rnvp_net_group(const rnvp_net_step* steps, int n, int dtype, int 
     if (!steps || n <= 0 || n > RNVP_NET_GROUP_MAX || grid <= 0 || lds_bytes < 0 || lds_bytes > 160 * 1024)
         return RNVP_E_INVALID;
     if (dtype != RNVP_F32 && dtype != RNVP_BF16) return RNVP_E_INVALID;
+    if (klass & (1 << 12)) {
+        if (dtype != RNVP_BF16 || n < 2) return RNVP_E_INVALID;
+        return rnvp_s1_fanout_launch(steps, n, klass, grid, lds_bytes, (hipStream_t)stream);
+    }
     const GroupKernel k = group_kernel(dtype, klass);
     if (!k) return RNVP_E_INVALID;
     const int nw = group_cfg_shape(klass & 15).nw;

@@ -281,7 +281,239 @@ int launch_s1_ops(const rnvp_conv_args* a, hipStream_t s) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Fan-out: several independent 1x1 convs of one net that read the SAME input
+// (wide scales, M > 16k pixels): each input tile is loaded once and feeds
+// every member's MFMAs and epilogue.  The forward pairs core_skips[i] with the
+// next block's first 1x1 (both read x1_{i+1}; in_skip with block 0's, both
+// read x1_0) and the backward runs the data gradients of in_skip and every
+// core_skips[i] (all read d out) -- modules_realnvp.py:175-194.  Members:
+// optional BN+ReLU prologue (their own table), bias, skip accumulation, next-
+// BN statistics (at most one member), no residual / dgrad epilogue
+// (rnvp_net_group_prepare checks).  Weights of all members in LDS.
+constexpr int FAN_MAX = 8;
+
+template <int NT, int NKS, int TW>
+__global__ __launch_bounds__(256, 2) void k_s1_fanout(const rnvp_net_step* __restrict__ steps, int nm) {
+    constexpr int CH = 8, KS = 32, NC = 16 * NT, KL = NKS * KS + CH;   // LDS weight row pitch (+16 B)
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    bf16_t* Wl = (bf16_t*)lds;                                   // [nm][NC][KL]
+    float* bnp = (float*)(Wl + nm * NC * KL);                    // [nm][2][64] prologue scale | shift
+    float* btab = bnp + nm * 128;                                // [nm][NC] bias
+    double* red = (double*)(btab + nm * NC);                     // [4 waves][NC][2]
+    double* tmp = red + 4 * NC * 2;                              // [128] BN-table scratch
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, li = lane & 15;
+    const rnvp_conv_args& a0 = steps[0].conv;
+    const int M = a0.B * a0.H * a0.W;
+    const int cs = a0.cs_in;
+    int sm = -1;                                                 // the member with statistics
+    for (int c = 0; c < nm; ++c)
+        if (steps[c].conv.out_sums) sm = c;
+
+    // ---- weights, bias, prologue tables -> LDS (once per workgroup) ----
+    for (int c = 0; c < nm; ++c) {
+        const rnvp_conv_args& a = steps[c].conv;
+        const bf16_t* Wg = (const bf16_t*)a.w;
+        for (int q = tid; q < NC * (NKS * KS / CH); q += 256) {
+            const int r = q / (NKS * KS / CH), ch = q - r * (NKS * KS / CH);
+            u32x4 v = u32x4{0u, 0u, 0u, 0u};
+            if (r < a.n && ch * CH < cs) v = *(const u32x4*)(Wg + (long long)r * a.kp + ch * CH);
+            *(u32x4*)(Wl + (c * NC + r) * KL + ch * CH) = v;
+        }
+        for (int n = tid; n < NC; n += 256) btab[c * NC + n] = (a.bias && n < a.n) ? a.bias[n] : 0.f;
+        if (a.pro_bn_relu) block_bn_table(a.pro, a.cin, 0, cs, bnp + c * 128, bnp + c * 128 + 64, nullptr, nullptr, tmp);
+    }
+    __syncthreads();
+
+    const __amdgpu_buffer_rsrc_t XR = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a0.x), 0,
+                                                                        (int)((long long)M * cs * 2), 0x00020000);
+    constexpr int OOB = 0x7ffffff0;
+    const int ntiles = (M + 16 * TW - 1) / (16 * TW);
+    const int nwaves = gridDim.x * 4;
+    float s1[NT][4], s2[NT][4];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.f;
+    u32x4 xr[2][TW][NKS];
+    auto load = [&](int t, u32x4 (&X)[TW][NKS]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < TW; ++i) {
+            const int m = t * (16 * TW) + i * 16 + li;
+            const bool okm = (t < ntiles) & (m < M);
+#pragma unroll
+            for (int s = 0; s < NKS; ++s) {
+                const int k = s * KS + g * CH;
+                X[i][s] = __builtin_amdgcn_raw_buffer_load_b128(XR, (okm & (k < cs)) ? (m * cs + k) * 2 : OOB, 0, 0);
+            }
+        }
+    };
+    auto run = [&](int t, const u32x4 (&X)[TW][NKS]) __attribute__((always_inline)) {
+        for (int c = 0; c < nm; ++c) {
+            const rnvp_conv_args& a = steps[c].conv;
+            const bool pro = a.pro_bn_relu != 0;
+            const int cso = a.cs_out, N = a.n;
+            floatx4 acc[TW][NT];
+#pragma unroll
+            for (int i = 0; i < TW; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < NKS; ++s) {
+                u32x4 wf[NT];
+#pragma unroll
+                for (int j = 0; j < NT; ++j) wf[j] = *(const u32x4*)(Wl + (c * NC + j * 16 + li) * KL + s * KS + g * CH);
+#pragma unroll
+                for (int i = 0; i < TW; ++i) {
+                    u32x4 v = X[i][s];
+                    if (pro) {
+                        float f[CH];
+                        unpack(v, f, bf16_t());
+                        const int c0 = s * KS + g * CH;
+                        const float* sc = bnp + c * 128 + c0;
+                        const float* sh = sc + 64;
+#pragma unroll
+                        for (int e = 0; e < CH; ++e) f[e] = fmaxf(f[e] * sc[e] + sh[e], 0.f);
+                        v = pack(f, bf16_t());
+                        const int m = t * (16 * TW) + i * 16 + li;
+                        const uint32_t keep = ((m < M) & (c0 < cs)) ? ~0u : 0u;
+                        v &= u32x4{keep, keep, keep, keep};
+                    }
+#pragma unroll
+                    for (int j = 0; j < NT; ++j) Mf<bf16_t>::step(wf[j], v, acc[i][j]);
+                }
+            }
+            bf16_t* __restrict__ Y = (bf16_t*)a.y;
+            const bool accu = a.accumulate != 0, st = c == sm;
+#pragma unroll
+            for (int i = 0; i < TW; ++i) {
+                const int m = t * (16 * TW) + i * 16 + li;
+                if (m >= M) continue;
+#pragma unroll
+                for (int j = 0; j < NT; ++j) {
+                    const int n0 = j * 16 + 4 * g;
+                    if (n0 >= cso) continue;
+                    float v[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + btab[c * NC + n0 + r];
+                    if (accu) {
+                        float o[4];
+                        ld4(Y + (long long)m * cso + n0, o);
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) v[r] += o[r];
+                    }
+                    if (st) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            s1[j][r] += v[r];
+                            s2[j][r] += v[r] * v[r];
+                        }
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (n0 + r >= N) v[r] = 0.f;
+                    st4(Y + (long long)m * cso + n0, v);
+                }
+            }
+        }
+    };
+    // walk this wave's tiles with the next one in flight (static ring slots)
+    int t = blockIdx.x * 4 + wid;
+    if (t < ntiles) load(t, xr[0]);
+    while (t < ntiles) {
+        if (t + nwaves < ntiles) load(t + nwaves, xr[1]);
+        run(t, xr[0]);
+        t += nwaves;
+        if (t >= ntiles) break;
+        if (t + nwaves < ntiles) load(t + nwaves, xr[0]);
+        run(t, xr[1]);
+        t += nwaves;
+    }
+    if (sm >= 0) {
+        const rnvp_conv_args& a = steps[sm].conv;
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double u1 = row_sum16((double)s1[j][r]), u2 = row_sum16((double)s2[j][r]);
+                if (li == 0) {
+                    red[(wid * NC + j * 16 + 4 * g + r) * 2] = u1;
+                    red[(wid * NC + j * 16 + 4 * g + r) * 2 + 1] = u2;
+                }
+            }
+        __syncthreads();
+        double* sums = shard_ptr(a.out_sums, steps[sm].shards, a.n);
+        for (int n = tid; n < a.n; n += 256) {
+            double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                t1 += red[(w * NC + n) * 2];
+                t2 += red[(w * NC + n) * 2 + 1];
+            }
+            atomicAdd(&sums[n], t1);
+            atomicAdd(&sums[a.n + n], t2);
+        }
+    }
+}
+
+using FanKernel = void (*)(const rnvp_net_step*, int);
+
+FanKernel fan_kernel(int nt, int nks) {
+    if (nt == 1) return nks == 1 ? k_s1_fanout<1, 1, 4> : k_s1_fanout<1, 2, 4>;
+    if (nt == 2) return nks == 1 ? k_s1_fanout<2, 1, 4> : k_s1_fanout<2, 2, 4>;
+    return nks == 1 ? k_s1_fanout<4, 1, 2> : k_s1_fanout<4, 2, 2>;
+}
+
 }  // namespace
+
+// fan-out group of the wide scales (rnvp_net_group_prepare's M > 16k branch):
+// validates, fills the members' shard counts and returns klass = 1 << 12 |
+// NT << 4 | NKS, the grid and the LDS bytes (RNVP_E_UNSUPPORTED: no such form)
+int rnvp_s1_fanout_prepare(rnvp_net_step* steps, int n, int* klass, int* grid, int* lds_bytes) {
+    static const int mode = [] { const char* e = getenv("RNVP_FANOUT"); return e ? atoi(e) : 1; }();
+    if (!mode || n < 2 || n > FAN_MAX) return RNVP_E_UNSUPPORTED;
+    const rnvp_conv_args& a0 = steps[0].conv;
+    const long long M = (long long)a0.B * a0.H * a0.W;
+    if (a0.dtype != RNVP_BF16 || M <= 16384 || M * 64 * 2 >= (1ll << 31)) return RNVP_E_UNSUPPORTED;
+    if (a0.cs_in > 64 || (a0.cs_in & 7) || ((uintptr_t)a0.x & 15)) return RNVP_E_UNSUPPORTED;
+    int nmax = 0, nstats = 0;
+    for (int i = 0; i < n; ++i) {
+        const rnvp_net_step& st = steps[i];
+        const rnvp_conv_args& a = st.conv;
+        if (st.kind != RNVP_STEP_CONV || a.ks != 1 || a.dtype != RNVP_BF16) return RNVP_E_UNSUPPORTED;
+        if (a.x != a0.x || a.cs_in != a0.cs_in || a.B != a0.B || a.H != a0.H || a.W != a0.W) return RNVP_E_UNSUPPORTED;
+        if (a.residual || a.epi_relu_bn_bwd || a.n <= 0 || a.n > 64 || a.cs_out > 64 || a.cs_out < a.n) return RNVP_E_UNSUPPORTED;
+        if (!a.w || !a.y || (a.kp & 63) || a.kp < a.cs_in || ((uintptr_t)a.y & 7) || ((uintptr_t)a.w & 15))
+            return RNVP_E_UNSUPPORTED;
+        if (a.pro_bn_relu && a.pro.sums && a.pro.shards > 32) return RNVP_E_UNSUPPORTED;
+        nstats += a.out_sums != nullptr;
+        nmax = a.n > nmax ? a.n : nmax;
+    }
+    if (nstats > 1) return RNVP_E_UNSUPPORTED;
+    const int nt = nmax <= 16 ? 1 : (nmax <= 32 ? 2 : 4), nks = a0.cs_in <= 32 ? 1 : 2;
+    for (int i = 0; i < n; ++i) steps[i].shards = rnvp_stat_shards(M);
+    const int NC = 16 * nt, KL = nks * 32 + 8;
+    const size_t lds = (size_t)n * NC * KL * 2 + (size_t)n * 128 * 4 + (size_t)n * NC * 4 + 4 * NC * 2 * 8 + 128 * 8;
+    if (lds > 64 * 1024) return RNVP_E_UNSUPPORTED;
+    const FanKernel k = fan_kernel(nt, nks);
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+    const int tw = nt == 4 ? 2 : 4;
+    const long long ntiles = (M + 16 * tw - 1) / (16 * tw);
+    long long gr = (ntiles + 3) / 4;
+    if (gr > 256LL * per_cu) gr = 256LL * per_cu;
+    *klass = (1 << 12) | (nt << 4) | nks;
+    *grid = (int)gr;
+    *lds_bytes = (int)lds;
+    return RNVP_OK;
+}
+
+int rnvp_s1_fanout_launch(const rnvp_net_step* steps, int n, int klass, int grid, int lds_bytes, hipStream_t s) {
+    const FanKernel k = fan_kernel((klass >> 4) & 15, klass & 15);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds_bytes, s, steps, n);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
 
 // 1x1, bf16, N <= 64, cs_in <= 64, M >= 16k: the register-pipelined stream
 int rnvp_conv_s1_launch(const rnvp_conv_args* a, hipStream_t s) {
