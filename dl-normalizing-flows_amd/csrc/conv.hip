@@ -321,7 +321,7 @@ __global__ __launch_bounds__(256) void k_conv_stream(rnvp_conv_args a, int shard
     const int N = a.n, cs = a.cs_in, ks = a.ks, pad = ks >> 1;
     const int K = ks * ks * cs;
     const int nsteps = (K + KS - 1) / KS;
-    const int kpl = nsteps * KS + CH;      // LDS row pitch (+16 B: conflict-free row reads)
+    const int kpl = lds_mfma_pitch(nsteps * KS, CH);   // LDS row pitch (conflict-free row reads)
     const bool pro = a.pro_bn_relu != 0;
     const bool epi_bn = a.epi_relu_bn_bwd != 0;
     const int ntmp = cs > NC ? cs : NC;
@@ -477,7 +477,7 @@ template <typename T>
 size_t stream_lds_bytes(const rnvp_conv_args* a, int nt) {
     constexpr int CH = Mf<T>::CH, KS = 4 * CH;
     const int K = a->ks * a->ks * a->cs_in;
-    const int kpl = ((K + KS - 1) / KS) * KS + CH;
+    const int kpl = lds_mfma_pitch(((K + KS - 1) / KS) * KS, CH);
     const int nc = 16 * nt, ntmp = a->cs_in > nc ? a->cs_in : nc;
     return 16 * (size_t)ntmp + 8 * (size_t)a->cs_in + 16 * (size_t)nc + 4 * (size_t)nc + 64 * (size_t)nc +
            (size_t)nc * kpl * sizeof(T);
@@ -892,11 +892,11 @@ size_t band_lds_bytes(int cs, int n, int W, int ks) {
     constexpr int CH = Mf<T>::CH, KS = 4 * CH, BM = 256;
     const int nc = n <= 16 ? 16 : (n <= 32 ? 32 : 64);
     const int K = ks * ks * cs;
-    const int kpl = ((K + KS - 1) / KS) * KS + CH;
+    const int kpl = lds_mfma_pitch(((K + KS - 1) / KS) * KS, CH);
     const int R = BM + 2 * (ks / 2) * (W + 1);
     const int ntmp = cs > nc ? cs : nc;
     return 16 * (size_t)ntmp + 8 * (size_t)cs + 20 * (size_t)nc + 64 * (size_t)nc +
-           ((size_t)nc * kpl + (size_t)(R + 1) * (cs + CH)) * sizeof(T);
+           ((size_t)nc * kpl + (size_t)(R + 1) * lds_mfma_pitch(cs, CH)) * sizeof(T);
 }
 
 // NH = 2: eight waves, wave pairs split the output channels (each wave 64
@@ -918,11 +918,11 @@ __global__ __launch_bounds__(256 * NH) void k_conv_band(rnvp_conv_args a, int sh
     const int N = a.n, cs = a.cs_in;
     const int K = KSZ * KSZ * cs;
     const int nsteps = (K + KS - 1) / KS;
-    const int kpl = nsteps * KS + CH;          // weight row pitch (+16 B)
+    const int kpl = lds_mfma_pitch(nsteps * KS, CH);   // weight row pitch (conflict-free)
     const bool epi_bn = a.epi_relu_bn_bwd != 0;
     const int ntmp = cs > NC ? cs : NC;
     const int hal = PAD * (W + 1), R = BM + 2 * hal;
-    const int pitch = cs + CH;                 // band row pitch (+16 B)
+    const int pitch = lds_mfma_pitch(cs, CH);  // band row pitch (conflict-free reads)
 
     double* tmp = dsm;
     float* bnp = (float*)(dsm + 2 * ntmp);     // scale | shift [cs each]

@@ -45,7 +45,7 @@ template <typename T>
 __host__ __device__ inline int band2_kpl(int cs) {
     constexpr int CH = Mf<T>::CH, KS = 4 * CH;
     const int nsteps = (9 * cs + KS - 1) / KS;
-    return nsteps * KS + CH;   // weight row pitch (+16 B)
+    return lds_mfma_pitch(nsteps * KS, CH);   // weight row pitch (conflict-free)
 }
 
 template <typename T, int NT, int TM>
@@ -53,7 +53,7 @@ size_t band2_lds_bytes(int cs, int W) {
     using G = BandGeo<T, NT, TM>;
     const int ntmp = cs > G::NC ? cs : G::NC;
     const int R = G::BM + 2 * (W + 1);
-    const int pitch = cs + G::CH;
+    const int pitch = lds_mfma_pitch(cs, G::CH);
     return 16 * (size_t)ntmp + 8 * (size_t)cs + 20 * (size_t)G::NC + 64 * (size_t)G::NC +
            ((size_t)G::NC * band2_kpl<T>(cs) + (size_t)pitch + 2 * (size_t)R * pitch) * sizeof(T);
 }
@@ -93,11 +93,11 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
     const int N = a.n, cs = a.cs_in;
     const int K = 9 * cs;
     const int nsteps = (K + KS - 1) / KS;
-    const int kpl = nsteps * KS + CH;
+    const int kpl = band2_kpl<T>(cs);
     const bool epi_bn = a.epi_relu_bn_bwd != 0;
     const int ntmp = cs > NC ? cs : NC;
     const int hal = W + 1, R = BM + 2 * hal;
-    const int pitch = cs + CH;                  // band row pitch (+16 B)
+    const int pitch = lds_mfma_pitch(cs, CH);   // band row pitch (conflict-free reads)
     const int nbands = (M + BM - 1) / BM;
     const int b0 = blockIdx.x * per, b1 = min(nbands, b0 + per);
     if (b0 >= b1) return;                       // (uniform: whole workgroup)

@@ -1,5 +1,5 @@
-// Deep-scale conv family, device side (included by conv_deep.hip and the
-// persistent net chain, net_chain.hip): the per-tile body and its LDS size.
+// Deep-scale conv family, device side (included by conv_deep.hip): the
+// per-tile body and its LDS size.
 #pragma once
 #include <stdlib.h>
 
@@ -21,7 +21,7 @@ __device__ unsigned long long* g_deep_stamps;
 constexpr int DEEP_MAX_CS = 1024;    // prologue BN table capacity (channels)
 
 template <typename T>
-__host__ __device__ constexpr int deep_pitch(int cs) { return cs + Mf<T>::CH; }
+__host__ __device__ constexpr int deep_pitch(int cs) { return lds_mfma_pitch(cs, Mf<T>::CH); }
 
 template <typename T, int BN, int NW, int WK>
 size_t deep_lds_bytes(int cs, int W, int ks) {

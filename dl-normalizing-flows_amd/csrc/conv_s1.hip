@@ -295,7 +295,7 @@ constexpr int FAN_MAX = 8;
 
 template <int NT, int NKS, int TW>
 __global__ __launch_bounds__(256, 2) void k_s1_fanout(const rnvp_net_step* __restrict__ steps, int nm) {
-    constexpr int CH = 8, KS = 32, NC = 16 * NT, KL = NKS * KS + CH;   // LDS weight row pitch (+16 B)
+    constexpr int CH = 8, KS = 32, NC = 16 * NT, KL = lds_mfma_pitch(NKS * KS, CH);   // LDS weight row pitch
     extern __shared__ __attribute__((aligned(16))) char lds[];
     bf16_t* Wl = (bf16_t*)lds;                                   // [nm][NC][KL]
     float* bnp = (float*)(Wl + nm * NC * KL);                    // [nm][2][64] prologue scale | shift
@@ -492,7 +492,7 @@ int rnvp_s1_fanout_prepare(rnvp_net_step* steps, int n, int* klass, int* grid, i
     if (nstats > 1) return RNVP_E_UNSUPPORTED;
     const int nt = nmax <= 16 ? 1 : (nmax <= 32 ? 2 : 4), nks = a0.cs_in <= 32 ? 1 : 2;
     for (int i = 0; i < n; ++i) steps[i].shards = rnvp_stat_shards(M);
-    const int NC = 16 * nt, KL = nks * 32 + 8;
+    const int NC = 16 * nt, KL = lds_mfma_pitch(nks * 32, 8);
     const size_t lds = (size_t)n * NC * KL * 2 + (size_t)n * 128 * 4 + (size_t)n * NC * 4 + 4 * NC * 2 * 8 + 128 * 8;
     if (lds > 64 * 1024) return RNVP_E_UNSUPPORTED;
     const FanKernel k = fan_kernel(nt, nks);

@@ -480,11 +480,16 @@ int rnvp_wgrad_tap_launch(rnvp_wgrad_group* g, hipStream_t s) {
         v.tk = (v.cs_in + wt_tci(cls) - 1) / wt_tci(cls);
         if (wt_tasks(v, cls) <= 0 || wt_tasks(v, cls) > (1ll << 28)) return RNVP_E_INVALID;
     }
-    // one launch per class present, its convs' tasks concatenated (each class
-    // kernel with its own register budget); RNVP_WT_SPLIT=0: one launch of
-    // the all-class kernel (the largest class's 207 VGPRs for every task)
-    static const int split = [] { const char* e = getenv("RNVP_WT_SPLIT"); return e ? atoi(e) : 1; }();
-    if (!split) {
+    // default: ONE launch for the group -- the class kernel (its own register
+    // budget) when every conv has the same class, else the all-class kernel
+    // (the largest class's 207 VGPRs for every task).  Splitting a mixed group
+    // into one launch per class serialises the launches on the stream and
+    // measured 0.3 ms/step slower (profiles/r4_wgrad_split.txt);
+    // RNVP_WT_SPLIT=1 keeps that variant for A/B.
+    static const int split = [] { const char* e = getenv("RNVP_WT_SPLIT"); return e ? atoi(e) : 0; }();
+    bool one_class = true;
+    for (int c = 1; c < g->n_conv; ++c) one_class = one_class && g->conv[c].cls == g->conv[0].cls;
+    if (!split || one_class) {
         long long tasks = 0;
         size_t shm = 0;
         for (int c = 0; c < g->n_conv; ++c) {
@@ -494,7 +499,10 @@ int rnvp_wgrad_tap_launch(rnvp_wgrad_group* g, hipStream_t s) {
             shm = wt_lds_bytes(v.cls, H, W) > shm ? wt_lds_bytes(v.cls, H, W) : shm;
         }
         if (tasks > (1ll << 30)) return RNVP_E_INVALID;
-        k_wgrad_tap<-1><<<(unsigned)tasks, WT_NT, shm, s>>>(*g);
+        if (one_class)
+            hipLaunchKernelGGL(wt_kernel(g->conv[0].cls), dim3((unsigned)tasks), dim3(WT_NT), shm, s, *g);
+        else
+            k_wgrad_tap<-1><<<(unsigned)tasks, WT_NT, shm, s>>>(*g);
         RNVP_LAUNCH_CHECK();
         return RNVP_OK;
     }
