@@ -74,6 +74,12 @@ __device__ __forceinline__ Tile tile_of(const Geo& g, int TP) {
     return t;
 }
 
+// Elements of a block's first CP_K passes (e0 = 256 k) whose global operands
+// are loaded at kernel entry, before the BN tables / LDS tiles: their memory
+// round trip overlaps the table's (one exposed latency instead of two or
+// three per launch; at the deep scales every thread has <= 2 elements)
+constexpr int CP_K = 4;
+
 // sum over groups of `seg` lanes (power of 2 <= 64; 1 = no reduction)
 __device__ __forceinline__ float seg_sum(float v, int seg) {
     for (int o = 1; o < seg; o <<= 1) v += __shfl_xor(v, o, 64);
@@ -149,21 +155,38 @@ __global__ __launch_bounds__(256) void k_in_stats(rnvp_coupling_args a, int TP, 
     const Geo g = geo(a);
     const Tile t = tile_of(g, TP);
     const int lane = threadIdx.x & 63;
+    const int total = g.Cb * t.tp;
+    auto xidx = [&](int e) {
+        const int cb = e / t.tp, p = t.p0 + (e - cb * t.tp);
+        const int c = (g.kind == 0) ? cb : g.off_base + cb;
+        return ((long long)t.b * g.C + c) * g.HW + p;
+    };
+    float xp[CP_K];
+#pragma unroll
+    for (int k = 0; k < CP_K; ++k) {
+        const int e = k * 256 + threadIdx.x;
+        xp[k] = e < total ? a.x[xidx(e)] : 0.f;
+    }
     lds_zero(red, 2 * g.Cb);
     __syncthreads();
-    const int total = g.Cb * t.tp;
-    for (int e0 = 0; e0 < total; e0 += blockDim.x) {
+    auto body = [&](int e0, float xv) {
         const int e = e0 + threadIdx.x;
         const bool ok = e < total;
         const int cb = ok ? e / t.tp : 0, p = t.p0 + (ok ? e - cb * t.tp : 0);
-        const int c = (g.kind == 0) ? cb : g.off_base + cb;
-        float v = ok ? a.x[((long long)t.b * g.C + c) * g.HW + p] : 0.f;
+        float v = ok ? xv : 0.f;
         if (g.kind == 0 && !ckbd_m(g, p)) v = 0.f;
         const double s1 = seg_sum((double)v, seg), s2 = seg_sum((double)v * v, seg);
         if (ok && (lane & (seg - 1)) == 0) {
             atomicAdd(&red[cb], s1);
             atomicAdd(&red[g.Cb + cb], s2);
         }
+    };
+#pragma unroll
+    for (int k = 0; k < CP_K; ++k)
+        if (k * 256 < total) body(k * 256, xp[k]);
+    for (int e0 = CP_K * 256; e0 < total; e0 += 256) {
+        const int e = e0 + threadIdx.x;
+        body(e0, e < total ? a.x[xidx(e)] : 0.f);
     }
     __syncthreads();
     double* dst = cshard(a.in_sums, 2 * g.Cb);
@@ -180,6 +203,18 @@ __global__ __launch_bounds__(256) void k_in_apply(rnvp_coupling_args a, int TP, 
     float* tab = (float*)dsm;                   // [4*Cb]
     T* h = (T*)(tab + 4 * ((g.Cb + 3) / 4 * 4));  // [tp][cs_h0] (16-B aligned)
     const int cs = a.cs_h0;
+    const int total = g.Cb * t.tp;
+    auto xidx = [&](int e) {
+        const int cb = e / t.tp, p = t.p0 + (e - cb * t.tp);
+        const int c = (g.kind == 0) ? cb : g.off_base + cb;
+        return ((long long)t.b * g.C + c) * g.HW + p;
+    };
+    float xp[CP_K];
+#pragma unroll
+    for (int k = 0; k < CP_K; ++k) {
+        const int e = k * 256 + threadIdx.x;
+        xp[k] = e < total ? a.x[xidx(e)] : 0.f;
+    }
     in_bn_table(a, g, tab);
     if (blockIdx.x == 0 && a.training && a.in_rmean) {
         const double cnt = (double)g.B * g.HW;
@@ -203,16 +238,19 @@ __global__ __launch_bounds__(256) void k_in_apply(rnvp_coupling_args a, int TP, 
         }
     }
     __syncthreads();
-    const int total = g.Cb * t.tp;
-    for (int e = threadIdx.x; e < total; e += blockDim.x) {
+    auto body = [&](int e, float v) {
         const int cb = e / t.tp, pl = e - cb * t.tp, p = t.p0 + pl;
-        const int c = (g.kind == 0) ? cb : g.off_base + cb;
-        float v = a.x[((long long)t.b * g.C + c) * g.HW + p];
         if (g.kind == 0 && !ckbd_m(g, p)) v = 0.f;
         const float xa = v * tab[cb] + tab[g.Cb + cb];
         stv(&h[pl * cs + cb], fmaxf(xa, 0.f));
         stv(&h[pl * cs + g.Cb + cb], fmaxf(-xa, 0.f));
+    };
+#pragma unroll
+    for (int k = 0; k < CP_K; ++k) {
+        const int e = k * 256 + threadIdx.x;
+        if (e < total) body(e, xp[k]);
     }
+    for (int e = CP_K * 256 + threadIdx.x; e < total; e += 256) body(e, a.x[xidx(e)]);
     __syncthreads();
     tile_copy_out<T>(h, t.m0, t.tp, cs, a.h0);
 }
@@ -232,13 +270,23 @@ __global__ __launch_bounds__(256) void k_out1(rnvp_coupling_args a, int TP, int 
     __shared__ float redl[16];
     T* st = (T*)(dsm + 4 * ((g.Cb + 1) / 2 * 2));   // [tp][cs_st]
     const bool nxt = a.next_sums != nullptr && g.kind == 0;
+    const int total = g.C * t.tp;
+    auto xidx = [&](int e) {
+        const int c = e / t.tp, pl = e - c * t.tp;
+        return ((long long)t.b * g.C + c) * g.HW + t.p0 + pl;
+    };
+    float xp[CP_K];
+#pragma unroll
+    for (int k = 0; k < CP_K; ++k) {
+        const int e = k * 256 + threadIdx.x;
+        xp[k] = e < total ? a.x[xidx(e)] : 0.f;
+    }
     lds_zero(red, 4 * g.Cb);
     tile_copy_in<T>(a.st, t.m0, t.tp, a.cs_st, st);
     __syncthreads();
     const float sc = a.scale[0], ss = a.scale_shift[0];
     float sl = 0.f;
-    const int total = g.C * t.tp;
-    for (int e0 = 0; e0 < total; e0 += blockDim.x) {
+    auto body = [&](int e0, float xv) {
         const int e = e0 + threadIdx.x;
         const bool ok = e < total;
         const int c = ok ? e / t.tp : 0, pl = ok ? e - c * t.tp : 0, p = t.p0 + pl;
@@ -246,7 +294,7 @@ __global__ __launch_bounds__(256) void k_out1(rnvp_coupling_args a, int TP, int 
         const bool chan_on = g.kind == 1 && c >= g.on_base && c < g.on_base + g.Cb;
         const int cb = g.kind == 0 ? c : c - g.on_base;
         const bool tr = ok && (g.kind == 0 ? !ckbd_m(g, p) : chan_on);
-        float u = ok ? a.x[idx] : 0.f;
+        float u = ok ? xv : 0.f;
         if (tr) {
             const float sh = ldv(&st[pl * a.cs_st + cb]);
             const float r = ldv(&st[pl * a.cs_st + g.Cb + cb]);
@@ -267,6 +315,14 @@ __global__ __launch_bounds__(256) void k_out1(rnvp_coupling_args a, int TP, int 
                 atomicAdd(&red[3 * g.Cb + cb], t2);
             }
         }
+    };
+    // e0 is block-uniform (seg_sum shuffles need every lane)
+#pragma unroll
+    for (int k = 0; k < CP_K; ++k)
+        if (k * 256 < total) body(k * 256, xp[k]);
+    for (int e0 = CP_K * 256; e0 < total; e0 += 256) {
+        const int e = e0 + threadIdx.x;
+        body(e0, e < total ? a.x[xidx(e)] : 0.f);
     }
     const float dl = block_sum(sl, redl);   // (barriers also publish red)
     if (threadIdx.x == 0 && dl != 0.f) atomicAdd(&a.ldj_sample[t.b], dl);
@@ -341,6 +397,17 @@ __global__ __launch_bounds__(256) void k_out2_in(rnvp_coupling_args a, rnvp_coup
     T* h = (T*)(it + 2 * Cr);                    // nx's h0 tile [tp][cs_h0] (16-B aligned: 20*Cr B)
     const int cs = nx.cs_h0;
     const double cnt = (double)g.B * g.HW;
+    const int total = g.C * t.tp;
+    auto uidx = [&](int e) {
+        const int c = e / t.tp, pl = e - c * t.tp;
+        return ((long long)t.b * g.C + c) * g.HW + t.p0 + pl;
+    };
+    float up[CP_K];
+#pragma unroll
+    for (int k = 0; k < CP_K; ++k) {
+        const int e = k * 256 + threadIdx.x;
+        up[k] = e < total ? a.u[uidx(e)] : 0.f;
+    }
     for (int cb = threadIdx.x; cb < Cb; cb += blockDim.x) {
         float mf, rf, hl;
         double D1, D2;
@@ -397,8 +464,7 @@ __global__ __launch_bounds__(256) void k_out2_in(rnvp_coupling_args a, rnvp_coup
         k = -k * (float)n_transformed(g);
         for (int b = threadIdx.x; b < g.B; b += blockDim.x) a.ldj_sample[b] += k;
     }
-    const int total = g.C * t.tp;
-    for (int e = threadIdx.x; e < total; e += blockDim.x) {
+    auto body = [&](int e, float u) {
         const int c = e / t.tp, pl = e - c * t.tp, p = t.p0 + pl;
         const long long idx = ((long long)t.b * g.C + c) * g.HW + p;
         bool tr;
@@ -410,7 +476,6 @@ __global__ __launch_bounds__(256) void k_out2_in(rnvp_coupling_args a, rnvp_coup
             tr = c >= g.on_base && c < g.on_base + Cb;
             cb = c - g.on_base;
         }
-        const float u = a.u[idx];
         const float zv = tr ? (u - ot[cb]) * ot[Cr + cb] : u;
         a.z[idx] = zv;
         // nx's in part: masked input (checkerboard: every channel at nx's kept
@@ -421,14 +486,20 @@ __global__ __launch_bounds__(256) void k_out2_in(rnvp_coupling_args a, rnvp_coup
             cn = c;
             xm = ckbd_m(gn, p) ? zv : 0.f;
         } else {
-            if (c < gn.off_base || c >= gn.off_base + Cb) continue;
+            if (c < gn.off_base || c >= gn.off_base + Cb) return;
             cn = c - gn.off_base;
             xm = zv;
         }
         const float xa = xm * it[cn] + it[Cr + cn];
         stv(&h[pl * cs + cn], fmaxf(xa, 0.f));
         stv(&h[pl * cs + Cb + cn], fmaxf(-xa, 0.f));
+    };
+#pragma unroll
+    for (int k = 0; k < CP_K; ++k) {
+        const int e = k * 256 + threadIdx.x;
+        if (e < total) body(e, up[k]);
     }
+    for (int e = CP_K * 256 + threadIdx.x; e < total; e += 256) body(e, a.u[uidx(e)]);
     __syncthreads();
     tile_copy_out<T>(h, t.m0, t.tp, cs, nx.h0);
 }
@@ -457,6 +528,9 @@ __global__ void k_out2(rnvp_coupling_args a, int main_grid) {
     }
     const Geo g = geo(a);
     const double cnt = (double)g.B * g.HW;
+    const long long n = (long long)g.B * g.C * g.HW;
+    const long long e_first = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    const float u_first = e_first < n ? a.u[e_first] : 0.f;   // in flight under the table
     for (int cb = threadIdx.x; cb < g.Cb; cb += blockDim.x) {
         double mean = 0, var = 1;
         if (a.coupling_bn) {
@@ -491,8 +565,7 @@ __global__ void k_out2(rnvp_coupling_args a, int main_grid) {
     }
     const T* st = cptr<T>(a.st);
     const float sc = a.scale[0], ss = a.scale_shift[0];
-    const long long n = (long long)g.B * g.C * g.HW;
-    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)main_grid * blockDim.x) {
+    for (long long e = e_first; e < n; e += (long long)main_grid * blockDim.x) {
         const int p = (int)(e % g.HW);
         const long long t = e / g.HW;
         const int c = (int)(t % g.C);
@@ -506,7 +579,7 @@ __global__ void k_out2(rnvp_coupling_args a, int main_grid) {
             tr = c >= g.on_base && c < g.on_base + g.Cb;
             cb = c - g.on_base;
         }
-        float u = a.u[e];
+        float u = e == e_first ? u_first : a.u[e];
         float zv = u;
         if (tr && a.coupling_bn) zv = (u - sh[cb]) * sh[g.Cb + cb];
         a.z[e] = zv;
@@ -594,23 +667,34 @@ __global__ __launch_bounds__(256) void k_out_bwd_red(rnvp_coupling_args a, int T
     const int lane = threadIdx.x & 63;
     double* red = dsm;                           // [3*Cb]
     float* tab = (float*)(dsm + 3 * g.Cb);       // mean | rstd [Cb each]
+    const int total = g.Cb * t.tp;
+    auto eidx = [&](int e) {
+        const int cb = e / t.tp, p = t.p0 + (e - cb * t.tp);
+        const int c = g.kind == 0 ? cb : g.on_base + cb;
+        return ((long long)t.b * g.C + c) * g.HW + p;
+    };
+    float gzp[CP_K], up[CP_K], glp[CP_K];
+#pragma unroll
+    for (int k = 0; k < CP_K; ++k) {
+        const int e = k * 256 + threadIdx.x;
+        const long long idx = e < total ? eidx(e) : 0;
+        gzp[k] = e < total ? a.gz[idx] : 0.f;
+        up[k] = e < total ? a.u[idx] : 0.f;
+        glp[k] = e < total ? gl_at(a, idx, t.b) : 0.f;
+    }
     lds_zero(red, 3 * g.Cb);
     for (int cb = threadIdx.x; cb < g.Cb; cb += blockDim.x) out_bn_stats(a, g, cb, tab[cb], tab[g.Cb + cb]);
     __syncthreads();
-    const int total = g.Cb * t.tp;
-    for (int e0 = 0; e0 < total; e0 += blockDim.x) {
+    auto body = [&](int e0, float gz, float uv, float glv) {
         const int e = e0 + threadIdx.x;
         const bool ok = e < total;
         const int cb = ok ? e / t.tp : 0, p = t.p0 + (ok ? e - cb * t.tp : 0);
-        const int c = g.kind == 0 ? cb : g.on_base + cb;
         const bool tr = ok && (g.kind == 0 ? !ckbd_m(g, p) : true);
         float vA = 0.f, vB = 0.f, vG = 0.f;
         if (tr) {
-            const long long idx = ((long long)t.b * g.C + c) * g.HW + p;
-            const float gz = a.gz[idx];
             vA = gz;
-            vB = gz * (a.u[idx] - tab[cb]) * tab[g.Cb + cb];
-            vG = gl_at(a, idx, t.b);
+            vB = gz * (uv - tab[cb]) * tab[g.Cb + cb];
+            vG = glv;
         }
         const double dA = seg_sum((double)vA, seg), dB = seg_sum((double)vB, seg), dG = seg_sum((double)vG, seg);
         if (ok && (lane & (seg - 1)) == 0) {
@@ -618,6 +702,14 @@ __global__ __launch_bounds__(256) void k_out_bwd_red(rnvp_coupling_args a, int T
             atomicAdd(&red[g.Cb + cb], dB);
             atomicAdd(&red[2 * g.Cb + cb], dG);
         }
+    };
+#pragma unroll
+    for (int k = 0; k < CP_K; ++k)
+        if (k * 256 < total) body(k * 256, gzp[k], up[k], glp[k]);
+    for (int e0 = CP_K * 256; e0 < total; e0 += 256) {
+        const int e = e0 + threadIdx.x;
+        const long long idx = e < total ? eidx(e) : 0;
+        body(e0, e < total ? a.gz[idx] : 0.f, e < total ? a.u[idx] : 0.f, e < total ? gl_at(a, idx, t.b) : 0.f);
     }
     __syncthreads();
     double* dst = cshard(a.bwd_sums, 3 * g.Cb);
@@ -637,6 +729,21 @@ __global__ __launch_bounds__(256) void k_out_bwd_apply(rnvp_coupling_args a, int
     T* st = (T*)(tab + tabn);                         // [tp][cs_st]
     T* gs = st + t.tp * a.cs_st;                      // [tp][cs_gst]
     const double cnt = (double)g.B * g.HW;
+    const int total = g.C * t.tp;
+    auto eidx = [&](int e) {
+        const int c = e / t.tp, pl = e - c * t.tp;
+        return ((long long)t.b * g.C + c) * g.HW + t.p0 + pl;
+    };
+    float gzp[CP_K], up[CP_K], xp[CP_K], glp[CP_K];
+#pragma unroll
+    for (int k = 0; k < CP_K; ++k) {
+        const int e = k * 256 + threadIdx.x;
+        const long long idx = e < total ? eidx(e) : 0;
+        gzp[k] = e < total ? a.gz[idx] : 0.f;
+        up[k] = e < total ? a.u[idx] : 0.f;
+        xp[k] = e < total ? a.x[idx] : 0.f;
+        glp[k] = e < total ? gl_at(a, idx, t.b) : 0.f;
+    }
     for (int cb = threadIdx.x; cb < g.Cb; cb += blockDim.x) {
         float fm = 0.f, rstd = 1.f, kA = 0.f, kB = 0.f;
         if (a.coupling_bn) {
@@ -653,15 +760,13 @@ __global__ __launch_bounds__(256) void k_out_bwd_apply(rnvp_coupling_args a, int
     __syncthreads();
     const float sc = a.scale[0], ss = a.scale_shift[0];
     double gsc = 0.0, gss = 0.0;
-    const int total = g.C * t.tp;
-    for (int e = threadIdx.x; e < total; e += blockDim.x) {
+    auto body = [&](int e, float gz, float uv, float xv, float glv) {
         const int c = e / t.tp, pl = e - c * t.tp, p = t.p0 + pl;
         const long long idx = ((long long)t.b * g.C + c) * g.HW + p;
         const bool chan_on = g.kind == 1 && c >= g.on_base && c < g.on_base + g.Cb;
         const int cb = g.kind == 0 ? c : c - g.on_base;
         const bool has_bn_chan = g.kind == 0 || chan_on;
         const bool tr = g.kind == 0 ? !ckbd_m(g, p) : chan_on;
-        const float gz = a.gz[idx];
         float gu;
         if (!a.coupling_bn || !has_bn_chan) {
             gu = gz;
@@ -669,10 +774,10 @@ __global__ __launch_bounds__(256) void k_out_bwd_apply(rnvp_coupling_args a, int
             const float fm = tab[cb], rstd = tab[g.Cb + cb], kA = tab[2 * g.Cb + cb], kB = tab[3 * g.Cb + cb];
             if (!tr) {   // ckbd kept position: z = u, but u still moves the batch stats
                 gu = gz;
-                if (a.training) gu += rstd * (-kA - (a.u[idx] - fm) * rstd * kB);
+                if (a.training) gu += rstd * (-kA - (uv - fm) * rstd * kB);
             } else {
                 gu = rstd * gz;
-                if (a.training) gu = rstd * (gz - kA - (a.u[idx] - fm) * rstd * kB);
+                if (a.training) gu = rstd * (gz - kA - (uv - fm) * rstd * kB);
             }
         }
         if (tr) {
@@ -680,7 +785,7 @@ __global__ __launch_bounds__(256) void k_out_bwd_apply(rnvp_coupling_args a, int
             const float th = tanhf(r);
             const float ex = expf(sc * th + ss);
             a.gx[idx] = gu * ex;
-            const float glr = gu * a.x[idx] * ex + gl_at(a, idx, t.b);
+            const float glr = gu * xv * ex + glv;
             stv(&gs[pl * a.cs_gst + cb], gu);
             stv(&gs[pl * a.cs_gst + g.Cb + cb], glr * sc * (1.f - th * th));
             gsc += (double)glr * th;
@@ -688,6 +793,15 @@ __global__ __launch_bounds__(256) void k_out_bwd_apply(rnvp_coupling_args a, int
         } else {
             a.gx[idx] = gu;
         }
+    };
+#pragma unroll
+    for (int k = 0; k < CP_K; ++k) {
+        const int e = k * 256 + threadIdx.x;
+        if (e < total) body(e, gzp[k], up[k], xp[k], glp[k]);
+    }
+    for (int e = CP_K * 256 + threadIdx.x; e < total; e += 256) {
+        const long long idx = eidx(e);
+        body(e, a.gz[idx], a.u[idx], a.x[idx], gl_at(a, idx, t.b));
     }
     const float dsc = (float)block_sum(gsc, redl);   // (barriers also publish gs)
     const float dss = (float)block_sum(gss, redl);
@@ -710,10 +824,8 @@ __global__ __launch_bounds__(256) void k_out_bwd_apply(rnvp_coupling_args a, int
 // gxa = d/dxa of [relu(xa), relu(-xa)] . [g1, g2]; gh: LDS tile [tp][cs_gh0]
 template <typename T>
 __device__ __forceinline__ void in_bwd_vals(const rnvp_coupling_args& a, const Geo& g, const Tile& t, const T* gh,
-                                            const float* tab, int cb, int pl, float& gxa, float& xh) {
-    const int c = (g.kind == 0) ? cb : g.off_base + cb;
+                                            const float* tab, int cb, int pl, float v, float& gxa, float& xh) {
     const int p = t.p0 + pl;
-    float v = a.x[((long long)t.b * g.C + c) * g.HW + p];
     if (g.kind == 0 && !ckbd_m(g, p)) v = 0.f;
     const float xa = v * tab[cb] + tab[g.Cb + cb];
     const float g1 = ldv(&gh[pl * a.cs_gh0 + cb]);
@@ -731,22 +843,40 @@ __global__ __launch_bounds__(256) void k_in_bwd_red(rnvp_coupling_args a, int TP
     double* red = dsm;                                   // [2*Cb]
     float* tab = (float*)(dsm + 2 * g.Cb);               // [4*Cb]
     T* gh = (T*)(tab + 4 * ((g.Cb + 3) / 4 * 4));        // [tp][cs_gh0]
+    const int total = g.Cb * t.tp;
+    auto xidx = [&](int e) {
+        const int cb = e / t.tp, p = t.p0 + (e - cb * t.tp);
+        const int c = (g.kind == 0) ? cb : g.off_base + cb;
+        return ((long long)t.b * g.C + c) * g.HW + p;
+    };
+    float xp[CP_K];
+#pragma unroll
+    for (int k = 0; k < CP_K; ++k) {
+        const int e = k * 256 + threadIdx.x;
+        xp[k] = e < total ? a.x[xidx(e)] : 0.f;
+    }
     lds_zero(red, 2 * g.Cb);
     in_bn_table(a, g, tab);
     tile_copy_in<T>(a.gh0, t.m0, t.tp, a.cs_gh0, gh);
     __syncthreads();
-    const int total = g.Cb * t.tp;
-    for (int e0 = 0; e0 < total; e0 += blockDim.x) {
+    auto body = [&](int e0, float xv) {
         const int e = e0 + threadIdx.x;
         const bool ok = e < total;
         const int cb = ok ? e / t.tp : 0, pl = ok ? e - cb * t.tp : 0;
         float gxa = 0.f, xh = 0.f;
-        if (ok) in_bwd_vals<T>(a, g, t, gh, tab, cb, pl, gxa, xh);
+        if (ok) in_bwd_vals<T>(a, g, t, gh, tab, cb, pl, xv, gxa, xh);
         const double s1 = seg_sum((double)gxa, seg), s2 = seg_sum((double)gxa * xh, seg);
         if (ok && (lane & (seg - 1)) == 0) {
             atomicAdd(&red[cb], s1);
             atomicAdd(&red[g.Cb + cb], s2);
         }
+    };
+#pragma unroll
+    for (int k = 0; k < CP_K; ++k)
+        if (k * 256 < total) body(k * 256, xp[k]);
+    for (int e0 = CP_K * 256; e0 < total; e0 += 256) {
+        const int e = e0 + threadIdx.x;
+        body(e0, e < total ? a.x[xidx(e)] : 0.f);
     }
     __syncthreads();
     double* dst = cshard(a.in_bwd_sums, 2 * g.Cb);
@@ -763,6 +893,21 @@ __global__ __launch_bounds__(256) void k_in_bwd_apply(rnvp_coupling_args a, rnvp
     const int tabn = 12 * ((g.Cb + 3) / 4 * 4);
     double* pred = (double*)(tab + tabn);                // CHAIN: prev's A | B | G [Cb each]
     T* gh = (T*)(pred + (CHAIN ? 3 * ((g.Cb + 1) / 2 * 2) : 0));
+    const int total = g.Cb * t.tp;
+    auto xidx = [&](int e) {
+        const int cb = e / t.tp, p = t.p0 + (e - cb * t.tp);
+        const int c = (g.kind == 0) ? cb : g.off_base + cb;
+        return ((long long)t.b * g.C + c) * g.HW + p;
+    };
+    float xp[CP_K], gxp[CP_K], pup[CP_K];
+#pragma unroll
+    for (int k = 0; k < CP_K; ++k) {
+        const int e = k * 256 + threadIdx.x;
+        const long long idx = e < total ? xidx(e) : 0;
+        xp[k] = e < total ? a.x[idx] : 0.f;
+        gxp[k] = e < total ? a.gx[idx] : 0.f;
+        pup[k] = (CHAIN && e < total) ? pv.u[idx] : 0.f;
+    }
     if (CHAIN) {
         lds_zero(pred, 3 * g.Cb);
         const Geo gp = geo(pv);
@@ -802,8 +947,7 @@ __global__ __launch_bounds__(256) void k_in_bwd_apply(rnvp_coupling_args a, rnvp
     }
     tile_copy_in<T>(a.gh0, t.m0, t.tp, a.cs_gh0, gh);
     __syncthreads();
-    const int total = g.Cb * t.tp;
-    for (int e0 = 0; e0 < total; e0 += blockDim.x) {
+    auto body = [&](int e0, float xv, float gxv, float puv) {
         const int e = e0 + threadIdx.x;
         const bool ok = e < total;
         const int cb = ok ? e / t.tp : 0, pl = ok ? e - cb * t.tp : 0, p = t.p0 + pl;
@@ -813,11 +957,11 @@ __global__ __launch_bounds__(256) void k_in_bwd_apply(rnvp_coupling_args a, rnvp
         bool ptr = false;   // a transformed position of prev (= kept square / conditioning half of a)
         if (ok) {
             float gxa, xh;
-            in_bwd_vals<T>(a, g, t, gh, tab, cb, pl, gxa, xh);
+            in_bwd_vals<T>(a, g, t, gh, tab, cb, pl, xv, gxa, xh);
             float gxm = tab[4 * g.Cb + cb] * (gxa - tab[5 * g.Cb + cb] - xh * tab[6 * g.Cb + cb]);
             const bool kept = g.kind != 0 || ckbd_m(g, p);
             if (!kept) gxm = 0.f;   // xm = x * mask
-            gfin = a.gx[idx] + gxm;
+            gfin = gxv + gxm;
             a.gx[idx] = gfin;
             ptr = kept;
         }
@@ -827,7 +971,7 @@ __global__ __launch_bounds__(256) void k_in_bwd_apply(rnvp_coupling_args a, rnvp
             float vA = 0.f, vB = 0.f, vG = 0.f;
             if (ptr) {
                 vA = gfin;
-                vB = gfin * (pv.u[idx] - tab[7 * g.Cb + cb]) * tab[8 * g.Cb + cb];
+                vB = gfin * (puv - tab[7 * g.Cb + cb]) * tab[8 * g.Cb + cb];
                 vG = pv.gl_sample ? pv.gl_sample[t.b] : 0.f;
             }
             const double dA = seg_sum((double)vA, seg), dB = seg_sum((double)vB, seg), dG = seg_sum((double)vG, seg);
@@ -837,6 +981,15 @@ __global__ __launch_bounds__(256) void k_in_bwd_apply(rnvp_coupling_args a, rnvp
                 atomicAdd(&pred[2 * g.Cb + cb], dG);
             }
         }
+    };
+    // e0 block-uniform (the CHAIN seg_sum shuffles need every lane)
+#pragma unroll
+    for (int k = 0; k < CP_K; ++k)
+        if (k * 256 < total) body(k * 256, xp[k], gxp[k], pup[k]);
+    for (int e0 = CP_K * 256; e0 < total; e0 += 256) {
+        const int e = e0 + threadIdx.x;
+        const long long idx = e < total ? xidx(e) : 0;
+        body(e0, e < total ? a.x[idx] : 0.f, e < total ? a.gx[idx] : 0.f, (CHAIN && e < total) ? pv.u[idx] : 0.f);
     }
     if (CHAIN) {
         __syncthreads();
