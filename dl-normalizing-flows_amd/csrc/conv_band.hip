@@ -18,10 +18,20 @@
 //     workgroup's bands: one fp64 atomic per channel and workgroup.
 // MFMA: transposed product D[n][m] (a lane owns 4 consecutive output
 // channels of one pixel), eight waves = 4 pixel groups x 2 channel halves.
+#include <type_traits>
+
 #include "common.h"
 #include "conv_common.h"
 
 namespace {
+
+template <int N, int I = 0, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<N, I + 1>(f);
+    }
+}
 
 // phase stamps for tools/probe/band_stamps.hip (compiled out of the product):
 // [wg][16]: 0 start, 1 tables + weights in LDS, 2 first band in LDS, then per
@@ -76,11 +86,17 @@ template <> struct Raw4<float> {
 
 // NOPS epilogue operand streams (residual, previous y for the skip
 // accumulation, the dgrad epilogue's pre-BN x -- in that order, those present)
-template <typename T, int NT, int TM, bool PRO, int NOPS>
+// CS: the input channel stride (a power of two, 8..64): the K sequence of a
+// lane -- tap and channel of every k-step -- is static, the k-loop fully
+// unrolled with the next step's fragments read before the current MFMAs.
+template <typename T, int NT, int TM, int CS, bool PRO, int NOPS>
 __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards, int per) {
     using RT = typename Raw4<T>::type;
     using G = BandGeo<T, NT, TM>;
     constexpr int CH = G::CH, KS = G::KS, NC = G::NC, BM = G::BM;
+    static_assert((CS & (CS - 1)) == 0 && CS >= CH && CS <= 64, "channel stride");
+    constexpr int NSTEP = (9 * CS + KS - 1) / KS;
+    constexpr int KPL = lds_mfma_pitch(NSTEP * KS, CH);
     constexpr int NTW = NT / 2;                 // channel tiles per wave (two channel halves)
     constexpr int NTH = 512;
     constexpr int SB = 8;                       // staged 16-B chunks per thread per band (checked by the launcher)
@@ -90,14 +106,14 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
     const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
     const int wid = (tid >> 6) & 3, hf = tid >> 8;   // pixel group, channel half
     const int M = a.B * a.H * a.W, W = a.W, H = a.H;
-    const int N = a.n, cs = a.cs_in;
-    const int K = 9 * cs;
-    const int nsteps = (K + KS - 1) / KS;
-    const int kpl = band2_kpl<T>(cs);
+    const int N = a.n;
+    constexpr int cs = CS;
+    constexpr int nsteps = NSTEP;
+    constexpr int kpl = KPL;
     const bool epi_bn = a.epi_relu_bn_bwd != 0;
     const int ntmp = cs > NC ? cs : NC;
     const int hal = W + 1, R = BM + 2 * hal;
-    const int pitch = lds_mfma_pitch(cs, CH);   // band row pitch (conflict-free reads)
+    constexpr int pitch = lds_mfma_pitch(CS, CH);   // band row pitch (conflict-free reads)
     const int nbands = (M + BM - 1) / BM;
     const int b0 = blockIdx.x * per, b1 = min(nbands, b0 + per);
     if (b0 >= b1) return;                       // (uniform: whole workgroup)
@@ -114,8 +130,9 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
     const T* __restrict__ X = (const T*)a.x;
     // cs <= 64: a row is cpr <= 16 chunks and NTH % cpr == 0 (launcher), so a
     // thread's chunk column is fixed: its BN coefficients live in registers
-    const int cpr = cs / CH;
-    const int cfix = tid % cpr, rbase = tid / cpr, rstep = NTH / cpr;
+    constexpr int cpr = CS / CH;
+    const int cfix = tid % cpr, rbase = tid / cpr;
+    constexpr int rstep = NTH / cpr;
     u32x4 sv[SB];
     auto stage_load = [&](int band) {
         const int m0 = band * BM;
@@ -154,13 +171,12 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
     BAND_STAMP(0);
     stage_load(b0);
     const T* Wg = (const T*)a.w;
-    const int wcpr = kpl / CH, wtot = NC * wcpr, kv = nsteps * KS;
-    const float rw = 1.0f / (float)wcpr;
+    constexpr int wcpr = KPL / CH, wtot = NC * wcpr, kv = NSTEP * KS;
     u32x4 wv[WB];
 #pragma unroll
     for (int u = 0; u < WB; ++u) {
         const int q = u * NTH + tid;
-        const int r = fdiv_small(q, rw), c = q - r * wcpr;
+        const int r = q / wcpr, c = q - r * wcpr;
         const bool ok = (q < wtot) & (r < N) & (c * CH < kv);
         wv[u] = *(const u32x4*)(Wg + (ok ? (long long)r * a.kp + c * CH : 0));
         if (!ok) wv[u] = u32x4{0u, 0u, 0u, 0u};
@@ -171,7 +187,7 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
     for (int u = 0; u < WB; ++u) {
         const int q = u * NTH + tid;
         if (q < wtot) {
-            const int r = fdiv_small(q, rw), c = q - r * wcpr;
+            const int r = q / wcpr, c = q - r * wcpr;
             *(u32x4*)(Wl + r * kpl + c * CH) = wv[u];
         }
     }
@@ -208,6 +224,16 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
     for (int j = 0; j < NTW; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.0;
+    // lane's K position of step st: k = st*KS + g*CH -> (tap, ci) (a chunk
+    // never straddles a tap); its LDS offset from the pixel's own row and the
+    // tap's bit in the in-image mask (31: K padding, never set)
+    int toffl[NSTEP], tshl[NSTEP];
+#pragma unroll
+    for (int st = 0; st < NSTEP; ++st) {
+        const int k = st * KS + g * CH, tap = k / CS, ci = k % CS;
+        toffl[st] = tap < 9 ? ((tap / 3 - 1) * W + (tap % 3 - 1)) * pitch + ci : 0;
+        tshl[st] = tap < 9 ? tap : 31;
+    }
 
     for (int band = b0; band < b1; ++band) {
         const int cur = (band - b0) & 1;
@@ -250,34 +276,29 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < NTW; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-        // lane's K position k = s*KS + g*CH -> (tap, ci); a chunk never
-        // straddles a tap (cs % CH == 0); KS / cs <= 4 wraps per step
-        int tap = 0, ci = g * CH;
+        // the static k-loop: step st's fragments are in registers before its
+        // MFMAs, step st+1's reads issued ahead of them
+        const T* wl = Wl + (hf * NTW * 16 + li) * KPL + g * CH;
+        u32x4 wf[2][NTW], av[2][TM];
+        auto frag = [&](auto STC, int buf) {
+            constexpr int st = decltype(STC)::value;
 #pragma unroll
-        for (int w = 0; w < 4; ++w)
-            if (ci >= cs) { ci -= cs; ++tap; }
-        const T* wl = Wl + (hf * NTW * 16 + li) * kpl + g * CH;
-        for (int st = 0; st < nsteps; ++st) {
-            const int ty = tap / 3;
-            const int toff = ((ty - 1) * W + (tap - ty * 3 - 1)) * pitch + ci;
-            const int tsh = tap < 9 ? tap : 31;   // bit 31 of tvm is never set
-            u32x4 wf[NTW], av[TM];
-#pragma unroll
-            for (int j = 0; j < NTW; ++j) wf[j] = *(const u32x4*)(wl + j * 16 * kpl + st * KS);
+            for (int j = 0; j < NTW; ++j) wf[buf][j] = *(const u32x4*)(wl + j * 16 * KPL + st * KS);
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
-                const bool ok = (tvm[i] >> tsh) & 1u;
-                av[i] = *(const u32x4*)(ok ? act + rowoff[i] + toff : zrow);
+                const bool ok = (tvm[i] >> tshl[st]) & 1u;
+                av[buf][i] = *(const u32x4*)(ok ? act + rowoff[i] + toffl[st] : zrow);
             }
+        };
+        frag(std::integral_constant<int, 0>{}, 0);
+        static_for<NSTEP>([&](auto STC) {
+            constexpr int st = decltype(STC)::value;
+            if constexpr (st + 1 < NSTEP) frag(std::integral_constant<int, st + 1>{}, (st + 1) & 1);
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
-                for (int j = 0; j < NTW; ++j) Mf<T>::step(wf[j], av[i], acc[i][j]);
-            ci += KS;
-#pragma unroll
-            for (int w = 0; w < 4; ++w)
-                if (ci >= cs) { ci -= cs; ++tap; }
-        }
+                for (int j = 0; j < NTW; ++j) Mf<T>::step(wf[st & 1][j], av[st & 1][i], acc[i][j]);
+        });
         if ((band - b0) < 6) BAND_STAMP(3 + 2 * (band - b0));
         // epilogue: lane owns channels j*16 + 4g .. +3 of its pixels
 #pragma unroll
@@ -359,7 +380,7 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
     BAND_STAMP(15);
 }
 
-template <typename T, int NT, int TM>
+template <typename T, int NT, int TM, int CS>
 int launch_band2(const rnvp_conv_args* a, hipStream_t s) {
     using G = BandGeo<T, NT, TM>;
     const long long M = (long long)a->B * a->H * a->W;
@@ -378,34 +399,45 @@ int launch_band2(const rnvp_conv_args* a, hipStream_t s) {
     const int nops = (a->residual ? 1 : 0) + (a->accumulate ? 1 : 0) + (a->epi_relu_bn_bwd ? 1 : 0);
     if (a->pro_bn_relu) {
         switch (nops) {
-            case 0: k_conv_band2<T, NT, TM, true, 0><<<ng, 512, shm, s>>>(*a, sh, per); break;
-            case 1: k_conv_band2<T, NT, TM, true, 1><<<ng, 512, shm, s>>>(*a, sh, per); break;
-            case 2: k_conv_band2<T, NT, TM, true, 2><<<ng, 512, shm, s>>>(*a, sh, per); break;
+            case 0: k_conv_band2<T, NT, TM, CS, true, 0><<<ng, 512, shm, s>>>(*a, sh, per); break;
+            case 1: k_conv_band2<T, NT, TM, CS, true, 1><<<ng, 512, shm, s>>>(*a, sh, per); break;
+            case 2: k_conv_band2<T, NT, TM, CS, true, 2><<<ng, 512, shm, s>>>(*a, sh, per); break;
             default: return RNVP_E_UNSUPPORTED;
         }
     } else {
         switch (nops) {
-            case 0: k_conv_band2<T, NT, TM, false, 0><<<ng, 512, shm, s>>>(*a, sh, per); break;
-            case 1: k_conv_band2<T, NT, TM, false, 1><<<ng, 512, shm, s>>>(*a, sh, per); break;
-            case 2: k_conv_band2<T, NT, TM, false, 2><<<ng, 512, shm, s>>>(*a, sh, per); break;
-            default: k_conv_band2<T, NT, TM, false, 3><<<ng, 512, shm, s>>>(*a, sh, per); break;
+            case 0: k_conv_band2<T, NT, TM, CS, false, 0><<<ng, 512, shm, s>>>(*a, sh, per); break;
+            case 1: k_conv_band2<T, NT, TM, CS, false, 1><<<ng, 512, shm, s>>>(*a, sh, per); break;
+            case 2: k_conv_band2<T, NT, TM, CS, false, 2><<<ng, 512, shm, s>>>(*a, sh, per); break;
+            default: k_conv_band2<T, NT, TM, CS, false, 3><<<ng, 512, shm, s>>>(*a, sh, per); break;
         }
     }
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
 }
 
-template <typename T>
-int dispatch_band2(const rnvp_conv_args* a, hipStream_t s) {
+template <typename T, int CS>
+int dispatch_band2_cs(const rnvp_conv_args* a, hipStream_t s) {
     const long long M = (long long)a->B * a->H * a->W;
     const long long b256 = (M + 255) / 256;
-    // 32 outputs (bf16): 256-pixel bands while that leaves >= 2 bands per
+    // 32 outputs: 256-pixel bands while that leaves >= 2 bands per
     // workgroup; otherwise 128-pixel bands (64 outputs: registers)
     if (a->n <= 32) {
-        if (sizeof(T) == 2 && b256 >= 512) return launch_band2<T, 2, 4>(a, s);
-        return launch_band2<T, 2, 2>(a, s);
+        if (b256 >= 512) return launch_band2<T, 2, 4, CS>(a, s);
+        return launch_band2<T, 2, 2, CS>(a, s);
     }
-    return launch_band2<T, 4, 2>(a, s);
+    return launch_band2<T, 4, 2, CS>(a, s);
+}
+
+template <typename T>
+int dispatch_band2(const rnvp_conv_args* a, hipStream_t s) {
+    switch (a->cs_in) {
+        case 8: return dispatch_band2_cs<T, 8>(a, s);
+        case 16: return dispatch_band2_cs<T, 16>(a, s);
+        case 32: return dispatch_band2_cs<T, 32>(a, s);
+        case 64: return dispatch_band2_cs<T, 64>(a, s);
+        default: return RNVP_E_UNSUPPORTED;
+    }
 }
 
 }  // namespace
@@ -418,7 +450,7 @@ int rnvp_conv_band2_launch(const rnvp_conv_args* a, hipStream_t s) {
     const long long M = (long long)a->B * a->H * a->W;
     if (a->ks != 3 || a->n <= 16 || a->n > 64 || a->cs_in > 64 || a->cs_out > 64) return RNVP_E_UNSUPPORTED;
     if (M < 32768 || M >= (1ll << 21)) return RNVP_E_UNSUPPORTED;
-    const int ch = a->dtype == RNVP_F32 ? 4 : 8;
-    if (a->cs_in % ch || 512 % (a->cs_in / ch) != 0) return RNVP_E_UNSUPPORTED;
-    return a->dtype == RNVP_F32 ? dispatch_band2<float>(a, s) : dispatch_band2<bf16_t>(a, s);
+    // bf16 (the fp32 parity mode keeps the one-band-per-workgroup kernel)
+    if (a->dtype != RNVP_BF16) return RNVP_E_UNSUPPORTED;
+    return dispatch_band2<bf16_t>(a, s);
 }
