@@ -44,11 +44,13 @@ __device__ unsigned long long* g_band_stamps;
 #define BAND_STAMP(i) do {} while (0)
 #endif
 
-template <typename T, int NT, int TM>
+// HF channel groups x WPG = 8 / HF pixel groups of waves
+template <typename T, int NT, int TM, int HF>
 struct BandGeo {
     static constexpr int CH = Mf<T>::CH, KS = 4 * CH;
     static constexpr int NC = 16 * NT;          // output channels (padded)
-    static constexpr int BM = 64 * TM;          // band pixels: 4 pixel groups x 16*TM
+    static constexpr int WPG = 8 / HF;          // pixel groups
+    static constexpr int BM = 16 * TM * WPG;    // band pixels
 };
 
 template <typename T>
@@ -58,13 +60,13 @@ __host__ __device__ inline int band2_kpl(int cs) {
     return lds_mfma_pitch(nsteps * KS, CH);   // weight row pitch (conflict-free)
 }
 
-template <typename T, int NT, int TM>
+template <typename T, int NT, int TM, int HF>
 size_t band2_lds_bytes(int cs, int W) {
-    using G = BandGeo<T, NT, TM>;
+    using G = BandGeo<T, NT, TM, HF>;
     const int ntmp = cs > G::NC ? cs : G::NC;
     const int R = G::BM + 2 * (W + 1);
     const int pitch = lds_mfma_pitch(cs, G::CH);
-    return 16 * (size_t)ntmp + 8 * (size_t)cs + 20 * (size_t)G::NC + 64 * (size_t)G::NC +
+    return 16 * (size_t)ntmp + 8 * (size_t)cs + 20 * (size_t)G::NC + 16 * (size_t)G::WPG * G::NC +
            ((size_t)G::NC * band2_kpl<T>(cs) + (size_t)pitch + 2 * (size_t)R * pitch) * sizeof(T);
 }
 
@@ -89,22 +91,26 @@ template <> struct Raw4<float> {
 // CS: the input channel stride (a power of two, 8..64): the K sequence of a
 // lane -- tap and channel of every k-step -- is static, the k-loop fully
 // unrolled with the next step's fragments read before the current MFMAs.
-template <typename T, int NT, int TM, int CS, bool PRO, int NOPS>
+// HF: channel groups of waves (1: every wave holds all NT channel tiles of
+// its pixels; 2: wave pairs split them).  WREG: the wave's weight fragments
+// of every k-step in registers (read from LDS once per workgroup), so the
+// k-loop reads only activation fragments from LDS.
+template <typename T, int NT, int TM, int CS, int HF, bool WREG, bool PRO, int NOPS>
 __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards, int per) {
     using RT = typename Raw4<T>::type;
-    using G = BandGeo<T, NT, TM>;
-    constexpr int CH = G::CH, KS = G::KS, NC = G::NC, BM = G::BM;
+    using G = BandGeo<T, NT, TM, HF>;
+    constexpr int CH = G::CH, KS = G::KS, NC = G::NC, BM = G::BM, WPG = G::WPG;
     static_assert((CS & (CS - 1)) == 0 && CS >= CH && CS <= 64, "channel stride");
     constexpr int NSTEP = (9 * CS + KS - 1) / KS;
     constexpr int KPL = lds_mfma_pitch(NSTEP * KS, CH);
-    constexpr int NTW = NT / 2;                 // channel tiles per wave (two channel halves)
+    constexpr int NTW = NT / HF;                // channel tiles per wave
     constexpr int NTH = 512;
     constexpr int SB = 8;                       // staged 16-B chunks per thread per band (checked by the launcher)
     constexpr int WB = 10;                      // weight chunks per thread (launcher: NC * kpl / CH <= WB * NTH)
-    static_assert(NT % 2 == 0, "two channel halves");
+    static_assert(NT % HF == 0 && (HF == 1 || HF == 2), "channel groups");
     extern __shared__ double dsm[];
     const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
-    const int wid = (tid >> 6) & 3, hf = tid >> 8;   // pixel group, channel half
+    const int wid = (tid >> 6) % WPG, hf = (tid >> 6) / WPG;   // pixel group, channel group
     const int M = a.B * a.H * a.W, W = a.W, H = a.H;
     const int N = a.n;
     constexpr int cs = CS;
@@ -122,8 +128,8 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
     float* bnp = (float*)(dsm + 2 * ntmp);      // scale | shift [cs each]
     float* etab = bnp + 2 * cs;                 // scale | shift | mean | rstd [NC each]
     float* btab = etab + 4 * NC;                // bias [NC]
-    double* red = (double*)(btab + NC);         // [4 pixel groups][NC][2]
-    T* Wl = (T*)(red + 8 * NC);                 // [NC][kpl]
+    double* red = (double*)(btab + NC);         // [WPG pixel groups][NC][2]
+    T* Wl = (T*)(red + 2 * WPG * NC);           // [NC][kpl]
     T* zrow = Wl + NC * kpl;                    // [pitch] zeros
     T* act0 = zrow + pitch;                     // [2][R][pitch]
 
@@ -203,6 +209,14 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
         }
     }
     stage_store(b0, act0);
+    const T* wl = Wl + (hf * NTW * 16 + li) * KPL + g * CH;
+    u32x4 wr[WREG ? NSTEP : 1][NTW];
+    if constexpr (WREG) {
+#pragma unroll
+        for (int st = 0; st < NSTEP; ++st)
+#pragma unroll
+            for (int j = 0; j < NTW; ++j) wr[st][j] = *(const u32x4*)(wl + j * 16 * KPL + st * KS);
+    }
     __syncthreads();
     BAND_STAMP(2);
 
@@ -278,12 +292,13 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
             for (int j = 0; j < NTW; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
         // the static k-loop: step st's fragments are in registers before its
         // MFMAs, step st+1's reads issued ahead of them
-        const T* wl = Wl + (hf * NTW * 16 + li) * KPL + g * CH;
-        u32x4 wf[2][NTW], av[2][TM];
+        u32x4 wf[2][WREG ? 1 : NTW], av[2][TM];
         auto frag = [&](auto STC, int buf) {
             constexpr int st = decltype(STC)::value;
+            if constexpr (!WREG) {
 #pragma unroll
-            for (int j = 0; j < NTW; ++j) wf[buf][j] = *(const u32x4*)(wl + j * 16 * KPL + st * KS);
+                for (int j = 0; j < NTW; ++j) wf[buf][j] = *(const u32x4*)(wl + j * 16 * KPL + st * KS);
+            }
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
                 const bool ok = (tvm[i] >> tshl[st]) & 1u;
@@ -297,7 +312,10 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
-                for (int j = 0; j < NTW; ++j) Mf<T>::step(wf[st & 1][j], av[st & 1][i], acc[i][j]);
+                for (int j = 0; j < NTW; ++j) {
+                    if constexpr (WREG) Mf<T>::step(wr[st][j], av[st & 1][i], acc[i][j]);
+                    else Mf<T>::step(wf[st & 1][j], av[st & 1][i], acc[i][j]);
+                }
         });
         if ((band - b0) < 6) BAND_STAMP(3 + 2 * (band - b0));
         // epilogue: lane owns channels j*16 + 4g .. +3 of its pixels
@@ -369,7 +387,7 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
         for (int n = tid; n < N; n += NTH) {
             double t1 = 0.0, t2 = 0.0;
 #pragma unroll
-            for (int w = 0; w < 4; ++w) {
+            for (int w = 0; w < WPG; ++w) {
                 t1 += red[(w * NC + n) * 2];
                 t2 += red[(w * NC + n) * 2 + 1];
             }
@@ -380,11 +398,11 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
     BAND_STAMP(15);
 }
 
-template <typename T, int NT, int TM, int CS>
+template <typename T, int NT, int TM, int CS, int HF, bool WREG>
 int launch_band2(const rnvp_conv_args* a, hipStream_t s) {
-    using G = BandGeo<T, NT, TM>;
+    using G = BandGeo<T, NT, TM, HF>;
     const long long M = (long long)a->B * a->H * a->W;
-    const size_t shm = band2_lds_bytes<T, NT, TM>(a->cs_in, a->W);
+    const size_t shm = band2_lds_bytes<T, NT, TM, HF>(a->cs_in, a->W);
     if (shm > 160 * 1024) return RNVP_E_UNSUPPORTED;
     // every staged row of a band in SB chunks per thread, every weight chunk in WB
     const int cpr = a->cs_in / G::CH;
@@ -399,17 +417,17 @@ int launch_band2(const rnvp_conv_args* a, hipStream_t s) {
     const int nops = (a->residual ? 1 : 0) + (a->accumulate ? 1 : 0) + (a->epi_relu_bn_bwd ? 1 : 0);
     if (a->pro_bn_relu) {
         switch (nops) {
-            case 0: k_conv_band2<T, NT, TM, CS, true, 0><<<ng, 512, shm, s>>>(*a, sh, per); break;
-            case 1: k_conv_band2<T, NT, TM, CS, true, 1><<<ng, 512, shm, s>>>(*a, sh, per); break;
-            case 2: k_conv_band2<T, NT, TM, CS, true, 2><<<ng, 512, shm, s>>>(*a, sh, per); break;
+            case 0: k_conv_band2<T, NT, TM, CS, HF, WREG, true, 0><<<ng, 512, shm, s>>>(*a, sh, per); break;
+            case 1: k_conv_band2<T, NT, TM, CS, HF, WREG, true, 1><<<ng, 512, shm, s>>>(*a, sh, per); break;
+            case 2: k_conv_band2<T, NT, TM, CS, HF, WREG, true, 2><<<ng, 512, shm, s>>>(*a, sh, per); break;
             default: return RNVP_E_UNSUPPORTED;
         }
     } else {
         switch (nops) {
-            case 0: k_conv_band2<T, NT, TM, CS, false, 0><<<ng, 512, shm, s>>>(*a, sh, per); break;
-            case 1: k_conv_band2<T, NT, TM, CS, false, 1><<<ng, 512, shm, s>>>(*a, sh, per); break;
-            case 2: k_conv_band2<T, NT, TM, CS, false, 2><<<ng, 512, shm, s>>>(*a, sh, per); break;
-            default: k_conv_band2<T, NT, TM, CS, false, 3><<<ng, 512, shm, s>>>(*a, sh, per); break;
+            case 0: k_conv_band2<T, NT, TM, CS, HF, WREG, false, 0><<<ng, 512, shm, s>>>(*a, sh, per); break;
+            case 1: k_conv_band2<T, NT, TM, CS, HF, WREG, false, 1><<<ng, 512, shm, s>>>(*a, sh, per); break;
+            case 2: k_conv_band2<T, NT, TM, CS, HF, WREG, false, 2><<<ng, 512, shm, s>>>(*a, sh, per); break;
+            default: k_conv_band2<T, NT, TM, CS, HF, WREG, false, 3><<<ng, 512, shm, s>>>(*a, sh, per); break;
         }
     }
     RNVP_LAUNCH_CHECK();
@@ -420,13 +438,19 @@ template <typename T, int CS>
 int dispatch_band2_cs(const rnvp_conv_args* a, hipStream_t s) {
     const long long M = (long long)a->B * a->H * a->W;
     const long long b256 = (M + 255) / 256;
-    // 32 outputs: 256-pixel bands while that leaves >= 2 bands per
-    // workgroup; otherwise 128-pixel bands (64 outputs: registers)
+    // <= 32 outputs: every wave holds both channel tiles of its pixels and
+    // the weights in registers (k-loop LDS reads: the activation fragments
+    // only); 256-pixel bands while that leaves >= 2 bands per workgroup.
+    // 64 outputs: wave pairs split the channels, weights read from LDS per
+    // step (in registers they would take 144 VGPRs).
+    static const int tm64 = [] { const char* e = getenv("RNVP_BAND2_TM64"); return e ? atoi(e) : 2; }();
+    constexpr bool WR = CS <= 32;   // 36-72 VGPRs of weights (64 channels: 144)
     if (a->n <= 32) {
-        if (b256 >= 512) return launch_band2<T, 2, 4, CS>(a, s);
-        return launch_band2<T, 2, 2, CS>(a, s);
+        if (b256 >= 512) return launch_band2<T, 2, 2, CS, 1, WR>(a, s);
+        return launch_band2<T, 2, 1, CS, 1, WR>(a, s);
     }
-    return launch_band2<T, 4, 2, CS>(a, s);
+    if (tm64 == 4) return launch_band2<T, 4, 4, CS, 2, false>(a, s);
+    return launch_band2<T, 4, 2, CS, 2, false>(a, s);
 }
 
 template <typename T>
@@ -445,7 +469,7 @@ int dispatch_band2(const rnvp_conv_args* a, hipStream_t s) {
 // 3x3, 17..64 outputs, cs_in <= 64 with a fixed chunk column per thread,
 // 32k <= M < 2^21: the persistent band kernel (RNVP_E_UNSUPPORTED otherwise)
 int rnvp_conv_band2_launch(const rnvp_conv_args* a, hipStream_t s) {
-    static const int mode = [] { const char* e = getenv("RNVP_BAND2"); return e ? atoi(e) : 0; }();
+    static const int mode = [] { const char* e = getenv("RNVP_BAND2"); return e ? atoi(e) : 1; }();
     if (!mode) return RNVP_E_UNSUPPORTED;
     const long long M = (long long)a->B * a->H * a->W;
     if (a->ks != 3 || a->n <= 16 || a->n > 64 || a->cs_in > 64 || a->cs_out > 64) return RNVP_E_UNSUPPORTED;
