@@ -230,6 +230,51 @@ __device__ __forceinline__ void block_shard_sums(const double* sums, int C, int 
     block_shard_sums_n<1>(src);
 }
 
+// block_shard_sums split in two: shard_issue loads a thread's entries into
+// registers (first thing in a kernel, ahead of its bulk loads: vmcnt waits in
+// issue order), shard_finish folds them into s1 / s2 (LDS fp64 atomics, as
+// block_shard_sums).  Needs nc * shards <= U * blockDim.x (shard_fits).
+template <int U>
+struct ShardLoads {
+    double v1[U], v2[U];
+    int cc[U];
+};
+__device__ __forceinline__ bool shard_fits(int nc, int shards, int U) {
+    return (long long)nc * (shards < 1 ? 1 : shards) <= (long long)U * blockDim.x;
+}
+template <int U>
+__device__ __forceinline__ void shard_issue(const double* sums, int C, int shards, int c0, int nc, ShardLoads<U>& L) {
+    const int total = nc * (shards < 1 ? 1 : shards);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int t = u * blockDim.x + threadIdx.x;
+        L.cc[u] = -1;
+        L.v1[u] = L.v2[u] = 0.0;
+        if (t < total) {
+            const int c = t % nc, h = t / nc;
+            const double* p = sums + (long long)h * 2 * C + c0 + c;
+            L.v1[u] = p[0];
+            L.v2[u] = p[C];
+            L.cc[u] = c;
+        }
+    }
+}
+template <int U>
+__device__ __forceinline__ void shard_finish(const ShardLoads<U>& L, int nc, double* s1, double* s2) {
+    for (int i = threadIdx.x; i < nc; i += blockDim.x) {
+        s1[i] = 0.0;
+        s2[i] = 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        if (L.cc[u] >= 0) {
+            atomicAdd(&s1[L.cc[u]], L.v1[u]);
+            atomicAdd(&s2[L.cc[u]], L.v2[u]);
+        }
+    __syncthreads();
+}
+
 // BN table for channels [c0, c0+nc) from already-reduced sums tmp[0..nc) /
 // tmp[nc..2nc) (train) or the running stats (eval): scale/shift such that
 // bn(x) = x*scale + shift, plus mean / rstd when requested.  Channels >= C

@@ -173,8 +173,16 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
         }
     };
 
-    // ---- prologue: first band, all weights in flight; tables meanwhile ----
+    // ---- prologue: the BN tables' shard sums first (their wait then does
+    // not queue behind the bulk loads), the first band and all weights in
+    // flight behind them ----
     BAND_STAMP(0);
+    ShardLoads<2> pro_l, epi_l;
+    const int pnv = min(cs, a.cin);
+    const bool pro_pre = PRO && a.pro.sums && shard_fits(pnv, a.pro.shards, 2);
+    const bool epi_pre = epi_bn && a.epi.sums && shard_fits(min(NC, N), a.epi.shards, 2);
+    if (pro_pre) shard_issue<2>(a.pro.sums, a.cin, a.pro.shards, 0, pnv, pro_l);
+    if (epi_pre) shard_issue<2>(a.epi.sums, N, a.epi.shards, 0, min(NC, N), epi_l);
     stage_load(b0);
     const T* Wg = (const T*)a.w;
     constexpr int wcpr = KPL / CH, wtot = NC * wcpr, kv = NSTEP * KS;
@@ -187,8 +195,22 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
         wv[u] = *(const u32x4*)(Wg + (ok ? (long long)r * a.kp + c * CH : 0));
         if (!ok) wv[u] = u32x4{0u, 0u, 0u, 0u};
     }
-    if (PRO) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + cs, nullptr, nullptr, tmp);
-    if (epi_bn) block_bn_table(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp);
+    if (PRO) {
+        if (pro_pre) {
+            shard_finish<2>(pro_l, cs, tmp, tmp + cs);   // channels >= pnv stay zero (block_bn_finish pads them)
+            block_bn_finish(a.pro, a.cin, 0, cs, bnp, bnp + cs, nullptr, nullptr, tmp);
+        } else {
+            block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + cs, nullptr, nullptr, tmp);
+        }
+    }
+    if (epi_bn) {
+        if (epi_pre) {
+            shard_finish<2>(epi_l, NC, tmp, tmp + NC);
+            block_bn_finish(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp);
+        } else {
+            block_bn_table(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp);
+        }
+    }
 #pragma unroll
     for (int u = 0; u < WB; ++u) {
         const int q = u * NTH + tid;
