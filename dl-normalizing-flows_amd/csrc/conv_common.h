@@ -245,9 +245,16 @@ __device__ __forceinline__ void bn_bwd_body(const rnvp_bn_bwd_args& a, double* d
     const int cpr = cs / CH;
     const long long nch = a.M * cpr;
     const long long q0 = blk * (long long)blockDim.x + threadIdx.x, qs = (long long)nblk * blockDim.x;
-    // the first chunk's operands are loaded before the tables (their memory
-    // round trip overlaps the shard reductions'; at the deep scales that
-    // first chunk is a thread's whole share)
+    // the tables' shard sums are loaded first, then the first chunk's
+    // operands (vmcnt completes in issue order: the tables wait for their own
+    // loads only, the chunk's round trip overlaps theirs; at the deep scales
+    // that first chunk is a thread's whole share)
+    ShardLoads<4> gl, bl;
+    const bool spre = a.sums && shard_fits(C, a.sum_shards, 4) && (!a.bn.sums || shard_fits(C, a.bn.shards, 4));
+    if (spre) {
+        shard_issue<4>(a.sums, C, a.sum_shards, 0, C, gl);
+        if (a.bn.sums) shard_issue<4>(a.bn.sums, C, a.bn.shards, 0, C, bl);
+    }
     u32x4 pg = u32x4{0u, 0u, 0u, 0u}, px = pg, pr = pg, pa = pg;
     if (q0 < nch) {
         const long long o = q0 * CH;
@@ -256,7 +263,11 @@ __device__ __forceinline__ void bn_bwd_body(const rnvp_bn_bwd_args& a, double* d
         if (R) pr = *(const u32x4*)(R + o);
         if (a.accumulate) pa = *(const u32x4*)(DX + o);
     }
-    {   // both shard reductions (forward BN stats, backward g-sums) in one pass
+    if (spre) {
+        shard_finish<4>(gl, C, gs, gs + cs);
+        if (a.bn.sums) shard_finish<4>(bl, C, dsm, dsm + cs);
+        block_bn_finish(a.bn, C, 0, cs, t_sc, t_sc + cs, t_sc + 2 * cs, t_sc + 3 * cs, dsm);
+    } else {   // both shard reductions (forward BN stats, backward g-sums) in one pass
         if (a.bn.sums) {
             const ShardSrc src[2] = {{a.sums, C, a.sum_shards, 0, C, gs, gs + cs},
                                      {a.bn.sums, C, a.bn.shards, 0, C, dsm, dsm + cs}};

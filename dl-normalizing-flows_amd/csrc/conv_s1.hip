@@ -40,6 +40,15 @@ __global__ __launch_bounds__(256, (s1_min_blocks<NT, NKS, NOPS>())) void k_conv_
     const bool pro = a.pro_bn_relu != 0, epi_bn = a.epi_relu_bn_bwd != 0;
     const bool has_acc = a.accumulate != 0;
 
+    // the BN tables' shard sums first: their wait does not queue behind the
+    // weight and tile loads (vmcnt completes in issue order)
+    ShardLoads<4> pro_l, epi_l;
+    const int pnv = min(cs, a.cin);
+    const bool pro_pre = pro && a.pro.sums && shard_fits(pnv, a.pro.shards, 4);
+    const bool epi_pre = epi_bn && a.epi.sums && shard_fits(min(NC, N), a.epi.shards, 4);
+    if (pro_pre) shard_issue<4>(a.pro.sums, a.cin, a.pro.shards, 0, pnv, pro_l);
+    if (epi_pre) shard_issue<4>(a.epi.sums, N, a.epi.shards, 0, min(NC, N), epi_l);
+
     // ---- per-lane constants: weights, prologue coefficients, bias ----
     const bf16_t* __restrict__ Wg = (const bf16_t*)a.w;
     u32x4 wv[NKS][NT];
@@ -208,8 +217,22 @@ __global__ __launch_bounds__(256, (s1_min_blocks<NT, NKS, NOPS>())) void k_conv_
 
     // ---- tables (every thread: block-wide reductions), their loads in flight
     // behind the weights and the first tile's ----
-    if (pro) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + 64, nullptr, nullptr, tmp);
-    if (epi_bn) block_bn_table(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp);
+    if (pro) {
+        if (pro_pre) {
+            shard_finish<4>(pro_l, cs, tmp, tmp + cs);
+            block_bn_finish(a.pro, a.cin, 0, cs, bnp, bnp + 64, nullptr, nullptr, tmp);
+        } else {
+            block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + 64, nullptr, nullptr, tmp);
+        }
+    }
+    if (epi_bn) {
+        if (epi_pre) {
+            shard_finish<4>(epi_l, NC, tmp, tmp + NC);
+            block_bn_finish(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp);
+        } else {
+            block_bn_table(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp);
+        }
+    }
     __syncthreads();
 
     while (t < ntiles) {

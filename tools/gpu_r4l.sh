@@ -1,0 +1,15 @@
+#!/bin/bash
+# round 4 GPU call: 1x1 stream kernel with the BN-table shard loads first
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/${TAG:-r4l}
+mkdir -p $O
+step() { local log=$1; shift; "$@" > $O/$log 2>&1; local rc=$?; echo "$log rc=$rc"; tail -${TAILN:-4} $O/$log; if [ $rc -ne 0 ]; then exit $rc; fi; }
+soft() { local log=$1; shift; "$@" > $O/$log 2>&1; local rc=$?; echo "$log rc=$rc"; tail -${TAILN:-4} $O/$log; if [ $rc -ge 124 ]; then exit $rc; fi; }
+TAILN=20 soft pytest_conv.log timeout -k 10 600 python -u -m pytest tests/test_gpu_conv.py tests/test_gpu_group.py -m gpu -q -rf --timeout 300 --timeout-method thread
+TAILN=14 step mb.txt timeout -k 10 300 python3 -u tools/conv_microbench.py --case=1x1
+step ab.log env STEPS=30 VARIANTS='||' TAG=${TAG:-r4l}/ab bash tools/gpu_ab.sh
+step prof.log timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-secondary
+f=$(find $O/prof -name '*kernel_trace.csv' | head -1)
+TAILN=70 step step.txt python3 tools/step_dump.py $f
+rm -f $f
