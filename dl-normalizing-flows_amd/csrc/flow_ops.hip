@@ -412,8 +412,10 @@ __global__ void k_adam(float4* __restrict__ p, const float4* __restrict__ g, flo
     }
     __syncthreads();
     const float step_size = sh[0], inv_bc2s = sh[1];
-    auto upd = [&](float4& pp, const float4& gg, float4& mm, float4& vv, uint32_t mk) {
-        float* pa = (float*)&pp; const float* ga = (const float*)&gg; float* ma = (float*)&mm; float* va = (float*)&vv;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+        float4 pp = p[i], gg = g[i], mm = m[i], vv = v[i];
+        const uint32_t mk = regm ? regm[i] : 0x01010101u;
+        float* pa = (float*)&pp; float* ga = (float*)&gg; float* ma = (float*)&mm; float* va = (float*)&vv;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t f = (mk >> (8 * j)) & 0xff;
@@ -425,24 +427,6 @@ __global__ void k_adam(float4* __restrict__ p, const float4* __restrict__ g, flo
             float den = sqrtf(va[j]) * inv_bc2s + eps;
             pa[j] = pa[j] - step_size * ma[j] / den;
         }
-    };
-    // two elements per thread and trip, all eight 16-B loads issued before
-    // either update (twice the bytes in flight of the one-element loop)
-    const long long stride = (long long)gridDim.x * blockDim.x;
-    long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    for (; i + stride < n4; i += 2 * stride) {
-        const long long k = i + stride;
-        float4 p0 = p[i], g0 = g[i], m0 = m[i], v0 = v[i];
-        float4 p1 = p[k], g1 = g[k], m1 = m[k], v1 = v[k];
-        const uint32_t k0 = regm ? regm[i] : 0x01010101u, k1 = regm ? regm[k] : 0x01010101u;
-        upd(p0, g0, m0, v0, k0);
-        upd(p1, g1, m1, v1, k1);
-        p[i] = p0; m[i] = m0; v[i] = v0;
-        p[k] = p1; m[k] = m1; v[k] = v1;
-    }
-    if (i < n4) {
-        float4 pp = p[i], gg = g[i], mm = m[i], vv = v[i];
-        upd(pp, gg, mm, vv, regm ? regm[i] : 0x01010101u);
         p[i] = pp; m[i] = mm; v[i] = vv;
     }
 }

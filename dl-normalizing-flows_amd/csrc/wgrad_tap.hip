@@ -54,25 +54,43 @@ inline int wt_class_base(int ks, int cs_in, int cs_dy) {
 __host__ __device__ inline int wt_tco(int c) { return c == 1 ? 128 : (c == 2 ? 32 : 64); }
 __host__ __device__ inline int wt_tci(int c) { return c == 1 ? 128 : (c == 2 ? 32 : 64); }
 __host__ __device__ inline int wt_ks(int c) { return (c == 0 || c == 2) ? 3 : 1; }
-__host__ __device__ inline int wt_pitch(int t) { return t * 2 + 16; }            // bytes per LDS row
+// bytes per LDS row.  KO (the consecutive-row k order, wt_krow): an odd
+// number of 32-byte granules, so that the 8 consecutive rows one
+// ds_read_b64_tr_b16 half-wave reads land in 8 distinct 32-byte bank groups
+// for any starting row; otherwise (the identity order, when the wider rows do
+// not fit LDS) +16 B
+__host__ __device__ inline int wt_pitch(int t, bool ko) { return t * 2 + (ko ? 32 : 16); }
 // padded rows a stage of rs output rows can touch (image boundaries add 2 each)
 __host__ __device__ inline int wt_npr(int rs, int H) { return rs + 2 + 2 * ((rs - 1 + H - 1) / H); }
 
-__host__ __device__ inline size_t wt_stage_bytes(int c, int H, int W) {
+__host__ __device__ inline size_t wt_stage_bytes(int c, int H, int W, bool ko) {
     const int tco = wt_tco(c), tci = wt_tci(c);
-    const size_t dy = (size_t)WT_SP * wt_pitch(tco);
+    const size_t dy = (size_t)WT_SP * wt_pitch(tco, ko);
     size_t x;
-    if (wt_ks(c) == 1) x = (size_t)WT_SP * wt_pitch(tci);
-    else x = (size_t)wt_npr(WT_SP / W, H) * (W + 2) * wt_pitch(tci);
+    if (wt_ks(c) == 1) x = (size_t)WT_SP * wt_pitch(tci, ko);
+    else x = (size_t)wt_npr(WT_SP / W, H) * (W + 2) * wt_pitch(tci, ko);
     return dy + x;
 }
-__host__ __device__ inline size_t wt_lds_bytes(int c, int H, int W) {
-    return 2 * wt_stage_bytes(c, H, W) + 24 * (size_t)wt_tci(c);   // 2 stages + BN table + fp64 scratch
+__host__ __device__ inline size_t wt_lds_bytes(int c, int H, int W, bool ko) {
+    return 2 * wt_stage_bytes(c, H, W, ko) + 24 * (size_t)wt_tci(c);   // 2 stages + BN table + fp64 scratch
 }
 
+// the k -> pixel order of one 32-pixel k-step: lane group gq's B/A fragment
+// takes k = 8gq .. 8gq+7 as two transposed 4-row reads (lo, hi); k is any
+// permutation of the step's pixels as long as both operands use the same one.
+// KO: a half-wave's lo read covers 8 CONSECUTIVE pixel rows (pixels
+// 16*(gq/2) + 4*(gq%2) + 0..3) and its hi read the next 8 (+8) -- with an odd
+// granule pitch (wt_pitch) every read is bank-conflict-free; the identity
+// order (rows r..r+3 and r+8..r+11 per half-wave) is 2-way on any linear pitch
+template <bool KO>
+__device__ __forceinline__ int wt_krow(int gq, int qq) { return KO ? 16 * (gq >> 1) + 4 * (gq & 1) + qq : 8 * gq + qq; }
+template <bool KO>
+constexpr int wt_khi() { return KO ? 8 : 4; }   // rows from a lane's lo read to its hi read
+
+template <bool KO>
 __device__ __forceinline__ u32x4 tr_pair(const char* base, int pitch) {
     const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)base);
-    const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)(base + 4 * pitch));
+    const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)(base + wt_khi<KO>() * pitch));
     const uint2 l = __builtin_bit_cast(uint2, lo), h = __builtin_bit_cast(uint2, hi);
     return u32x4{l.x, l.y, h.x, h.y};
 }
@@ -86,14 +104,14 @@ struct WtConv {
     long long m_per_slab;
 };
 
-template <int CLS>
+template <int CLS, bool KO>
 __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int z, char* lds) {
     using Cfg = WtCfg<CLS>;
     constexpr int TCO = Cfg::TCO, TCI = Cfg::TCI, KS = Cfg::KS, T = KS * KS;
     constexpr int WCO = Cfg::WCO, WCI = Cfg::WCI, WTG = Cfg::WTG, NX = Cfg::NX, DEPTH = Cfg::DEPTH;
     constexpr int FCO = TCO / (16 * WCO), FCI = TCI / (16 * WCI);
     constexpr int TPW = (T + WTG - 1) / WTG;                    // taps per wave
-    constexpr int DP = TCO * 2 + 16, XP = TCI * 2 + 16;         // LDS row pitches (bytes)
+    constexpr int DP = TCO * 2 + (KO ? 32 : 16), XP = TCI * 2 + (KO ? 32 : 16);   // LDS row pitches (bytes, wt_pitch)
     constexpr int CPO = TCO / 8, CPI = TCI / 8;                 // 16-byte chunks per row
     constexpr int NDY = WT_SP * CPO / WT_NT;
     static_assert(WCO * WCI * WTG * 64 == WT_NT, "wave layout");
@@ -114,7 +132,7 @@ __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int 
     const int NPR = KS == 3 ? wt_npr(RS, H) : 0;
     const int xrows = KS == 3 ? NPR * PW : WT_SP;               // staged x positions per stage
     const int xtot = xrows * CPI;                               // x chunks per stage
-    const size_t sbytes = wt_stage_bytes(CLS, H, W);
+    const size_t sbytes = wt_stage_bytes(CLS, H, W, KO);
     float* bnp = (float*)(lds + 2 * sbytes);                    // scale [TCI] | shift [TCI] | fp64 scratch [2 TCI]
     const bool pro = cv.pro_bn_relu != 0;
 
@@ -252,8 +270,8 @@ __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int 
         if constexpr (KS == 1) {
 #pragma unroll
             for (int kk = 0; kk < WT_KST; ++kk) {
-                plo[kk] = kk * 32 + 8 * gq + qq;
-                phi[kk] = plo[kk] + 4;
+                plo[kk] = kk * 32 + wt_krow<KO>(gq, qq);
+                phi[kk] = plo[kk] + wt_khi<KO>();
             }
         } else {
             // pixel j of the stage: output row o0 + j / W, column j % W; its
@@ -267,17 +285,17 @@ __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int 
             };
 #pragma unroll
             for (int kk = 0; kk < WT_KST; ++kk) {
-                plo[kk] = posof(kk * 32 + 8 * gq + qq);
-                phi[kk] = posof(kk * 32 + 8 * gq + qq + 4);
+                plo[kk] = posof(kk * 32 + wt_krow<KO>(gq, qq));
+                phi[kk] = posof(kk * 32 + wt_krow<KO>(gq, qq) + wt_khi<KO>());
             }
         }
 #pragma unroll
         for (int kk = 0; kk < WT_KST; ++kk) {
-            const int jl = kk * 32 + 8 * gq + qq;                 // dy pixel rows of this lane (lo; hi = +4)
+            const int jl = kk * 32 + wt_krow<KO>(gq, qq);         // dy pixel rows of this lane (lo; hi = + wt_khi)
             u32x4 af[FCO];
 #pragma unroll
             for (int a = 0; a < FCO; ++a)
-                af[a] = tr_pair(dyL + jl * DP + (wco * FCO * 16 + a * 16 + 4 * pp) * 2, DP);
+                af[a] = tr_pair<KO>(dyL + jl * DP + (wco * FCO * 16 + a * 16 + 4 * pp) * 2, DP);
             auto bfrag = [&](int b, int t) {
                 const int col = (wci * FCI * 16 + b * 16 + 4 * pp) * 2;
                 const i16x4 lo =
@@ -385,7 +403,7 @@ __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int 
 // tile class (every conv of the launch has class CLS): each class gets its
 // own register allocation (the 1x1 classes fit more waves per SIMD than the
 // 3x3 ones; one kernel over all classes took the largest class's 207 VGPRs)
-template <int CLS>
+template <int CLS, bool KO>
 __global__ __launch_bounds__(WT_NT) void k_wgrad_tap(rnvp_wgrad_group g) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int nb = gridDim.x, b = blockIdx.x;
@@ -403,24 +421,25 @@ __global__ __launch_bounds__(WT_NT) void k_wgrad_tap(rnvp_wgrad_group g) {
     const int z = local / per, rr = local - z * per;
     const int cot = rr / tci, cit = rr - cot * tci;
     if constexpr (CLS >= 0) {
-        wt_body<CLS>(cv, cot, cit, z, lds);
+        wt_body<CLS, KO>(cv, cot, cit, z, lds);
     } else {
         switch (cls) {
-            case 0: wt_body<0>(cv, cot, cit, z, lds); break;
-            case 1: wt_body<1>(cv, cot, cit, z, lds); break;
-            case 2: wt_body<2>(cv, cot, cit, z, lds); break;
-            default: wt_body<3>(cv, cot, cit, z, lds); break;
+            case 0: wt_body<0, KO>(cv, cot, cit, z, lds); break;
+            case 1: wt_body<1, KO>(cv, cot, cit, z, lds); break;
+            case 2: wt_body<2, KO>(cv, cot, cit, z, lds); break;
+            default: wt_body<3, KO>(cv, cot, cit, z, lds); break;
         }
     }
 }
 
 using WtKernel = void (*)(rnvp_wgrad_group);
-WtKernel wt_kernel(int cls) {
+WtKernel wt_kernel(int cls, bool ko) {
     switch (cls) {
-        case 0: return k_wgrad_tap<0>;
-        case 1: return k_wgrad_tap<1>;
-        case 2: return k_wgrad_tap<2>;
-        default: return k_wgrad_tap<3>;
+        case 0: return ko ? k_wgrad_tap<0, true> : k_wgrad_tap<0, false>;
+        case 1: return ko ? k_wgrad_tap<1, true> : k_wgrad_tap<1, false>;
+        case 2: return ko ? k_wgrad_tap<2, true> : k_wgrad_tap<2, false>;
+        case 3: return ko ? k_wgrad_tap<3, true> : k_wgrad_tap<3, false>;
+        default: return ko ? k_wgrad_tap<-1, true> : k_wgrad_tap<-1, false>;
     }
 }
 
@@ -448,7 +467,7 @@ int wt_class(const rnvp_wgrad_conv& v, int H, int W) {
     if (policy == 0) return c;
     const int small = v.ks == 3 ? 2 : 3;
     if (c != small && wt_tasks(v, c) < 256 && wt_stage_fits(small, H, W) &&
-        wt_lds_bytes(small, H, W) <= 160 * 1024)
+        wt_lds_bytes(small, H, W, false) <= 160 * 1024)
         return small;
     return c;
 }
@@ -470,7 +489,7 @@ int rnvp_wgrad_tap_launch(rnvp_wgrad_group* g, hipStream_t s) {
         // 32-bit buffer offsets (bytes)
         if (M * v.cs_in * 2 >= (1ll << 31) || M * v.cs_dy * 2 >= (1ll << 31)) return RNVP_E_UNSUPPORTED;
         const int cls = wt_class(v, H, W);
-        if (wt_lds_bytes(cls, H, W) > 160 * 1024 || !wt_stage_fits(cls, H, W)) return RNVP_E_UNSUPPORTED;
+        if (wt_lds_bytes(cls, H, W, false) > 160 * 1024 || !wt_stage_fits(cls, H, W)) return RNVP_E_UNSUPPORTED;
         // slabs of whole stages; the slab count must stay v.nz (the replica
         // workspace and the weight-norm backward are sized by it)
         const long long stages = (M + WT_SP - 1) / WT_SP;
@@ -487,6 +506,11 @@ int rnvp_wgrad_tap_launch(rnvp_wgrad_group* g, hipStream_t s) {
     // measured 0.3 ms/step slower (profiles/r4_wgrad_split.txt);
     // RNVP_WT_SPLIT=1 keeps that variant for A/B.
     static const int split = [] { const char* e = getenv("RNVP_WT_SPLIT"); return e ? atoi(e) : 0; }();
+    // the conflict-free k order where every conv's wider rows fit LDS
+    // (RNVP_WT_KO=0: the identity order everywhere)
+    static const int ko_env = [] { const char* e = getenv("RNVP_WT_KO"); return e ? atoi(e) : 1; }();
+    bool ko = ko_env != 0;
+    for (int c = 0; c < g->n_conv; ++c) ko = ko && wt_lds_bytes(g->conv[c].cls, H, W, true) <= 160 * 1024;
     bool one_class = true;
     for (int c = 1; c < g->n_conv; ++c) one_class = one_class && g->conv[c].cls == g->conv[0].cls;
     if (!split || one_class) {
@@ -496,13 +520,10 @@ int rnvp_wgrad_tap_launch(rnvp_wgrad_group* g, hipStream_t s) {
             rnvp_wgrad_conv& v = g->conv[c];
             v.task0 = (int)tasks;
             tasks += wt_tasks(v, v.cls);
-            shm = wt_lds_bytes(v.cls, H, W) > shm ? wt_lds_bytes(v.cls, H, W) : shm;
+            shm = wt_lds_bytes(v.cls, H, W, ko) > shm ? wt_lds_bytes(v.cls, H, W, ko) : shm;
         }
         if (tasks > (1ll << 30)) return RNVP_E_INVALID;
-        if (one_class)
-            hipLaunchKernelGGL(wt_kernel(g->conv[0].cls), dim3((unsigned)tasks), dim3(WT_NT), shm, s, *g);
-        else
-            k_wgrad_tap<-1><<<(unsigned)tasks, WT_NT, shm, s>>>(*g);
+        hipLaunchKernelGGL(wt_kernel(one_class ? g->conv[0].cls : -1, ko), dim3((unsigned)tasks), dim3(WT_NT), shm, s, *g);
         RNVP_LAUNCH_CHECK();
         return RNVP_OK;
     }
@@ -519,7 +540,7 @@ int rnvp_wgrad_tap_launch(rnvp_wgrad_group* g, hipStream_t s) {
         }
         if (sub.n_conv == 0) continue;
         if (tasks > (1ll << 30)) return RNVP_E_INVALID;
-        hipLaunchKernelGGL(wt_kernel(cls), dim3((unsigned)tasks), dim3(WT_NT), wt_lds_bytes(cls, H, W), s, sub);
+        hipLaunchKernelGGL(wt_kernel(cls, ko), dim3((unsigned)tasks), dim3(WT_NT), wt_lds_bytes(cls, H, W, ko), s, sub);
         RNVP_LAUNCH_CHECK();
     }
     return RNVP_OK;
