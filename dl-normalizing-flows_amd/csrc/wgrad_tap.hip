@@ -129,7 +129,16 @@ __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int 
     const int ns = mb < me ? (int)((me - mb + WT_SP - 1) / WT_SP) : 0;
     const int PW = KS == 3 ? W + 2 : 0;
     const int RS = WT_SP / W;                                   // output rows per stage (launcher: W | 128)
-    const int NPR = KS == 3 ? wt_npr(RS, H) : 0;
+    // stage alignment (uniform; 3x3 classes): 1 = every stage lies inside one
+    // image (H*W % WT_SP == 0), 2 = every stage is whole images (WT_SP %
+    // H*W == 0), 0 = general.  Aligned stages have one padded layout: a
+    // chunk's pixel offset from the stage start and its column validity are
+    // stage-invariant (computed once below), and so are the lanes' LDS
+    // positions in compute(); they also stage exactly the rows they read (RS
+    // + 2 per image), wt_npr's bound covers any stage
+    const int HWi = H * W;
+    const int al = KS == 3 ? (HWi % WT_SP == 0 ? 1 : (WT_SP % HWi == 0 ? 2 : 0)) : 0;
+    const int NPR = KS == 3 ? (al == 1 ? RS + 2 : (al == 2 ? RS + 2 * (RS / H) : wt_npr(RS, H))) : 0;
     const int xrows = KS == 3 ? NPR * PW : WT_SP;               // staged x positions per stage
     const int xtot = xrows * CPI;                               // x chunks per stage
     const size_t sbytes = wt_stage_bytes(CLS, H, W, KO);
@@ -174,6 +183,26 @@ __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int 
         }
     }
 
+    int xrel[NX], xrow[NX];
+    unsigned xinv = 0;                                          // al 1: column ok; al 2: slot holds a pixel
+    if constexpr (KS == 3) {
+#pragma unroll
+        for (int u = 0; u < NX; ++u) {
+            const int j = xjp[u] >> 8, pc = xjp[u] & 255;
+            const bool colok = (xjp[u] >= 0) & (pc >= 1) & (pc <= W) & xcol_ok;
+            if (al == 1) {
+                xrel[u] = (j - 1) * W + pc - 1;
+                xrow[u] = j - 1;                                // image row = stage's first row + xrow
+                xinv |= (unsigned)colok << u;
+            } else {
+                const int bb = fdiv_small(j, rH2), yy = j - bb * (H + 2) - 1;
+                xrel[u] = (bb * H + yy) * W + pc - 1;
+                xrow[u] = 0;
+                xinv |= (unsigned)(colok & (yy >= 0) & (yy < H)) << u;
+            }
+        }
+    }
+
     // global loads of stage s into register slot SL
     auto gload = [&](int s, auto SLC) {
         constexpr int SL = decltype(SLC)::value;
@@ -191,6 +220,18 @@ __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int 
                 const int p = p0 + xjp[u];
                 const bool ok = (xjp[u] >= 0) & (p < me) & xcol_ok;
                 rx[SL][u] = __builtin_amdgcn_raw_buffer_load_b128(XR, ok ? (p * cs + ci0 + cch * 8) * 2 : OOB, 0, 0);
+                m |= (unsigned)ok << u;
+            }
+        } else if (al) {
+            // aligned stages: p0 + the chunk's invariant offset; al 1 also
+            // checks the row against the image (first / last stage of an image)
+            const int om = (p0 / W) % H;
+#pragma unroll
+            for (int u = 0; u < NX; ++u) {
+                const bool rowok = al == 2 || (unsigned)(om + xrow[u]) < (unsigned)H;
+                const bool ok = ((xinv >> u) & 1u) & rowok & (p0 + xrel[u] < me);
+                rx[SL][u] = __builtin_amdgcn_raw_buffer_load_b128(XR, ok ? ((p0 + xrel[u]) * cs + ci0 + cch * 8) * 2 : OOB,
+                                                                  0, 0);
                 m |= (unsigned)ok << u;
             }
         } else {
@@ -261,12 +302,11 @@ __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int 
         toff[t] = KS == 3 ? ((tap / 3 - 1) * PW + (tap % 3 - 1)) : 0;
     }
 
-    // MFMAs of the stage in LDS buffer cur (stage s)
-    auto compute = [&](int s, int cur) {
-        const char* dyL = lds + (size_t)cur * sbytes;
-        const char* xL = dyL + (size_t)WT_SP * DP;
-        // this lane's LDS x positions (pixel rows lo = jl, hi = jl + 4) per k-step
-        int plo[WT_KST], phi[WT_KST];
+    // this lane's LDS x positions (pixel rows lo, hi = lo + wt_khi) per k-step
+    // of a stage whose first output row is o0: pixel j sits in output row
+    // o0 + j / W, column j % W; its slot = rows since o0 + 2 per image
+    // boundary crossed + 1 (aligned stages: the same for every stage)
+    auto positions = [&](int o0, int* plo, int* phi) {
         if constexpr (KS == 1) {
 #pragma unroll
             for (int kk = 0; kk < WT_KST; ++kk) {
@@ -274,9 +314,6 @@ __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int 
                 phi[kk] = plo[kk] + wt_khi<KO>();
             }
         } else {
-            // pixel j of the stage: output row o0 + j / W, column j % W; its
-            // slot = rows since o0 + 2 per image boundary crossed + 1
-            const int o0 = (int)((mb + (long long)s * WT_SP) / W);
             const int ob0 = fdiv_small(o0, rH);
             auto posof = [&](int j) {
                 const int jr = fdiv_small(j, rW), xx = j - jr * W;
@@ -288,6 +325,24 @@ __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int 
                 plo[kk] = posof(kk * 32 + wt_krow<KO>(gq, qq));
                 phi[kk] = posof(kk * 32 + wt_krow<KO>(gq, qq) + wt_khi<KO>());
             }
+        }
+    };
+    int plo_a[WT_KST], phi_a[WT_KST];
+    positions(0, plo_a, phi_a);   // aligned (al != 0) and 1x1 stages
+
+    // MFMAs of the stage in LDS buffer cur (stage s)
+    auto compute = [&](int s, int cur) {
+        const char* dyL = lds + (size_t)cur * sbytes;
+        const char* xL = dyL + (size_t)WT_SP * DP;
+        int plo[WT_KST], phi[WT_KST];
+        if (KS == 1 || al) {
+#pragma unroll
+            for (int kk = 0; kk < WT_KST; ++kk) {
+                plo[kk] = plo_a[kk];
+                phi[kk] = phi_a[kk];
+            }
+        } else {
+            positions((int)((mb + (long long)s * WT_SP) / W), plo, phi);
         }
 #pragma unroll
         for (int kk = 0; kk < WT_KST; ++kk) {
