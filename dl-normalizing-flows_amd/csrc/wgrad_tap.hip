@@ -88,7 +88,7 @@ template <bool KO>
 constexpr int wt_khi() { return KO ? 8 : 4; }   // rows from a lane's lo read to its hi read
 
 template <bool KO>
-__device__ __forceinline__ u32x4 tr_pair(const char* base, int pitch) {
+__device__ __forceinline__ u32x4 tr_pair(const RNVP_LDS char* base, int pitch) {
     const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)base);
     const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)(base + wt_khi<KO>() * pitch));
     const uint2 l = __builtin_bit_cast(uint2, lo), h = __builtin_bit_cast(uint2, hi);
@@ -141,8 +141,11 @@ __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int 
     const int NPR = KS == 3 ? (al == 1 ? RS + 2 : (al == 2 ? RS + 2 * (RS / H) : wt_npr(RS, H))) : 0;
     const int xrows = KS == 3 ? NPR * PW : WT_SP;               // staged x positions per stage
     const int xtot = xrows * CPI;                               // x chunks per stage
-    const size_t sbytes = wt_stage_bytes(CLS, H, W, KO);
+    const unsigned sbytes = (unsigned)wt_stage_bytes(CLS, H, W, KO);
     float* bnp = (float*)(lds + 2 * sbytes);                    // scale [TCI] | shift [TCI] | fp64 scratch [2 TCI]
+    // LDS-space base: stage addresses in 32-bit arithmetic (generic-pointer
+    // offsets compiled to 64-bit multiply-adds per operand read)
+    RNVP_LDS char* const L3 = (RNVP_LDS char*)lds;
     const bool pro = cv.pro_bn_relu != 0;
 
     // ---- BN+ReLU table of this ci tile (channels >= cin: scale = shift = 0) ----
@@ -257,12 +260,12 @@ __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int 
     // transform + store of register slot SL into LDS buffer buf
     auto lstore = [&](int buf, auto SLC) {
         constexpr int SL = decltype(SLC)::value;
-        char* dyL = lds + (size_t)buf * sbytes;
-        char* xL = dyL + (size_t)WT_SP * DP;
+        RNVP_LDS char* dyL = L3 + buf * sbytes;
+        RNVP_LDS char* xL = dyL + WT_SP * DP;
 #pragma unroll
         for (int u = 0; u < NDY; ++u) {
             const int r = (tid + u * WT_NT) / CPO;
-            *(u32x4*)(dyL + r * DP + dch * 16) = rd[SL][u];
+            *(RNVP_LDS u32x4*)(dyL + r * DP + dch * 16) = rd[SL][u];
         }
 #pragma unroll
         for (int u = 0; u < NX; ++u) {
@@ -278,7 +281,7 @@ __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int 
                 const uint32_t k = ((xm[SL] >> u) & 1u) ? ~0u : 0u;
                 v &= u32x4{k, k, k, k};
             }
-            *(u32x4*)(xL + pos * XP + cch * 16) = v;
+            *(RNVP_LDS u32x4*)(xL + pos * XP + cch * 16) = v;
         }
     };
 
@@ -332,8 +335,8 @@ __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int 
 
     // MFMAs of the stage in LDS buffer cur (stage s)
     auto compute = [&](int s, int cur) {
-        const char* dyL = lds + (size_t)cur * sbytes;
-        const char* xL = dyL + (size_t)WT_SP * DP;
+        const RNVP_LDS char* dyL = L3 + cur * sbytes;
+        const RNVP_LDS char* xL = dyL + WT_SP * DP;
         int plo[WT_KST], phi[WT_KST];
         if (KS == 1 || al) {
 #pragma unroll
@@ -351,12 +354,13 @@ __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int 
 #pragma unroll
             for (int a = 0; a < FCO; ++a)
                 af[a] = tr_pair<KO>(dyL + jl * DP + (wco * FCO * 16 + a * 16 + 4 * pp) * 2, DP);
+            // per k-step lane bases; taps add a uniform offset
+            const RNVP_LDS char* xlo = xL + plo[kk] * XP + (wci * FCI * 16 + 4 * pp) * 2;
+            const RNVP_LDS char* xhi = xL + phi[kk] * XP + (wci * FCI * 16 + 4 * pp) * 2;
             auto bfrag = [&](int b, int t) {
-                const int col = (wci * FCI * 16 + b * 16 + 4 * pp) * 2;
-                const i16x4 lo =
-                    __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)(xL + (plo[kk] + toff[t]) * XP + col));
-                const i16x4 hi =
-                    __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)(xL + (phi[kk] + toff[t]) * XP + col));
+                const int off = toff[t] * XP + b * 32;
+                const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)(xlo + off));
+                const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((RNVP_LDS i16x4*)(xhi + off));
                 const uint2 l = __builtin_bit_cast(uint2, lo), h = __builtin_bit_cast(uint2, hi);
                 return u32x4{l.x, l.y, h.x, h.y};
             };
