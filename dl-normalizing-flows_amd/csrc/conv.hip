@@ -967,11 +967,15 @@ __global__ __launch_bounds__(256 * NH) void k_conv_band(rnvp_conv_args a, int sh
             const int p = m0 - hal + r;
             u32x4 w = sv[u];
             if (PRO) {
-                float f[CH];
-                unpack(w, f, T());
+                if constexpr (sizeof(T) == 2) {
+                    w = bn_relu_bf16x8(w, scv, shv);
+                } else {
+                    float f[CH];
+                    unpack(w, f, T());
 #pragma unroll
-                for (int e = 0; e < CH; ++e) f[e] = fmaxf(f[e] * scv[e] + shv[e], 0.f);
-                w = pack(f, T());
+                    for (int e = 0; e < CH; ++e) f[e] = fmaxf(f[e] * scv[e] + shv[e], 0.f);
+                    w = pack(f, T());
+                }
             }
             const uint32_t keep = (p >= 0 && p < M) ? ~0u : 0u;
             *(u32x4*)(act + r * pitch + cfix * CH) = w & u32x4{keep, keep, keep, keep};

@@ -130,6 +130,27 @@ __device__ __forceinline__ void epi4p(const rnvp_conv_args& a, long long o, cons
     st4((T*)a.y + o, v);
 }
 
+// BN+ReLU of 8 bf16 channels (one 16-B chunk), scale / shift per channel:
+// packed fp32 FMAs, the bf16 rounding, then ReLU as a packed signed-16-bit
+// max against 0 on the rounded pair (a bf16 with its sign bit set is a
+// negative int16; relu commutes with the monotone rounding, so the bits equal
+// rounding max(x*sc+sh, 0)).  20 VALU per chunk instead of 28.
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef short i16x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u32x4 bn_relu_bf16x8(const u32x4& c, const float* sc, const float* sh) {
+    const uint32_t w[4] = {c.x, c.y, c.z, c.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const f32x2_t x = {__uint_as_float(w[i] << 16), __uint_as_float(w[i] & 0xffff0000u)};
+        const f32x2_t y = __builtin_elementwise_fma(x, f32x2_t{sc[2 * i], sc[2 * i + 1]}, f32x2_t{sh[2 * i], sh[2 * i + 1]});
+        const uint32_t p = __builtin_bit_cast(uint32_t, __builtin_convertvector(y, bf16x2_t));
+        o[i] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(i16x2_t, p), i16x2_t{0, 0}));
+    }
+    return u32x4{o[0], o[1], o[2], o[3]};
+}
+
 // Row pitch (elements) of an LDS image read by MFMA operand loads: lane l
 // reads 16 B at row (l & 15) (+ a common row offset), 16-B column (l >> 4)
 // (+ a common column).  ds_read_b128 serves lanes {0-3,12-15,20-27},

@@ -142,17 +142,13 @@ __global__ __launch_bounds__(256, (s1_min_blocks<NT, NKS, NOPS>())) void k_conv_
             for (int s = 0; s < NKS; ++s) {
                 u32x4 v = T.x[i][s];
                 if (pro) {
-                    float f[CH];
-                    unpack(v, f, bf16_t());
                     // prologue coefficients from LDS (registers go to the tile ring)
                     const int c0 = s * KS + g * CH;
                     const float4 sa = *(const float4*)&bnp[c0], sb = *(const float4*)&bnp[c0 + 4];
                     const float4 ha = *(const float4*)&bnp[64 + c0], hb = *(const float4*)&bnp[64 + c0 + 4];
                     const float sc[CH] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
                     const float sh[CH] = {ha.x, ha.y, ha.z, ha.w, hb.x, hb.y, hb.z, hb.w};
-#pragma unroll
-                    for (int e = 0; e < CH; ++e) f[e] = fmaxf(f[e] * sc[e] + sh[e], 0.f);
-                    v = pack(f, bf16_t());
+                    v = bn_relu_bf16x8(v, sc, sh);
                     // a pixel outside the image / a channel chunk beyond cs stays zero
                     const int m = t * (16 * TW) + i * 16 + li, k = s * KS + g * CH;
                     const uint32_t keep = ((m < M) & (k < cs)) ? ~0u : 0u;
@@ -390,14 +386,10 @@ __global__ __launch_bounds__(256, 2) void k_s1_fanout(const rnvp_net_step* __res
                 for (int i = 0; i < TW; ++i) {
                     u32x4 v = X[i][s];
                     if (pro) {
-                        float f[CH];
-                        unpack(v, f, bf16_t());
                         const int c0 = s * KS + g * CH;
                         const float* sc = bnp + c * 128 + c0;
                         const float* sh = sc + 64;
-#pragma unroll
-                        for (int e = 0; e < CH; ++e) f[e] = fmaxf(f[e] * sc[e] + sh[e], 0.f);
-                        v = pack(f, bf16_t());
+                        v = bn_relu_bf16x8(v, sc, sh);
                         const int m = t * (16 * TW) + i * 16 + li;
                         const uint32_t keep = ((m < M) & (c0 < cs)) ? ~0u : 0u;
                         v &= u32x4{keep, keep, keep, keep};

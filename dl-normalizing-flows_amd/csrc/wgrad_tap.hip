@@ -273,11 +273,7 @@ __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int 
             const int pos = (tid + u * WT_NT) / CPI;
             u32x4 v = rx[SL][u];
             if (pro) {
-                float f[8];
-                unpack(v, f, bf16_t());
-#pragma unroll
-                for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e] * sc[e] + sh[e], 0.f);
-                v = pack(f, bf16_t());
+                v = bn_relu_bf16x8(v, sc, sh);
                 const uint32_t k = ((xm[SL] >> u) & 1u) ? ~0u : 0u;
                 v &= u32x4{k, k, k, k};
             }
