@@ -90,6 +90,15 @@ __device__ __forceinline__ double seg_sum(double v, int seg) {
     return v;
 }
 
+// per-channel sums of doubles over a lane segment: seg >= 16 (the wide
+// scales) -> DPP row sums on the VALU, every 16-lane row's lane 0 then adds
+// its row (rows never straddle a segment); shorter segments -> ds_bpermute
+// shuffles.  The shuffles were the coupling passes' bottleneck at the wide
+// scales (6 steps x 2 bpermutes per double and quantity).  seg_mask: a lane
+// with (lane & seg_mask(seg)) == 0 holds a sum to add.
+__device__ __forceinline__ double seg_red(double v, int seg) { return seg >= 16 ? row_sum16(v) : seg_sum(v, seg); }
+__device__ __forceinline__ int seg_mask(int seg) { return seg >= 16 ? 15 : seg - 1; }
+
 template <typename T>
 __device__ __forceinline__ void tile_copy_in(const void* src, long long m0, int tp, int cs, T* lds) {
     const int n16 = tp * cs * (int)sizeof(T) / 16;
@@ -175,8 +184,8 @@ __global__ __launch_bounds__(256) void k_in_stats(rnvp_coupling_args a, int TP, 
         const int cb = ok ? e / t.tp : 0, p = t.p0 + (ok ? e - cb * t.tp : 0);
         float v = ok ? xv : 0.f;
         if (g.kind == 0 && !ckbd_m(g, p)) v = 0.f;
-        const double s1 = seg_sum((double)v, seg), s2 = seg_sum((double)v * v, seg);
-        if (ok && (lane & (seg - 1)) == 0) {
+        const double s1 = seg_red((double)v, seg), s2 = seg_red((double)v * v, seg);
+        if (ok && (lane & seg_mask(seg)) == 0) {
             atomicAdd(&red[cb], s1);
             atomicAdd(&red[g.Cb + cb], s2);
         }
@@ -303,14 +312,14 @@ __global__ __launch_bounds__(256) void k_out1(rnvp_coupling_args a, int TP, int 
             sl += lr;
         }
         if (ok) a.u[idx] = u;
-        const double s1 = seg_sum((double)u, seg), s2 = seg_sum((double)u * u, seg);
-        if (ok && (g.kind == 0 || chan_on) && (lane & (seg - 1)) == 0) {
+        const double s1 = seg_red((double)u, seg), s2 = seg_red((double)u * u, seg);
+        if (ok && (g.kind == 0 || chan_on) && (lane & seg_mask(seg)) == 0) {
             atomicAdd(&red[cb], s1);
             atomicAdd(&red[g.Cb + cb], s2);
         }
         if (nxt) {   // uniform: the transformed positions' share, for the next coupling's in_bn
-            const double t1 = seg_sum(tr ? (double)u : 0.0, seg), t2 = seg_sum(tr ? (double)u * u : 0.0, seg);
-            if (ok && (lane & (seg - 1)) == 0) {
+            const double t1 = seg_red(tr ? (double)u : 0.0, seg), t2 = seg_red(tr ? (double)u * u : 0.0, seg);
+            if (ok && (lane & seg_mask(seg)) == 0) {
                 atomicAdd(&red[2 * g.Cb + cb], t1);
                 atomicAdd(&red[3 * g.Cb + cb], t2);
             }
@@ -696,8 +705,8 @@ __global__ __launch_bounds__(256) void k_out_bwd_red(rnvp_coupling_args a, int T
             vB = gz * (uv - tab[cb]) * tab[g.Cb + cb];
             vG = glv;
         }
-        const double dA = seg_sum((double)vA, seg), dB = seg_sum((double)vB, seg), dG = seg_sum((double)vG, seg);
-        if (ok && (lane & (seg - 1)) == 0) {
+        const double dA = seg_red((double)vA, seg), dB = seg_red((double)vB, seg), dG = seg_red((double)vG, seg);
+        if (ok && (lane & seg_mask(seg)) == 0) {
             atomicAdd(&red[cb], dA);
             atomicAdd(&red[g.Cb + cb], dB);
             atomicAdd(&red[2 * g.Cb + cb], dG);
@@ -865,8 +874,8 @@ __global__ __launch_bounds__(256) void k_in_bwd_red(rnvp_coupling_args a, int TP
         const int cb = ok ? e / t.tp : 0, pl = ok ? e - cb * t.tp : 0;
         float gxa = 0.f, xh = 0.f;
         if (ok) in_bwd_vals<T>(a, g, t, gh, tab, cb, pl, xv, gxa, xh);
-        const double s1 = seg_sum((double)gxa, seg), s2 = seg_sum((double)gxa * xh, seg);
-        if (ok && (lane & (seg - 1)) == 0) {
+        const double s1 = seg_red((double)gxa, seg), s2 = seg_red((double)gxa * xh, seg);
+        if (ok && (lane & seg_mask(seg)) == 0) {
             atomicAdd(&red[cb], s1);
             atomicAdd(&red[g.Cb + cb], s2);
         }
@@ -974,8 +983,8 @@ __global__ __launch_bounds__(256) void k_in_bwd_apply(rnvp_coupling_args a, rnvp
                 vB = gfin * (puv - tab[7 * g.Cb + cb]) * tab[8 * g.Cb + cb];
                 vG = pv.gl_sample ? pv.gl_sample[t.b] : 0.f;
             }
-            const double dA = seg_sum((double)vA, seg), dB = seg_sum((double)vB, seg), dG = seg_sum((double)vG, seg);
-            if (ok && (lane & (seg - 1)) == 0) {
+            const double dA = seg_red((double)vA, seg), dB = seg_red((double)vB, seg), dG = seg_red((double)vG, seg);
+            if (ok && (lane & seg_mask(seg)) == 0) {
                 atomicAdd(&pred[cb], dA);
                 atomicAdd(&pred[g.Cb + cb], dB);
                 atomicAdd(&pred[2 * g.Cb + cb], dG);
