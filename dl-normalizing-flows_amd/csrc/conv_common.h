@@ -259,36 +259,7 @@ __device__ __forceinline__ void bn_bwd_body(const rnvp_bn_bwd_args& a, double* d
     double* gs = dsm + 2 * cs;
     float* p = (float*)(dsm + 4 * cs);   // per channel: coef, k1, k2, mean, rstd
     float* t_sc = p + 5 * cs;            // scratch: scale, shift, mean, rstd [cs each]
-    const T* G = (const T*)a.g;
-    const T* X = (const T*)a.x;
-    const T* R = (const T*)a.residual;
-    T* DX = (T*)a.dx;
-    const int cpr = cs / CH;
-    const long long nch = a.M * cpr;
-    const long long q0 = blk * (long long)blockDim.x + threadIdx.x, qs = (long long)nblk * blockDim.x;
-    // the tables' shard sums are loaded first, then the first chunk's
-    // operands (vmcnt completes in issue order: the tables wait for their own
-    // loads only, the chunk's round trip overlaps theirs; at the deep scales
-    // that first chunk is a thread's whole share)
-    ShardLoads<4> gl, bl;
-    const bool spre = a.sums && shard_fits(C, a.sum_shards, 4) && (!a.bn.sums || shard_fits(C, a.bn.shards, 4));
-    if (spre) {
-        shard_issue<4>(a.sums, C, a.sum_shards, 0, C, gl);
-        if (a.bn.sums) shard_issue<4>(a.bn.sums, C, a.bn.shards, 0, C, bl);
-    }
-    u32x4 pg = u32x4{0u, 0u, 0u, 0u}, px = pg, pr = pg, pa = pg;
-    if (q0 < nch) {
-        const long long o = q0 * CH;
-        pg = *(const u32x4*)(G + o);
-        px = *(const u32x4*)(X + o);
-        if (R) pr = *(const u32x4*)(R + o);
-        if (a.accumulate) pa = *(const u32x4*)(DX + o);
-    }
-    if (spre) {
-        shard_finish<4>(gl, C, gs, gs + cs);
-        if (a.bn.sums) shard_finish<4>(bl, C, dsm, dsm + cs);
-        block_bn_finish(a.bn, C, 0, cs, t_sc, t_sc + cs, t_sc + 2 * cs, t_sc + 3 * cs, dsm);
-    } else {   // both shard reductions (forward BN stats, backward g-sums) in one pass
+    {   // both shard reductions (forward BN stats, backward g-sums) in one pass
         if (a.bn.sums) {
             const ShardSrc src[2] = {{a.sums, C, a.sum_shards, 0, C, gs, gs + cs},
                                      {a.bn.sums, C, a.bn.shards, 0, C, dsm, dsm + cs}};
@@ -319,6 +290,13 @@ __device__ __forceinline__ void bn_bwd_body(const rnvp_bn_bwd_args& a, double* d
         p[5 * c] = coef; p[5 * c + 1] = k1; p[5 * c + 2] = k2; p[5 * c + 3] = mean; p[5 * c + 4] = rstd;
     }
     __syncthreads();
+    const T* G = (const T*)a.g;
+    const T* X = (const T*)a.x;
+    const T* R = (const T*)a.residual;
+    T* DX = (T*)a.dx;
+    const int cpr = cs / CH;
+    const long long nch = a.M * cpr;
+    const long long q0 = blk * (long long)blockDim.x + threadIdx.x, qs = (long long)nblk * blockDim.x;
     // the grid stride is a multiple of the chunks per pixel in practice: the
     // channel chunk of a thread is then fixed (no 64-bit modulo per chunk)
     const bool fixed = qs % cpr == 0;
@@ -326,10 +304,9 @@ __device__ __forceinline__ void bn_bwd_body(const rnvp_bn_bwd_args& a, double* d
     for (long long q = q0; q < nch; q += qs) {
         const long long o = q * CH;
         if (!fixed) c0 = (int)(q % cpr) * CH;
-        const bool first = q == q0;
         float g[CH], x[CH], d[CH];
-        unpack(first ? pg : *(const u32x4*)(G + o), g, T());
-        unpack(first ? px : *(const u32x4*)(X + o), x, T());
+        unpack(*(const u32x4*)(G + o), g, T());
+        unpack(*(const u32x4*)(X + o), x, T());
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
             const float* pp = p + 5 * (c0 + j);
@@ -338,13 +315,13 @@ __device__ __forceinline__ void bn_bwd_body(const rnvp_bn_bwd_args& a, double* d
         }
         if (R) {
             float r[CH];
-            unpack(first ? pr : *(const u32x4*)(R + o), r, T());
+            unpack(*(const u32x4*)(R + o), r, T());
 #pragma unroll
             for (int j = 0; j < CH; ++j) d[j] += r[j];
         }
         if (a.accumulate) {
             float r[CH];
-            unpack(first ? pa : *(const u32x4*)(DX + o), r, T());
+            unpack(*(const u32x4*)(DX + o), r, T());
 #pragma unroll
             for (int j = 0; j < CH; ++j) d[j] += r[j];
         }
