@@ -720,13 +720,7 @@ __global__ __launch_bounds__(256) void k_conv_halo(rnvp_conv_args a, int shards)
         const int mm = m < M ? m : 0;
         const int row = fdiv_small(mm, rW);
         const int x = mm - row * W, y = row - fdiv_small(row, rH) * H;
-        unsigned bits = 0;
-#pragma unroll
-        for (int tp = 0; tp < KSZ * KSZ; ++tp) {
-            const int yy = y + tp / KSZ - PAD, xx = x + tp % KSZ - PAD;
-            bits |= (unsigned)((m < M) & (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W)) << tp;
-        }
-        tvm[i] = bits;
+        tvm[i] = tap_mask<KSZ>(x, y, W, H, m < M);
     }
     // K position of k = (wid + 4 it) * KS (+ g * CH for this lane).  UNI
     // (cs % KS == 0): a k-step never straddles a tap, so (tap, ci) are
@@ -1042,13 +1036,7 @@ __global__ __launch_bounds__(256 * NH) void k_conv_band(rnvp_conv_args a, int sh
         const int mm = m < M ? m : 0;
         const int row = fdiv_small(mm, rW);
         const int x = mm - row * W, y = row - fdiv_small(row, rH) * H;
-        unsigned bits = 0;
-#pragma unroll
-        for (int tp = 0; tp < KSZ * KSZ; ++tp) {
-            const int yy = y + tp / KSZ - PAD, xx = x + tp % KSZ - PAD;
-            bits |= (unsigned)((m < M) & (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W)) << tp;
-        }
-        tvm[i] = bits;
+        tvm[i] = tap_mask<KSZ>(x, y, W, H, m < M);
     }
 
     floatx4 acc[TM][NTW];

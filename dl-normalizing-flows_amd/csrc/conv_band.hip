@@ -303,13 +303,7 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
             const int mm = m < M ? m : 0;
             const int row = fdiv_small(mm, rW);
             const int x = mm - row * W, y = row - fdiv_small(row, rH) * H;
-            unsigned bits = 0;
-#pragma unroll
-            for (int tp = 0; tp < 9; ++tp) {
-                const int yy = y + tp / 3 - 1, xx = x + tp % 3 - 1;
-                bits |= (unsigned)((m < M) & (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W)) << tp;
-            }
-            tvm[i] = bits;
+            tvm[i] = tap_mask<3>(x, y, W, H, m < M);
         }
         floatx4 acc[TM][NTW];
 #pragma unroll

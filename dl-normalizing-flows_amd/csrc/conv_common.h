@@ -130,6 +130,22 @@ __device__ __forceinline__ void epi4p(const rnvp_conv_args& a, long long o, cons
     st4((T*)a.y + o, v);
 }
 
+// in-image tap mask of an output pixel at column x, row y (0 <= x < W,
+// 0 <= y < H): bit ky*KSZ + kx is set iff tap (ky, kx) of the KSZ x KSZ
+// (pad KSZ/2) window reads inside the image -- the outer product of three
+// row bits and three column bits (~8 VALU instead of 9 taps x 5 compares)
+template <int KSZ>
+__device__ __forceinline__ unsigned tap_mask(int x, int y, int W, int H, bool valid) {
+    static_assert(KSZ == 1 || KSZ == 3, "1x1 / 3x3");
+    if constexpr (KSZ == 1) {
+        return valid ? 1u : 0u;
+    } else {
+        const unsigned cb = (x > 0 ? 1u : 0u) | 2u | (x < W - 1 ? 4u : 0u);
+        const unsigned mk = (y > 0 ? cb : 0u) | (cb << 3) | (y < H - 1 ? cb << 6 : 0u);
+        return valid ? mk : 0u;
+    }
+}
+
 // BN+ReLU of 8 bf16 channels (one 16-B chunk), scale / shift per channel:
 // packed fp32 FMAs, the bf16 rounding, then ReLU as a packed signed-16-bit
 // max against 0 on the rounded pair (a bf16 with its sign bit set is a
