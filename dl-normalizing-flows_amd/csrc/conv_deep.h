@@ -119,13 +119,6 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
     // 128 channels the rows fill ~6 of the SB slots, and every wasted load
     // counts against the 63 outstanding vector memory operations a wave can
     // have, serialising the prologue into extra memory round trips
-    // buffer loads with 32-bit offsets where the operand spans < 2 GiB (an
-    // out-of-range offset reads zero): no 64-bit address arithmetic per load
-    constexpr int OOB = 0x7ffffff0;
-    const bool xbuf = (long long)M * cs * (long long)sizeof(T) < (1ll << 31) - 16;
-    const __amdgpu_buffer_rsrc_t XR = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(X), 0,
-                                                                        xbuf ? (int)((long long)M * cs * sizeof(T)) : 0,
-                                                                        0x00020000);
     auto stage_load = [&](int r0) {
 #pragma unroll
         for (int u = 0; u < SB; ++u) {
@@ -133,11 +126,7 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
             const int r = r0 + rbase + u * RSTEP;
             const int p = m0 - hal + r;
             const bool ok = (r < R) & (p >= 0) & (p < M);
-            if (xbuf)
-                sv[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                      XR, ok ? (p * cs + cfix * CH) * (int)sizeof(T) : OOB, 0, 0));
-            else
-                sv[u] = *(const u32x4*)(X + (ok ? (long long)p * cs + cfix * CH : 0));
+            sv[u] = *(const u32x4*)(X + (ok ? (long long)p * cs + cfix * CH : 0));
         }
     };
     float scv[CH], shv[CH];
@@ -191,26 +180,21 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
         epi_prefetch<T>(a, (long long)m * cso + n0 + col, m < M && n0 + col < cso, pre[e]);
     }
     stage_load(0);
-    // weights: per-lane row offsets (32-bit, rows >= N clamped to row 0: they
-    // only feed output columns that are never stored); the k-step's column
-    // is wave-uniform and goes in the buffer load's scalar offset
-    const __amdgpu_buffer_rsrc_t WR = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<T*>(Wt), 0, (int)((long long)N * a.kp * sizeof(T)), 0x00020000);
-    int wofs[TN];
+    const T* wrow[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
+        // rows >= N (clamped to row 0) only feed output columns that are never stored
         const int row = n0 + j * 16 + li;
-        wofs[j] = ((row < N ? row : 0) * a.kp + g * CH) * (int)sizeof(T);
+        wrow[j] = Wt + (long long)(row < N ? row : 0) * a.kp + g * CH;
     }
     // wave wk's k-step s: tap s / NC, channel chunk (s % NC) * WK + wk of KS
+    // (plain loads: buffer loads here measured slower -- the ring's waits)
     u32x4 rb[DK][TN];
     auto bload = [&](int st) {   // st is a compile-time constant after unrolling
         const int tp = st / NC, ch = st - (st / NC) * NC;
         const int k = tp * cs + (ch * WK + wk) * KS;
-        const int ks = __builtin_amdgcn_readfirstlane(k * (int)sizeof(T));
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-            rb[st % DK][j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(WR, wofs[j], ks, 0));
+        for (int j = 0; j < TN; ++j) rb[st % DK][j] = *(const u32x4*)(wrow[j] + k);
     };
 #pragma unroll
     for (int u = 0; u < DK; ++u)
