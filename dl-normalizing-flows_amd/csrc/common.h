@@ -247,16 +247,16 @@ __device__ __forceinline__ void shard_issue(const double* sums, int C, int shard
     const int total = nc * (shards < 1 ? 1 : shards);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
+        // unconditional loads (an index past the table reads entry 0 and is
+        // marked unused): no branch, so no wait is forced at its join
         const int t = u * blockDim.x + threadIdx.x;
-        L.cc[u] = -1;
-        L.v1[u] = L.v2[u] = 0.0;
-        if (t < total) {
-            const int c = t % nc, h = t / nc;
-            const double* p = sums + (long long)h * 2 * C + c0 + c;
-            L.v1[u] = p[0];
-            L.v2[u] = p[C];
-            L.cc[u] = c;
-        }
+        const bool ok = t < total;
+        const int tt = ok ? t : 0;
+        const int c = tt % nc, h = tt / nc;
+        const double* p = sums + (long long)h * 2 * C + c0 + c;
+        L.v1[u] = p[0];
+        L.v2[u] = p[C];
+        L.cc[u] = ok ? c : -1;
     }
 }
 template <int U>

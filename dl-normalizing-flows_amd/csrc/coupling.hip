@@ -174,7 +174,7 @@ __global__ __launch_bounds__(256) void k_in_stats(rnvp_coupling_args a, int TP, 
 #pragma unroll
     for (int k = 0; k < CP_K; ++k) {
         const int e = k * 256 + threadIdx.x;
-        xp[k] = e < total ? a.x[xidx(e)] : 0.f;
+        { const float v = a.x[xidx(e < total ? e : 0)]; xp[k] = e < total ? v : 0.f; }   // unconditional (clamped) load: no branch, no wait
     }
     lds_zero(red, 2 * g.Cb);
     __syncthreads();
@@ -195,7 +195,7 @@ __global__ __launch_bounds__(256) void k_in_stats(rnvp_coupling_args a, int TP, 
         if (k * 256 < total) body(k * 256, xp[k]);
     for (int e0 = CP_K * 256; e0 < total; e0 += 256) {
         const int e = e0 + threadIdx.x;
-        body(e0, e < total ? a.x[xidx(e)] : 0.f);
+        { const float v = a.x[xidx(e < total ? e : 0)]; body(e0, e < total ? v : 0.f); }
     }
     __syncthreads();
     double* dst = cshard(a.in_sums, 2 * g.Cb);
@@ -222,7 +222,7 @@ __global__ __launch_bounds__(256) void k_in_apply(rnvp_coupling_args a, int TP, 
 #pragma unroll
     for (int k = 0; k < CP_K; ++k) {
         const int e = k * 256 + threadIdx.x;
-        xp[k] = e < total ? a.x[xidx(e)] : 0.f;
+        { const float v = a.x[xidx(e < total ? e : 0)]; xp[k] = e < total ? v : 0.f; }   // unconditional (clamped) load: no branch, no wait
     }
     in_bn_table(a, g, tab);
     if (blockIdx.x == 0 && a.training && a.in_rmean) {
@@ -288,7 +288,7 @@ __global__ __launch_bounds__(256) void k_out1(rnvp_coupling_args a, int TP, int 
 #pragma unroll
     for (int k = 0; k < CP_K; ++k) {
         const int e = k * 256 + threadIdx.x;
-        xp[k] = e < total ? a.x[xidx(e)] : 0.f;
+        { const float v = a.x[xidx(e < total ? e : 0)]; xp[k] = e < total ? v : 0.f; }   // unconditional (clamped) load: no branch, no wait
     }
     lds_zero(red, 4 * g.Cb);
     tile_copy_in<T>(a.st, t.m0, t.tp, a.cs_st, st);
@@ -331,7 +331,7 @@ __global__ __launch_bounds__(256) void k_out1(rnvp_coupling_args a, int TP, int 
         if (k * 256 < total) body(k * 256, xp[k]);
     for (int e0 = CP_K * 256; e0 < total; e0 += 256) {
         const int e = e0 + threadIdx.x;
-        body(e0, e < total ? a.x[xidx(e)] : 0.f);
+        { const float v = a.x[xidx(e < total ? e : 0)]; body(e0, e < total ? v : 0.f); }
     }
     const float dl = block_sum(sl, redl);   // (barriers also publish red)
     if (threadIdx.x == 0 && dl != 0.f) atomicAdd(&a.ldj_sample[t.b], dl);
@@ -415,7 +415,7 @@ __global__ __launch_bounds__(256) void k_out2_in(rnvp_coupling_args a, rnvp_coup
 #pragma unroll
     for (int k = 0; k < CP_K; ++k) {
         const int e = k * 256 + threadIdx.x;
-        up[k] = e < total ? a.u[uidx(e)] : 0.f;
+        { const float v = a.u[uidx(e < total ? e : 0)]; up[k] = e < total ? v : 0.f; }
     }
     for (int cb = threadIdx.x; cb < Cb; cb += blockDim.x) {
         float mf, rf, hl;
@@ -539,7 +539,7 @@ __global__ void k_out2(rnvp_coupling_args a, int main_grid) {
     const double cnt = (double)g.B * g.HW;
     const long long n = (long long)g.B * g.C * g.HW;
     const long long e_first = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    const float u_first = e_first < n ? a.u[e_first] : 0.f;   // in flight under the table
+    const float u_first = a.u[e_first < n ? e_first : 0];   // in flight under the table (clamped: no branch)
     for (int cb = threadIdx.x; cb < g.Cb; cb += blockDim.x) {
         double mean = 0, var = 1;
         if (a.coupling_bn) {
@@ -651,6 +651,22 @@ __global__ void k_reverse(rnvp_coupling_args a) {
 __device__ __forceinline__ float gl_at(const rnvp_coupling_args& a, long long e, long long b) {
     return a.gl_full ? a.gl_full[e] : (a.gl_sample ? a.gl_sample[b] : 0.f);
 }
+// the same operand as one unconditional load (uniform base / index choice;
+// with neither gradient present a valid dummy address, weighted 0): a
+// prefetch without branches, so no wait is forced at the branch join
+struct GlOp {
+    const float* base;
+    bool full;
+    float w;
+};
+__device__ __forceinline__ GlOp gl_op(const rnvp_coupling_args& a) {
+    GlOp o;
+    o.full = a.gl_full != nullptr;
+    o.base = a.gl_full ? a.gl_full : (a.gl_sample ? a.gl_sample : a.gz);
+    o.w = (a.gl_full || a.gl_sample) ? 1.f : 0.f;
+    return o;
+}
+__device__ __forceinline__ float gl_ld(const GlOp& o, long long e, long long b) { return o.w * o.base[o.full ? e : b]; }
 
 // out_bn statistics of the forward (train) or running (eval) for channel cb
 __device__ __forceinline__ void out_bn_stats(const rnvp_coupling_args& a, const Geo& g, int cb, float& fm, float& rstd) {
@@ -683,13 +699,15 @@ __global__ __launch_bounds__(256) void k_out_bwd_red(rnvp_coupling_args a, int T
         return ((long long)t.b * g.C + c) * g.HW + p;
     };
     float gzp[CP_K], up[CP_K], glp[CP_K];
+    const GlOp glo = gl_op(a);
 #pragma unroll
     for (int k = 0; k < CP_K; ++k) {
         const int e = k * 256 + threadIdx.x;
-        const long long idx = e < total ? eidx(e) : 0;
-        gzp[k] = e < total ? a.gz[idx] : 0.f;
-        up[k] = e < total ? a.u[idx] : 0.f;
-        glp[k] = e < total ? gl_at(a, idx, t.b) : 0.f;
+        const long long idx = eidx(e < total ? e : 0);   // unconditional (clamped) loads
+        const float gz = a.gz[idx], uv = a.u[idx], gl = gl_ld(glo, idx, t.b);
+        gzp[k] = e < total ? gz : 0.f;
+        up[k] = e < total ? uv : 0.f;
+        glp[k] = e < total ? gl : 0.f;
     }
     lds_zero(red, 3 * g.Cb);
     for (int cb = threadIdx.x; cb < g.Cb; cb += blockDim.x) out_bn_stats(a, g, cb, tab[cb], tab[g.Cb + cb]);
@@ -717,8 +735,9 @@ __global__ __launch_bounds__(256) void k_out_bwd_red(rnvp_coupling_args a, int T
         if (k * 256 < total) body(k * 256, gzp[k], up[k], glp[k]);
     for (int e0 = CP_K * 256; e0 < total; e0 += 256) {
         const int e = e0 + threadIdx.x;
-        const long long idx = e < total ? eidx(e) : 0;
-        body(e0, e < total ? a.gz[idx] : 0.f, e < total ? a.u[idx] : 0.f, e < total ? gl_at(a, idx, t.b) : 0.f);
+        const long long idx = eidx(e < total ? e : 0);
+        const float gz = a.gz[idx], uv = a.u[idx], gl = gl_ld(glo, idx, t.b);
+        body(e0, e < total ? gz : 0.f, e < total ? uv : 0.f, e < total ? gl : 0.f);
     }
     __syncthreads();
     double* dst = cshard(a.bwd_sums, 3 * g.Cb);
@@ -744,14 +763,15 @@ __global__ __launch_bounds__(256) void k_out_bwd_apply(rnvp_coupling_args a, int
         return ((long long)t.b * g.C + c) * g.HW + t.p0 + pl;
     };
     float gzp[CP_K], up[CP_K], xp[CP_K], glp[CP_K];
+    const GlOp glo = gl_op(a);
 #pragma unroll
     for (int k = 0; k < CP_K; ++k) {
         const int e = k * 256 + threadIdx.x;
-        const long long idx = e < total ? eidx(e) : 0;
-        gzp[k] = e < total ? a.gz[idx] : 0.f;
-        up[k] = e < total ? a.u[idx] : 0.f;
-        xp[k] = e < total ? a.x[idx] : 0.f;
-        glp[k] = e < total ? gl_at(a, idx, t.b) : 0.f;
+        const long long idx = eidx(e < total ? e : 0);   // unconditional (clamped) loads
+        gzp[k] = a.gz[idx];
+        up[k] = a.u[idx];
+        xp[k] = a.x[idx];
+        glp[k] = gl_ld(glo, idx, t.b);
     }
     for (int cb = threadIdx.x; cb < g.Cb; cb += blockDim.x) {
         float fm = 0.f, rstd = 1.f, kA = 0.f, kB = 0.f;
@@ -810,7 +830,7 @@ __global__ __launch_bounds__(256) void k_out_bwd_apply(rnvp_coupling_args a, int
     }
     for (int e = CP_K * 256 + threadIdx.x; e < total; e += 256) {
         const long long idx = eidx(e);
-        body(e, a.gz[idx], a.u[idx], a.x[idx], gl_at(a, idx, t.b));
+        body(e, a.gz[idx], a.u[idx], a.x[idx], gl_ld(glo, idx, t.b));
     }
     const float dsc = (float)block_sum(gsc, redl);   // (barriers also publish gs)
     const float dss = (float)block_sum(gss, redl);
@@ -862,7 +882,7 @@ __global__ __launch_bounds__(256) void k_in_bwd_red(rnvp_coupling_args a, int TP
 #pragma unroll
     for (int k = 0; k < CP_K; ++k) {
         const int e = k * 256 + threadIdx.x;
-        xp[k] = e < total ? a.x[xidx(e)] : 0.f;
+        { const float v = a.x[xidx(e < total ? e : 0)]; xp[k] = e < total ? v : 0.f; }   // unconditional (clamped) load: no branch, no wait
     }
     lds_zero(red, 2 * g.Cb);
     in_bn_table(a, g, tab);
@@ -885,7 +905,7 @@ __global__ __launch_bounds__(256) void k_in_bwd_red(rnvp_coupling_args a, int TP
         if (k * 256 < total) body(k * 256, xp[k]);
     for (int e0 = CP_K * 256; e0 < total; e0 += 256) {
         const int e = e0 + threadIdx.x;
-        body(e0, e < total ? a.x[xidx(e)] : 0.f);
+        { const float v = a.x[xidx(e < total ? e : 0)]; body(e0, e < total ? v : 0.f); }
     }
     __syncthreads();
     double* dst = cshard(a.in_bwd_sums, 2 * g.Cb);
@@ -912,10 +932,10 @@ __global__ __launch_bounds__(256) void k_in_bwd_apply(rnvp_coupling_args a, rnvp
 #pragma unroll
     for (int k = 0; k < CP_K; ++k) {
         const int e = k * 256 + threadIdx.x;
-        const long long idx = e < total ? xidx(e) : 0;
-        xp[k] = e < total ? a.x[idx] : 0.f;
-        gxp[k] = e < total ? a.gx[idx] : 0.f;
-        pup[k] = (CHAIN && e < total) ? pv.u[idx] : 0.f;
+        const long long idx = xidx(e < total ? e : 0);   // unconditional (clamped) loads
+        xp[k] = a.x[idx];
+        gxp[k] = a.gx[idx];
+        pup[k] = CHAIN ? pv.u[idx] : 0.f;
     }
     if (CHAIN) {
         lds_zero(pred, 3 * g.Cb);
@@ -997,8 +1017,9 @@ __global__ __launch_bounds__(256) void k_in_bwd_apply(rnvp_coupling_args a, rnvp
         if (k * 256 < total) body(k * 256, xp[k], gxp[k], pup[k]);
     for (int e0 = CP_K * 256; e0 < total; e0 += 256) {
         const int e = e0 + threadIdx.x;
-        const long long idx = e < total ? xidx(e) : 0;
-        body(e0, e < total ? a.x[idx] : 0.f, e < total ? a.gx[idx] : 0.f, (CHAIN && e < total) ? pv.u[idx] : 0.f);
+        const long long idx = xidx(e < total ? e : 0);
+        const float xv = a.x[idx], gxv = a.gx[idx], puv = CHAIN ? pv.u[idx] : 0.f;
+        body(e0, e < total ? xv : 0.f, e < total ? gxv : 0.f, puv);
     }
     if (CHAIN) {
         __syncthreads();
