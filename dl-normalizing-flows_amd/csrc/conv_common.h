@@ -275,7 +275,33 @@ __device__ __forceinline__ void bn_bwd_body(const rnvp_bn_bwd_args& a, double* d
     double* gs = dsm + 2 * cs;
     float* p = (float*)(dsm + 4 * cs);   // per channel: coef, k1, k2, mean, rstd
     float* t_sc = p + 5 * cs;            // scratch: scale, shift, mean, rstd [cs each]
-    {   // both shard reductions (forward BN stats, backward g-sums) in one pass
+    const T* G = (const T*)a.g;
+    const T* X = (const T*)a.x;
+    const T* R = (const T*)a.residual;
+    T* DX = (T*)a.dx;
+    const int cpr = cs / CH;
+    const long long nch = a.M * cpr;
+    const long long q0 = blk * (long long)blockDim.x + threadIdx.x, qs = (long long)nblk * blockDim.x;
+    // the tables' shard sums are loaded first, then the first chunk's
+    // operands (vmcnt completes in issue order: the tables wait for their own
+    // loads only, the chunk's round trip overlaps theirs; at the deep scales
+    // that first chunk is a thread's whole share)
+    ShardLoads<4> gl, bl;
+    const bool spre = a.sums && shard_fits(C, a.sum_shards, 4) && (!a.bn.sums || shard_fits(C, a.bn.shards, 4));
+    if (spre) {
+        shard_issue<4>(a.sums, C, a.sum_shards, 0, C, gl);
+        if (a.bn.sums) shard_issue<4>(a.bn.sums, C, a.bn.shards, 0, C, bl);
+    }
+    // unconditional (clamped) loads: a guarded load becomes a branch whose
+    // join waits for everything in flight
+    const long long o0 = (q0 < nch ? q0 : 0) * CH;
+    const u32x4 pg = *(const u32x4*)(G + o0), px = *(const u32x4*)(X + o0);
+    const u32x4 pr = *(const u32x4*)((R ? R : G) + o0), pa = *(const u32x4*)((a.accumulate ? (const T*)DX : G) + o0);
+    if (spre) {
+        shard_finish<4>(gl, C, gs, gs + cs);
+        if (a.bn.sums) shard_finish<4>(bl, C, dsm, dsm + cs);
+        block_bn_finish(a.bn, C, 0, cs, t_sc, t_sc + cs, t_sc + 2 * cs, t_sc + 3 * cs, dsm);
+    } else {   // both shard reductions (forward BN stats, backward g-sums) in one pass
         if (a.bn.sums) {
             const ShardSrc src[2] = {{a.sums, C, a.sum_shards, 0, C, gs, gs + cs},
                                      {a.bn.sums, C, a.bn.shards, 0, C, dsm, dsm + cs}};
@@ -306,13 +332,6 @@ __device__ __forceinline__ void bn_bwd_body(const rnvp_bn_bwd_args& a, double* d
         p[5 * c] = coef; p[5 * c + 1] = k1; p[5 * c + 2] = k2; p[5 * c + 3] = mean; p[5 * c + 4] = rstd;
     }
     __syncthreads();
-    const T* G = (const T*)a.g;
-    const T* X = (const T*)a.x;
-    const T* R = (const T*)a.residual;
-    T* DX = (T*)a.dx;
-    const int cpr = cs / CH;
-    const long long nch = a.M * cpr;
-    const long long q0 = blk * (long long)blockDim.x + threadIdx.x, qs = (long long)nblk * blockDim.x;
     // the grid stride is a multiple of the chunks per pixel in practice: the
     // channel chunk of a thread is then fixed (no 64-bit modulo per chunk)
     const bool fixed = qs % cpr == 0;
@@ -320,9 +339,10 @@ __device__ __forceinline__ void bn_bwd_body(const rnvp_bn_bwd_args& a, double* d
     for (long long q = q0; q < nch; q += qs) {
         const long long o = q * CH;
         if (!fixed) c0 = (int)(q % cpr) * CH;
+        const bool first = q == q0;
         float g[CH], x[CH], d[CH];
-        unpack(*(const u32x4*)(G + o), g, T());
-        unpack(*(const u32x4*)(X + o), x, T());
+        unpack(first ? pg : *(const u32x4*)(G + o), g, T());
+        unpack(first ? px : *(const u32x4*)(X + o), x, T());
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
             const float* pp = p + 5 * (c0 + j);
@@ -331,13 +351,13 @@ __device__ __forceinline__ void bn_bwd_body(const rnvp_bn_bwd_args& a, double* d
         }
         if (R) {
             float r[CH];
-            unpack(*(const u32x4*)(R + o), r, T());
+            unpack(first ? pr : *(const u32x4*)(R + o), r, T());
 #pragma unroll
             for (int j = 0; j < CH; ++j) d[j] += r[j];
         }
         if (a.accumulate) {
             float r[CH];
-            unpack(*(const u32x4*)(DX + o), r, T());
+            unpack(first ? pa : *(const u32x4*)(DX + o), r, T());
 #pragma unroll
             for (int j = 0; j < CH; ++j) d[j] += r[j];
         }
