@@ -292,11 +292,26 @@ __device__ __forceinline__ void bn_bwd_body(const rnvp_bn_bwd_args& a, double* d
         shard_issue<4>(a.sums, C, a.sum_shards, 0, C, gl);
         if (a.bn.sums) shard_issue<4>(a.bn.sums, C, a.bn.shards, 0, C, bl);
     }
-    // unconditional (clamped) loads: a guarded load becomes a branch whose
-    // join waits for everything in flight
-    const long long o0 = (q0 < nch ? q0 : 0) * CH;
-    const u32x4 pg = *(const u32x4*)(G + o0), px = *(const u32x4*)(X + o0);
-    const u32x4 pr = *(const u32x4*)((R ? R : G) + o0), pa = *(const u32x4*)((a.accumulate ? (const T*)DX : G) + o0);
+    // chunks q0 + u*qs (u < UB) per batch, every operand of a batch loaded
+    // at once; the first batch before the tables.  Unconditional (clamped)
+    // loads: a guarded load becomes a branch whose join waits for everything
+    // in flight
+    constexpr int UB = 4;
+    const T* RR = R ? R : G;
+    const T* AA = a.accumulate ? (const T*)DX : G;
+    u32x4 bg[UB], bx[UB], br[UB], ba[UB];
+    auto batch_load = [&](long long qb) {
+#pragma unroll
+        for (int u = 0; u < UB; ++u) {
+            const long long qq = qb + u * qs;
+            const long long o = (qq < nch ? qq : 0) * CH;
+            bg[u] = *(const u32x4*)(G + o);
+            bx[u] = *(const u32x4*)(X + o);
+            br[u] = *(const u32x4*)(RR + o);
+            ba[u] = *(const u32x4*)(AA + o);
+        }
+    };
+    batch_load(q0);
     if (spre) {
         shard_finish<4>(gl, C, gs, gs + cs);
         if (a.bn.sums) shard_finish<4>(bl, C, dsm, dsm + cs);
@@ -335,33 +350,40 @@ __device__ __forceinline__ void bn_bwd_body(const rnvp_bn_bwd_args& a, double* d
     // the grid stride is a multiple of the chunks per pixel in practice: the
     // channel chunk of a thread is then fixed (no 64-bit modulo per chunk)
     const bool fixed = qs % cpr == 0;
-    int c0 = (int)(q0 % cpr) * CH;
-    for (long long q = q0; q < nch; q += qs) {
-        const long long o = q * CH;
-        if (!fixed) c0 = (int)(q % cpr) * CH;
-        const bool first = q == q0;
-        float g[CH], x[CH], d[CH];
-        unpack(first ? pg : *(const u32x4*)(G + o), g, T());
-        unpack(first ? px : *(const u32x4*)(X + o), x, T());
+    const int cfix = (int)(q0 % cpr) * CH;
+    for (long long qb = q0;;) {
 #pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            const float* pp = p + 5 * (c0 + j);
-            const float xh = (x[j] - pp[3]) * pp[4];
-            d[j] = pp[0] * (g[j] - pp[1] - xh * pp[2]);
-        }
-        if (R) {
-            float r[CH];
-            unpack(first ? pr : *(const u32x4*)(R + o), r, T());
+        for (int u = 0; u < UB; ++u) {
+            const long long q = qb + u * qs;
+            if (q >= nch) break;
+            const long long o = q * CH;
+            const int c0 = fixed ? cfix : (int)(q % cpr) * CH;
+            float g[CH], x[CH], d[CH];
+            unpack(bg[u], g, T());
+            unpack(bx[u], x, T());
 #pragma unroll
-            for (int j = 0; j < CH; ++j) d[j] += r[j];
-        }
-        if (a.accumulate) {
-            float r[CH];
-            unpack(first ? pa : *(const u32x4*)(DX + o), r, T());
+            for (int j = 0; j < CH; ++j) {
+                const float* pp = p + 5 * (c0 + j);
+                const float xh = (x[j] - pp[3]) * pp[4];
+                d[j] = pp[0] * (g[j] - pp[1] - xh * pp[2]);
+            }
+            if (R) {
+                float r[CH];
+                unpack(br[u], r, T());
 #pragma unroll
-            for (int j = 0; j < CH; ++j) d[j] += r[j];
+                for (int j = 0; j < CH; ++j) d[j] += r[j];
+            }
+            if (a.accumulate) {
+                float r[CH];
+                unpack(ba[u], r, T());
+#pragma unroll
+                for (int j = 0; j < CH; ++j) d[j] += r[j];
+            }
+            *(u32x4*)(DX + o) = pack(d, T());
         }
-        *(u32x4*)(DX + o) = pack(d, T());
+        qb += UB * qs;
+        if (qb >= nch) break;
+        batch_load(qb);
     }
 }
 
