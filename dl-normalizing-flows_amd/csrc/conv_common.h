@@ -275,48 +275,7 @@ __device__ __forceinline__ void bn_bwd_body(const rnvp_bn_bwd_args& a, double* d
     double* gs = dsm + 2 * cs;
     float* p = (float*)(dsm + 4 * cs);   // per channel: coef, k1, k2, mean, rstd
     float* t_sc = p + 5 * cs;            // scratch: scale, shift, mean, rstd [cs each]
-    const T* G = (const T*)a.g;
-    const T* X = (const T*)a.x;
-    const T* R = (const T*)a.residual;
-    T* DX = (T*)a.dx;
-    const int cpr = cs / CH;
-    const long long nch = a.M * cpr;
-    const long long q0 = blk * (long long)blockDim.x + threadIdx.x, qs = (long long)nblk * blockDim.x;
-    // the tables' shard sums are loaded first, then the first chunk's
-    // operands (vmcnt completes in issue order: the tables wait for their own
-    // loads only, the chunk's round trip overlaps theirs; at the deep scales
-    // that first chunk is a thread's whole share)
-    ShardLoads<4> gl, bl;
-    const bool spre = a.sums && shard_fits(C, a.sum_shards, 4) && (!a.bn.sums || shard_fits(C, a.bn.shards, 4));
-    if (spre) {
-        shard_issue<4>(a.sums, C, a.sum_shards, 0, C, gl);
-        if (a.bn.sums) shard_issue<4>(a.bn.sums, C, a.bn.shards, 0, C, bl);
-    }
-    // chunks q0 + u*qs (u < UB) per batch, every operand of a batch loaded
-    // at once; the first batch before the tables.  Unconditional (clamped)
-    // loads: a guarded load becomes a branch whose join waits for everything
-    // in flight
-    constexpr int UB = 4;
-    const T* RR = R ? R : G;
-    const T* AA = a.accumulate ? (const T*)DX : G;
-    u32x4 bg[UB], bx[UB], br[UB], ba[UB];
-    auto batch_load = [&](long long qb) {
-#pragma unroll
-        for (int u = 0; u < UB; ++u) {
-            const long long qq = qb + u * qs;
-            const long long o = (qq < nch ? qq : 0) * CH;
-            bg[u] = *(const u32x4*)(G + o);
-            bx[u] = *(const u32x4*)(X + o);
-            br[u] = *(const u32x4*)(RR + o);
-            ba[u] = *(const u32x4*)(AA + o);
-        }
-    };
-    batch_load(q0);
-    if (spre) {
-        shard_finish<4>(gl, C, gs, gs + cs);
-        if (a.bn.sums) shard_finish<4>(bl, C, dsm, dsm + cs);
-        block_bn_finish(a.bn, C, 0, cs, t_sc, t_sc + cs, t_sc + 2 * cs, t_sc + 3 * cs, dsm);
-    } else {   // both shard reductions (forward BN stats, backward g-sums) in one pass
+    {   // both shard reductions (forward BN stats, backward g-sums) in one pass
         if (a.bn.sums) {
             const ShardSrc src[2] = {{a.sums, C, a.sum_shards, 0, C, gs, gs + cs},
                                      {a.bn.sums, C, a.bn.shards, 0, C, dsm, dsm + cs}};
@@ -347,43 +306,42 @@ __device__ __forceinline__ void bn_bwd_body(const rnvp_bn_bwd_args& a, double* d
         p[5 * c] = coef; p[5 * c + 1] = k1; p[5 * c + 2] = k2; p[5 * c + 3] = mean; p[5 * c + 4] = rstd;
     }
     __syncthreads();
+    const T* G = (const T*)a.g;
+    const T* X = (const T*)a.x;
+    const T* R = (const T*)a.residual;
+    T* DX = (T*)a.dx;
+    const int cpr = cs / CH;
+    const long long nch = a.M * cpr;
+    const long long q0 = blk * (long long)blockDim.x + threadIdx.x, qs = (long long)nblk * blockDim.x;
     // the grid stride is a multiple of the chunks per pixel in practice: the
     // channel chunk of a thread is then fixed (no 64-bit modulo per chunk)
     const bool fixed = qs % cpr == 0;
-    const int cfix = (int)(q0 % cpr) * CH;
-    for (long long qb = q0;;) {
+    int c0 = (int)(q0 % cpr) * CH;
+    for (long long q = q0; q < nch; q += qs) {
+        const long long o = q * CH;
+        if (!fixed) c0 = (int)(q % cpr) * CH;
+        float g[CH], x[CH], d[CH];
+        unpack(*(const u32x4*)(G + o), g, T());
+        unpack(*(const u32x4*)(X + o), x, T());
 #pragma unroll
-        for (int u = 0; u < UB; ++u) {
-            const long long q = qb + u * qs;
-            if (q >= nch) break;
-            const long long o = q * CH;
-            const int c0 = fixed ? cfix : (int)(q % cpr) * CH;
-            float g[CH], x[CH], d[CH];
-            unpack(bg[u], g, T());
-            unpack(bx[u], x, T());
-#pragma unroll
-            for (int j = 0; j < CH; ++j) {
-                const float* pp = p + 5 * (c0 + j);
-                const float xh = (x[j] - pp[3]) * pp[4];
-                d[j] = pp[0] * (g[j] - pp[1] - xh * pp[2]);
-            }
-            if (R) {
-                float r[CH];
-                unpack(br[u], r, T());
-#pragma unroll
-                for (int j = 0; j < CH; ++j) d[j] += r[j];
-            }
-            if (a.accumulate) {
-                float r[CH];
-                unpack(ba[u], r, T());
-#pragma unroll
-                for (int j = 0; j < CH; ++j) d[j] += r[j];
-            }
-            *(u32x4*)(DX + o) = pack(d, T());
+        for (int j = 0; j < CH; ++j) {
+            const float* pp = p + 5 * (c0 + j);
+            const float xh = (x[j] - pp[3]) * pp[4];
+            d[j] = pp[0] * (g[j] - pp[1] - xh * pp[2]);
         }
-        qb += UB * qs;
-        if (qb >= nch) break;
-        batch_load(qb);
+        if (R) {
+            float r[CH];
+            unpack(*(const u32x4*)(R + o), r, T());
+#pragma unroll
+            for (int j = 0; j < CH; ++j) d[j] += r[j];
+        }
+        if (a.accumulate) {
+            float r[CH];
+            unpack(*(const u32x4*)(DX + o), r, T());
+#pragma unroll
+            for (int j = 0; j < CH; ++j) d[j] += r[j];
+        }
+        *(u32x4*)(DX + o) = pack(d, T());
     }
 }
 
