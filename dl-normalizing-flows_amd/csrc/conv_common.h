@@ -82,39 +82,16 @@ __device__ __forceinline__ void epi4(const rnvp_conv_args& a, long long o, const
 // the epilogue operands of one 4-channel element (residual, previous y for
 // the skip accumulation, the dgrad epilogue's pre-BN x), loaded at kernel
 // start so the epilogue waits on no global round trip
-// Raw bits, converted only in the epilogue (converting at load time made the
-// prologue wait for these loads), loaded unconditionally (an absent operand
-// reads y, valid, unused): no branch between the prologue's loads.
 struct EpiPre {
-    u32x4 r, y, x;
+    float r[4], y[4], x[4];
 };
-
-template <typename T>
-__device__ __forceinline__ u32x4 ld4raw(const T* p) {
-    if constexpr (sizeof(T) == 2) {
-        const uint2 t = *(const uint2*)p;
-        return u32x4{t.x, t.y, 0u, 0u};
-    } else {
-        return *(const u32x4*)p;
-    }
-}
-template <typename T>
-__device__ __forceinline__ void cvt4raw(const u32x4& w, float* v) {
-    if constexpr (sizeof(T) == 2) {
-        v[0] = __uint_as_float(w.x << 16); v[1] = __uint_as_float(w.x & 0xffff0000u);
-        v[2] = __uint_as_float(w.y << 16); v[3] = __uint_as_float(w.y & 0xffff0000u);
-    } else {
-        v[0] = __uint_as_float(w.x); v[1] = __uint_as_float(w.y); v[2] = __uint_as_float(w.z); v[3] = __uint_as_float(w.w);
-    }
-}
 
 template <typename T>
 __device__ __forceinline__ void epi_prefetch(const rnvp_conv_args& a, long long o, bool live, EpiPre& p) {
     const long long oo = live ? o : 0;
-    const T* Y = (const T*)a.y;
-    p.r = ld4raw<T>((a.residual ? (const T*)a.residual : Y) + oo);
-    p.y = ld4raw<T>(Y + oo);
-    p.x = ld4raw<T>((a.epi_relu_bn_bwd ? (const T*)a.epi_x : Y) + oo);
+    if (a.residual) ld4((const T*)a.residual + oo, p.r);
+    if (a.accumulate) ld4((const T*)a.y + oo, p.y);
+    if (a.epi_relu_bn_bwd) ld4((const T*)a.epi_x + oo, p.x);
 }
 
 // epi4 over prefetched operands
@@ -126,25 +103,19 @@ __device__ __forceinline__ void epi4p(const rnvp_conv_args& a, long long o, cons
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = acc[r] + bias[r];
     if (a.residual) {
-        float f[4];
-        cvt4raw<T>(p.r, f);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += f[r];
+        for (int r = 0; r < 4; ++r) v[r] += p.r[r];
     }
     if (a.accumulate) {
-        float f[4];
-        cvt4raw<T>(p.y, f);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += f[r];
+        for (int r = 0; r < 4; ++r) v[r] += p.y[r];
     }
     if (epi_bn) {
-        float px[4];
-        cvt4raw<T>(p.x, px);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            if (px[r] * et[r] + et[pitch + r] <= 0.f) v[r] = 0.f;
+            if (p.x[r] * et[r] + et[pitch + r] <= 0.f) v[r] = 0.f;
             s1[r] += v[r];
-            s2[r] += v[r] * (px[r] - et[2 * pitch + r]) * et[3 * pitch + r];
+            s2[r] += v[r] * (p.x[r] - et[2 * pitch + r]) * et[3 * pitch + r];
         }
     } else {
 #pragma unroll
@@ -220,9 +191,6 @@ struct BnTab {
     float gam[CPT], bet[CPT];
 };
 
-// a valid dummy operand for unconditional loads of absent optional vectors
-__device__ const float g_rnvp_zero_f[1] = {0.f};
-
 template <int CPT, int NT = 256>
 __device__ __forceinline__ void tab_issue(const rnvp_bn_src& s, int C, int c0, int nc, BnTab<CPT>& t) {
 #pragma unroll
@@ -243,10 +211,8 @@ __device__ __forceinline__ void tab_issue(const rnvp_bn_src& s, int C, int c0, i
             t.a2[j] = s.var[cc];
             t.b1[j] = t.b2[j] = 0.0;
         }
-        // unconditional loads (absent: the zero dummy; tab_finish applies the
-        // defaults 1 / 0): no branch between the prologue's loads
-        t.gam[j] = (s.gamma ? s.gamma : g_rnvp_zero_f)[s.gamma ? cc : 0];
-        t.bet[j] = (s.beta ? s.beta : g_rnvp_zero_f)[s.beta ? cc : 0];
+        t.gam[j] = s.gamma ? s.gamma[cc] : 1.f;
+        t.bet[j] = s.beta ? s.beta[cc] : 0.f;
     }
 }
 
@@ -272,9 +238,8 @@ __device__ __forceinline__ void tab_finish(const rnvp_bn_src& s, int C, int c0, 
                 var = t.a2[j];
             }
             const float rstd = (float)(1.0 / sqrt(var + (double)s.eps));
-            const float gm = s.gamma ? t.gam[j] : 1.f, bt = s.beta ? t.bet[j] : 0.f;
-            sc = gm * rstd;
-            sf = bt - (float)mean * gm * rstd;
+            sc = t.gam[j] * rstd;
+            sf = t.bet[j] - (float)mean * t.gam[j] * rstd;
             mo = (float)mean;
             ro = rstd;
         }

@@ -171,9 +171,7 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
     BnTab<1> etb;
     if (PRO) tab_issue<CPT, NT>(a.pro, a.cin, 0, cs, ptab);
     if (epi_bn) tab_issue<1, NT>(a.epi, N, n0, BN, etb);
-    const bool bok = (tid < BN) & (a.bias != nullptr) & (n0 + tid < N);
-    const float bld = (a.bias ? a.bias : g_rnvp_zero_f)[bok ? n0 + tid : 0];   // unconditional load
-    const float bval = bok ? bld : 0.f;
+    const float bval = (tid < BN && a.bias && n0 + tid < N) ? a.bias[n0 + tid] : 0.f;
     EpiPre pre[NE];
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
