@@ -267,31 +267,69 @@ __device__ __forceinline__ int fdiv_exact(int q, int d, float r) {
 // grid: every block reduces the statistic shards into its LDS table, then
 // grid-strides over the 16-byte chunks.  dsm: 68*cs bytes of LDS
 // (tmp [2*cs] | gsum [2*cs] fp64 | p [5*cs] f32 | table [4*cs] f32).
-template <typename T>
-__device__ __forceinline__ void bn_bwd_body(const rnvp_bn_bwd_args& a, double* dsm, int blk, int nblk) {
+// GAM: gamma present -- its values for the thread's first two channels are
+// loaded ahead of the shard reduction, so no global round trip sits between
+// the reduction and the streaming loop (mean / rstd / coef follow
+// block_bn_finish's arithmetic exactly).
+template <typename T, bool GAM>
+__device__ __forceinline__ void bn_bwd_run(const rnvp_bn_bwd_args& a, double* dsm, int blk, int nblk) {
     constexpr int CH = Mf<T>::CH;
     const int cs = a.cs, C = a.C;
     const double cnt = (double)a.M;
     double* gs = dsm + 2 * cs;
     float* p = (float*)(dsm + 4 * cs);   // per channel: coef, k1, k2, mean, rstd
-    float* t_sc = p + 5 * cs;            // scratch: scale, shift, mean, rstd [cs each]
-    {   // both shard reductions (forward BN stats, backward g-sums) in one pass
-        if (a.bn.sums) {
-            const ShardSrc src[2] = {{a.sums, C, a.sum_shards, 0, C, gs, gs + cs},
-                                     {a.bn.sums, C, a.bn.shards, 0, C, dsm, dsm + cs}};
-            block_shard_sums_n<2>(src);
-        } else {
-            const ShardSrc src[1] = {{a.sums, C, a.sum_shards, 0, C, gs, gs + cs}};
-            block_shard_sums_n<1>(src);
-        }
-        block_bn_finish(a.bn, C, 0, cs, t_sc, t_sc + cs, t_sc + 2 * cs, t_sc + 3 * cs, dsm);
+    float gpre[2] = {1.f, 1.f};
+    if constexpr (GAM) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) gpre[j] = a.bn.gamma[min((int)threadIdx.x + j * (int)blockDim.x, C - 1)];
     }
-    for (int c = threadIdx.x; c < cs; c += blockDim.x) {
+    // both shard reductions (forward BN stats, backward g-sums): every load
+    // issued up front, without branches, when the tables fit one pass
+    // (ShardLoads); otherwise the looping block reduction
+    const bool two = a.bn.sums != nullptr;
+    if (shard_fits(C, a.sum_shards, 4) && shard_fits(C, two ? a.bn.shards : 1, 4)) {
+        ShardLoads<4> lg, lb;
+        shard_issue<4>(a.sums, C, a.sum_shards, 0, C, lg);
+        shard_issue<4>(two ? a.bn.sums : a.sums, C, two ? a.bn.shards : a.sum_shards, 0, C, lb);
+        for (int i = threadIdx.x; i < C; i += blockDim.x) {
+            gs[i] = gs[cs + i] = 0.0;
+            dsm[i] = dsm[cs + i] = 0.0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (lg.cc[u] >= 0) {
+                atomicAdd(&gs[lg.cc[u]], lg.v1[u]);
+                atomicAdd(&gs[cs + lg.cc[u]], lg.v2[u]);
+            }
+            if (two && lb.cc[u] >= 0) {
+                atomicAdd(&dsm[lb.cc[u]], lb.v1[u]);
+                atomicAdd(&dsm[cs + lb.cc[u]], lb.v2[u]);
+            }
+        }
+        __syncthreads();
+    } else if (two) {
+        const ShardSrc src[2] = {{a.sums, C, a.sum_shards, 0, C, gs, gs + cs},
+                                 {a.bn.sums, C, a.bn.shards, 0, C, dsm, dsm + cs}};
+        block_shard_sums_n<2>(src);
+    } else {
+        const ShardSrc src[1] = {{a.sums, C, a.sum_shards, 0, C, gs, gs + cs}};
+        block_shard_sums_n<1>(src);
+    }
+    auto entry = [&](int c, float gam) {
         float coef = 0.f, k1 = 0.f, k2 = 0.f, mean = 0.f, rstd = 1.f;
         if (c < C) {
-            mean = t_sc[2 * cs + c];
-            rstd = t_sc[3 * cs + c];
-            const float gam = a.bn.gamma ? a.bn.gamma[c] : 1.f;
+            double mn, var;
+            if (a.bn.sums) {
+                mn = dsm[c] / a.bn.count;
+                var = dsm[cs + c] / a.bn.count - mn * mn;
+                if (var < 0) var = 0;
+            } else {
+                mn = a.bn.mean[c];
+                var = a.bn.var[c];
+            }
+            rstd = (float)(1.0 / sqrt(var + (double)a.bn.eps));
+            mean = (float)mn;
             coef = gam * rstd;
             const double g1 = gs[c], g2 = gs[cs + c];
             if (a.bn.sums) {   // train mode: batch statistics carry gradient
@@ -304,7 +342,13 @@ __device__ __forceinline__ void bn_bwd_body(const rnvp_bn_bwd_args& a, double* d
             }
         }
         p[5 * c] = coef; p[5 * c + 1] = k1; p[5 * c + 2] = k2; p[5 * c + 3] = mean; p[5 * c + 4] = rstd;
+    };
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int c = threadIdx.x + j * blockDim.x;
+        if (c < cs) entry(c, gpre[j]);
     }
+    for (int c = threadIdx.x + 2 * blockDim.x; c < cs; c += blockDim.x) entry(c, GAM ? a.bn.gamma[c] : 1.f);
     __syncthreads();
     const T* G = (const T*)a.g;
     const T* X = (const T*)a.x;
@@ -343,6 +387,12 @@ __device__ __forceinline__ void bn_bwd_body(const rnvp_bn_bwd_args& a, double* d
         }
         *(u32x4*)(DX + o) = pack(d, T());
     }
+}
+
+template <typename T>
+__device__ __forceinline__ void bn_bwd_body(const rnvp_bn_bwd_args& a, double* dsm, int blk, int nblk) {
+    if (a.bn.gamma) bn_bwd_run<T, true>(a, dsm, blk, nblk);
+    else bn_bwd_run<T, false>(a, dsm, blk, nblk);
 }
 
 }  // namespace
