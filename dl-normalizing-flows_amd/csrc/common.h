@@ -12,6 +12,10 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 #define RNVP_LDS __attribute__((address_space(3)))
+// global-memory view of a pointer read from memory (a descriptor table):
+// accesses through it compile to global_* instead of flat_* operations (a
+// flat operation also counts on lgkmcnt, so LDS waits wait for it as well)
+#define RNVP_GLOBAL __attribute__((address_space(1)))
 
 __device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 __device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
@@ -275,6 +279,46 @@ __device__ __forceinline__ void shard_finish(const ShardLoads<U>& L, int nc, dou
     __syncthreads();
 }
 
+// Affine parameters of channel c0 + threadIdx.x, loaded into registers with
+// a prologue's other loads (bn_aff_issue) so that the table finish below
+// waits on no global load.  No branch: an absent gamma / beta reads `any` (a
+// valid global address of the same launch, value unused) and the finish
+// applies the default 1 / 0.
+struct BnAff { float g, b; };
+__device__ __forceinline__ BnAff bn_aff_issue(const rnvp_bn_src& s, int C, int c0, const void* any) {
+    const int c = max(0, min(c0 + (int)threadIdx.x, C - 1));
+    const float* gp = s.gamma ? s.gamma : (const float*)any;
+    const float* bp = s.beta ? s.beta : (const float*)any;
+    return BnAff{gp[s.gamma ? c : 0], bp[s.beta ? c : 0]};
+}
+
+// one channel of the BN table (i < nv: a real channel; else padding)
+__device__ __forceinline__ void bn_finish_entry(const rnvp_bn_src& s, int c, int i, int nc, int nv, const double* tmp,
+                                                float g, float b, float* scale, float* shift, float* mean_out,
+                                                float* rstd_out) {
+    float sc = 0.f, sf = 0.f, mo = 0.f, ro = 1.f;
+    if (i < nv) {
+        double mean, var;
+        if (s.sums) {
+            mean = tmp[i] / s.count;
+            var = tmp[nc + i] / s.count - mean * mean;
+            if (var < 0) var = 0;
+        } else {
+            mean = s.mean[c];
+            var = s.var[c];
+        }
+        const float rstd = (float)(1.0 / sqrt(var + (double)s.eps));
+        sc = g * rstd;
+        sf = b - (float)mean * g * rstd;
+        mo = (float)mean;
+        ro = rstd;
+    }
+    scale[i] = sc;
+    shift[i] = sf;
+    if (mean_out) mean_out[i] = mo;
+    if (rstd_out) rstd_out[i] = ro;
+}
+
 // BN table for channels [c0, c0+nc) from already-reduced sums tmp[0..nc) /
 // tmp[nc..2nc) (train) or the running stats (eval): scale/shift such that
 // bn(x) = x*scale + shift, plus mean / rstd when requested.  Channels >= C
@@ -284,30 +328,23 @@ __device__ __forceinline__ void block_bn_finish(const rnvp_bn_src& s, int C, int
     const int nv = max(0, min(nc, C - c0));
     for (int i = threadIdx.x; i < nc; i += blockDim.x) {
         const int c = c0 + i;
-        float sc = 0.f, sf = 0.f, mo = 0.f, ro = 1.f;
-        if (i < nv) {
-            double mean, var;
-            if (s.sums) {
-                mean = tmp[i] / s.count;
-                var = tmp[nc + i] / s.count - mean * mean;
-                if (var < 0) var = 0;
-            } else {
-                mean = s.mean[c];
-                var = s.var[c];
-            }
-            const float rstd = (float)(1.0 / sqrt(var + (double)s.eps));
-            const float g = s.gamma ? s.gamma[c] : 1.f;
-            const float b = s.beta ? s.beta[c] : 0.f;
-            sc = g * rstd;
-            sf = b - (float)mean * g * rstd;
-            mo = (float)mean;
-            ro = rstd;
-        }
-        scale[i] = sc;
-        shift[i] = sf;
-        if (mean_out) mean_out[i] = mo;
-        if (rstd_out) rstd_out[i] = ro;
+        const float g = (i < nv && s.gamma) ? s.gamma[c] : 1.f;
+        const float b = (i < nv && s.beta) ? s.beta[c] : 0.f;
+        bn_finish_entry(s, c, i, nc, nv, tmp, g, b, scale, shift, mean_out, rstd_out);
     }
+    __syncthreads();
+}
+
+// block_bn_finish for nc <= blockDim.x with the affine parameters in
+// registers (bn_aff_issue(s, C, c0, ...))
+__device__ __forceinline__ void block_bn_finish_aff(const rnvp_bn_src& s, int C, int c0, int nc, float* scale,
+                                                    float* shift, float* mean_out, float* rstd_out, const double* tmp,
+                                                    BnAff A) {
+    const int nv = max(0, min(nc, C - c0));
+    const int i = threadIdx.x;
+    if (i < nc)
+        bn_finish_entry(s, c0 + i, i, nc, nv, tmp, s.gamma ? A.g : 1.f, s.beta ? A.b : 0.f, scale, shift, mean_out,
+                        rstd_out);
     __syncthreads();
 }
 

@@ -1601,10 +1601,16 @@ __device__ __forceinline__ void wn_bwd_tail(const rnvp_wn_desc& d, float* gbase,
     }
     if (d.zero_after) {   // leave the replicas zero for the next atomic accumulation
         __syncthreads();
-        float* dwz = d.dw + (long long)co * d.kp_f;
+        RNVP_GLOBAL float* dwz = (RNVP_GLOBAL float*)(d.dw + (long long)co * d.kp_f);
         const int K = d.ks * d.ks * d.cs_in;
-        for (int z = 0; z < nz; ++z)
-            for (int k = threadIdx.x; k < K; k += blockDim.x) dwz[z * zs + k] = 0.f;
+        if ((K & 3) == 0 && (zs & 3) == 0 && (((uintptr_t)dwz) & 15) == 0) {
+            for (int z = 0; z < nz; ++z)
+                for (int k = 4 * threadIdx.x; k < K; k += 4 * blockDim.x)
+                    *(RNVP_GLOBAL floatx4*)(dwz + z * zs + k) = floatx4{0.f, 0.f, 0.f, 0.f};
+        } else {
+            for (int z = 0; z < nz; ++z)
+                for (int k = threadIdx.x; k < K; k += blockDim.x) dwz[z * zs + k] = 0.f;
+        }
     }
 }
 
@@ -1641,26 +1647,24 @@ __global__ void k_wn_bwd(const rnvp_wn_desc* __restrict__ descs, int n_desc, flo
         constexpr int PT = WN_ROW_LDS / 256, P4 = (WN_ROW_LDS / 4 + 255) / 256;
         const int K4 = kk * d.cs_in / 4;            // cs_in % 8 == 0: a chunk never straddles a tap
         const float rcs = 1.0f / (float)d.cs_in;
+        const RNVP_GLOBAL float* vg = (const RNVP_GLOBAL float*)v;
         float vr[PT];
 #pragma unroll
         for (int j = 0; j < PT; ++j) {
             const int i = threadIdx.x + j * 256;
-            vr[j] = v[i < kr ? i : 0];
+            vr[j] = vg[i < kr ? i : 0];
         }
         float4 cw[P4];
 #pragma unroll
         for (int j = 0; j < P4; ++j) {
             const int q4 = threadIdx.x + j * 256;
-            const float4* src = (const float4*)dw + (q4 < K4 ? q4 : 0);
-            float4 t = src[0];
+            const RNVP_GLOBAL floatx4* src = (const RNVP_GLOBAL floatx4*)dw + (q4 < K4 ? q4 : 0);
+            floatx4 t = src[0];
 #pragma unroll
             for (int z = 1; z < 8; ++z) {
-                if (z < nz) {
-                    const float4 u = src[z * zs / 4];
-                    t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
-                }
+                if (z < nz) t += src[z * zs / 4];
             }
-            cw[j] = t;
+            cw[j] = float4{t.x, t.y, t.z, t.w};
         }
 #pragma unroll
         for (int j = 0; j < P4; ++j) {
@@ -1683,7 +1687,7 @@ __global__ void k_wn_bwd(const rnvp_wn_desc* __restrict__ descs, int n_desc, flo
             dot += (double)dr[j] * vr[j];
         }
         dot = block_sum(dot, red);
-        float* dv = gbase + d.dv_off + (long long)co * kr;
+        RNVP_GLOBAL float* dv = (RNVP_GLOBAL float*)(gbase + d.dv_off + (long long)co * kr);
         if (d.g) {
             const float nrm = d.norm[co];
             const float gs = d.g[co] / nrm;

@@ -187,6 +187,12 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
     const bool epi_pre = epi_bn && a.epi.sums && shard_fits(min(NC, N), a.epi.shards, 2);
     if (pro_pre) shard_issue<2>(a.pro.sums, a.cin, a.pro.shards, 0, pnv, pro_l);
     if (epi_pre) shard_issue<2>(a.epi.sums, N, a.epi.shards, 0, min(NC, N), epi_l);
+    // the tables' affine parameters and the bias, in the same batch (no
+    // global round trip left between the reductions and the first band)
+    static_assert(NC <= NTH, "one table channel per thread");
+    const BnAff pro_a = bn_aff_issue(a.pro, a.cin, 0, a.w);
+    const BnAff epi_a = bn_aff_issue(a.epi, N, 0, a.w);
+    const float bias_v = (a.bias ? a.bias : (const float*)a.w)[a.bias ? max(0, min(tid, N - 1)) : 0];
     stage_load(b0);
     const T* Wg = (const T*)a.w;
     constexpr int wcpr = KPL / CH, wtot = NC * wcpr, kv = NSTEP * KS;
@@ -202,7 +208,7 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
     if (PRO) {
         if (pro_pre) {
             shard_finish<2>(pro_l, cs, tmp, tmp + cs);   // channels >= pnv stay zero (block_bn_finish pads them)
-            block_bn_finish(a.pro, a.cin, 0, cs, bnp, bnp + cs, nullptr, nullptr, tmp);
+            block_bn_finish_aff(a.pro, a.cin, 0, cs, bnp, bnp + cs, nullptr, nullptr, tmp, pro_a);
         } else {
             block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + cs, nullptr, nullptr, tmp);
         }
@@ -210,7 +216,7 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
     if (epi_bn) {
         if (epi_pre) {
             shard_finish<2>(epi_l, NC, tmp, tmp + NC);
-            block_bn_finish(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp);
+            block_bn_finish_aff(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp, epi_a);
         } else {
             block_bn_table(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp);
         }
@@ -223,7 +229,7 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
             *(u32x4*)(Wl + r * kpl + c * CH) = wv[u];
         }
     }
-    for (int n = tid; n < NC; n += NTH) btab[n] = (a.bias && n < N) ? a.bias[n] : 0.f;
+    if (tid < NC) btab[tid] = (a.bias && tid < N) ? bias_v : 0.f;
     for (int c = tid * CH; c < pitch; c += NTH * CH) *(u32x4*)(zrow + c) = u32x4{0u, 0u, 0u, 0u};
     __syncthreads();
     BAND_STAMP(1);

@@ -413,8 +413,19 @@ int rnvp_conv_s1_launch(const rnvp_conv_args* a, hipStream_t s);
 
 // fan-out groups of 1x1 convs sharing one input at the wide scales (conv_s1.hip):
 // the M > 16k branch of rnvp_net_group_prepare / rnvp_net_group (klass bit 12)
+// A group's members travel BY VALUE in the kernel arguments (2.2 KB):
+// pointers a kernel reads from its argument segment are known to address
+// global memory (global_load / global_store).  Read from a device table they
+// were generic -- flat operations, which count on lgkmcnt as well as vmcnt, so
+// every LDS wait of a tile also waited for its global loads and stores.
+struct rnvp_group_kargs {
+    rnvp_conv_args conv[RNVP_NET_GROUP_MAX];
+    int shards[RNVP_NET_GROUP_MAX], tiles[RNVP_NET_GROUP_MAX], xa[RNVP_NET_GROUP_MAX], xb[RNVP_NET_GROUP_MAX];
+    int n;
+};
+rnvp_group_kargs group_kargs(const rnvp_net_step* steps, int n);
 int rnvp_s1_fanout_prepare(rnvp_net_step* steps, int n, int* klass, int* grid, int* lds_bytes);
-int rnvp_s1_fanout_launch(const rnvp_net_step* steps, int n, int klass, int grid, int lds_bytes, hipStream_t s);
+int rnvp_s1_fanout_launch(const rnvp_group_kargs& g, int klass, int grid, int lds_bytes, hipStream_t s);
 
 // persistent band kernel for the wide-scale 3x3 convs (conv_band.hip):
 // RNVP_E_UNSUPPORTED outside 3x3 / 17..64 outputs / cs_in <= 64 / 32k <= M < 2^21

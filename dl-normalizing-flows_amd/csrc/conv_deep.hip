@@ -101,21 +101,20 @@ int launch_cfg(const rnvp_conv_args* a, hipStream_t s, int cfg) {
 // (block b -> the conv whose tile range holds b; every conv keeps its own
 // XCD-aware tile order).  Both prologue forms are compiled in.
 template <typename T, int BN, int NW, int WK, int DK, int NC>
-__global__ __launch_bounds__(64 * NW) void k_net_group(const rnvp_net_step* __restrict__ steps, int n) {
+__global__ __launch_bounds__(64 * NW) void k_net_group(const rnvp_group_kargs g) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     int b = blockIdx.x, c = 0;
-    while (c + 1 < n && b >= steps[c].tiles) {   // uniform scan over <= RNVP_NET_GROUP_MAX tile counts
-        b -= steps[c].tiles;
+    while (c + 1 < g.n && b >= g.tiles[c]) {   // uniform scan over <= RNVP_NET_GROUP_MAX tile counts
+        b -= g.tiles[c];
         ++c;
     }
-    const rnvp_net_step& st = steps[c];
-    if (st.conv.pro_bn_relu)
-        deep_tile<T, BN, 1, true, NW, WK, DK, NC>(st.conv, st.shards, st.xa, st.xb, b, st.tiles, lds);
+    if (g.conv[c].pro_bn_relu)
+        deep_tile<T, BN, 1, true, NW, WK, DK, NC>(g.conv[c], g.shards[c], g.xa[c], g.xb[c], b, g.tiles[c], lds);
     else
-        deep_tile<T, BN, 1, false, NW, WK, DK, NC>(st.conv, st.shards, st.xa, st.xb, b, st.tiles, lds);
+        deep_tile<T, BN, 1, false, NW, WK, DK, NC>(g.conv[c], g.shards[c], g.xa[c], g.xb[c], b, g.tiles[c], lds);
 }
 
-using GroupKernel = void (*)(const rnvp_net_step*, int);
+using GroupKernel = void (*)(const rnvp_group_kargs);
 
 template <typename T, int BN, int NW, int WK, int DK>
 GroupKernel group_kernel_nc(int nc) {
@@ -224,19 +223,33 @@ extern "C" int rnvp_net_group_prepare(rnvp_net_step* steps, int n, int* klass, i
     return group_kernel(a0.dtype, *klass) ? RNVP_OK : RNVP_E_UNSUPPORTED;
 }
 
+rnvp_group_kargs group_kargs(const rnvp_net_step* steps, int n) {
+    rnvp_group_kargs g = {};
+    for (int i = 0; i < n; ++i) {
+        g.conv[i] = steps[i].conv;
+        g.shards[i] = steps[i].shards;
+        g.tiles[i] = steps[i].tiles;
+        g.xa[i] = steps[i].xa;
+        g.xb[i] = steps[i].xb;
+    }
+    g.n = n;
+    return g;
+}
+
 extern "C" int rnvp_net_group(const rnvp_net_step* steps, int n, int dtype, int klass, int grid, int lds_bytes,
                               void* stream) {
     if (!steps || n <= 0 || n > RNVP_NET_GROUP_MAX || grid <= 0 || lds_bytes < 0 || lds_bytes > 160 * 1024)
         return RNVP_E_INVALID;
     if (dtype != RNVP_F32 && dtype != RNVP_BF16) return RNVP_E_INVALID;
+    const rnvp_group_kargs g = group_kargs(steps, n);
     if (klass & (1 << 12)) {
         if (dtype != RNVP_BF16 || n < 2) return RNVP_E_INVALID;
-        return rnvp_s1_fanout_launch(steps, n, klass, grid, lds_bytes, (hipStream_t)stream);
+        return rnvp_s1_fanout_launch(g, klass, grid, lds_bytes, (hipStream_t)stream);
     }
     const GroupKernel k = group_kernel(dtype, klass);
     if (!k) return RNVP_E_INVALID;
     const int nw = group_cfg_shape(klass & 15).nw;
-    hipLaunchKernelGGL(k, dim3(grid), dim3(64 * nw), lds_bytes, (hipStream_t)stream, steps, n);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(64 * nw), lds_bytes, (hipStream_t)stream, g);
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
 }

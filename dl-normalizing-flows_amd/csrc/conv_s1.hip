@@ -48,6 +48,9 @@ __global__ __launch_bounds__(256, (s1_min_blocks<NT, NKS, NOPS>())) void k_conv_
     const bool epi_pre = epi_bn && a.epi.sums && shard_fits(min(NC, N), a.epi.shards, 4);
     if (pro_pre) shard_issue<4>(a.pro.sums, a.cin, a.pro.shards, 0, pnv, pro_l);
     if (epi_pre) shard_issue<4>(a.epi.sums, N, a.epi.shards, 0, min(NC, N), epi_l);
+    // the tables' affine parameters in the same batch (cs, NC <= 64 < 256)
+    const BnAff pro_a = bn_aff_issue(a.pro, a.cin, 0, a.w);
+    const BnAff epi_a = bn_aff_issue(a.epi, N, 0, a.w);
 
     // ---- per-lane constants: weights, prologue coefficients, bias ----
     const bf16_t* __restrict__ Wg = (const bf16_t*)a.w;
@@ -216,7 +219,7 @@ __global__ __launch_bounds__(256, (s1_min_blocks<NT, NKS, NOPS>())) void k_conv_
     if (pro) {
         if (pro_pre) {
             shard_finish<4>(pro_l, cs, tmp, tmp + cs);
-            block_bn_finish(a.pro, a.cin, 0, cs, bnp, bnp + 64, nullptr, nullptr, tmp);
+            block_bn_finish_aff(a.pro, a.cin, 0, cs, bnp, bnp + 64, nullptr, nullptr, tmp, pro_a);
         } else {
             block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + 64, nullptr, nullptr, tmp);
         }
@@ -224,7 +227,7 @@ __global__ __launch_bounds__(256, (s1_min_blocks<NT, NKS, NOPS>())) void k_conv_
     if (epi_bn) {
         if (epi_pre) {
             shard_finish<4>(epi_l, NC, tmp, tmp + NC);
-            block_bn_finish(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp);
+            block_bn_finish_aff(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp, epi_a);
         } else {
             block_bn_table(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp);
         }
@@ -313,25 +316,26 @@ int launch_s1_ops(const rnvp_conv_args* a, hipStream_t s) {
 constexpr int FAN_MAX = 8;
 
 template <int NT, int NKS, int TW>
-__global__ __launch_bounds__(256, 2) void k_s1_fanout(const rnvp_net_step* __restrict__ steps, int nm) {
+__global__ __launch_bounds__(256, 2) void k_s1_fanout(const rnvp_group_kargs gk) {
     constexpr int CH = 8, KS = 32, NC = 16 * NT, KL = lds_mfma_pitch(NKS * KS, CH);   // LDS weight row pitch
     extern __shared__ __attribute__((aligned(16))) char lds[];
+    const int nm = gk.n;
     bf16_t* Wl = (bf16_t*)lds;                                   // [nm][NC][KL]
     float* bnp = (float*)(Wl + nm * NC * KL);                    // [nm][2][64] prologue scale | shift
     float* btab = bnp + nm * 128;                                // [nm][NC] bias
     double* red = (double*)(btab + nm * NC);                     // [4 waves][NC][2]
     double* tmp = red + 4 * NC * 2;                              // [128] BN-table scratch
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, li = lane & 15;
-    const rnvp_conv_args& a0 = steps[0].conv;
+    const rnvp_conv_args& a0 = gk.conv[0];
     const int M = a0.B * a0.H * a0.W;
     const int cs = a0.cs_in;
     int sm = -1;                                                 // the member with statistics
     for (int c = 0; c < nm; ++c)
-        if (steps[c].conv.out_sums) sm = c;
+        if (gk.conv[c].out_sums) sm = c;
 
     // ---- weights, bias, prologue tables -> LDS (once per workgroup) ----
     for (int c = 0; c < nm; ++c) {
-        const rnvp_conv_args& a = steps[c].conv;
+        const rnvp_conv_args& a = gk.conv[c];
         const bf16_t* Wg = (const bf16_t*)a.w;
         for (int q = tid; q < NC * (NKS * KS / CH); q += 256) {
             const int r = q / (NKS * KS / CH), ch = q - r * (NKS * KS / CH);
@@ -369,7 +373,7 @@ __global__ __launch_bounds__(256, 2) void k_s1_fanout(const rnvp_net_step* __res
     };
     auto run = [&](int t, const u32x4 (&X)[TW][NKS]) __attribute__((always_inline)) {
         for (int c = 0; c < nm; ++c) {
-            const rnvp_conv_args& a = steps[c].conv;
+            const rnvp_conv_args& a = gk.conv[c];
             const bool pro = a.pro_bn_relu != 0;
             const int cso = a.cs_out, N = a.n;
             floatx4 acc[TW][NT];
@@ -445,7 +449,7 @@ __global__ __launch_bounds__(256, 2) void k_s1_fanout(const rnvp_net_step* __res
         t += nwaves;
     }
     if (sm >= 0) {
-        const rnvp_conv_args& a = steps[sm].conv;
+        const rnvp_conv_args& a = gk.conv[sm];
 #pragma unroll
         for (int j = 0; j < NT; ++j)
 #pragma unroll
@@ -457,7 +461,7 @@ __global__ __launch_bounds__(256, 2) void k_s1_fanout(const rnvp_net_step* __res
                 }
             }
         __syncthreads();
-        double* sums = shard_ptr(a.out_sums, steps[sm].shards, a.n);
+        double* sums = shard_ptr(a.out_sums, gk.shards[sm], a.n);
         for (int n = tid; n < a.n; n += 256) {
             double t1 = 0.0, t2 = 0.0;
 #pragma unroll
@@ -471,7 +475,7 @@ __global__ __launch_bounds__(256, 2) void k_s1_fanout(const rnvp_net_step* __res
     }
 }
 
-using FanKernel = void (*)(const rnvp_net_step*, int);
+using FanKernel = void (*)(const rnvp_group_kargs);
 
 FanKernel fan_kernel(int nt, int nks) {
     if (nt == 1) return nks == 1 ? k_s1_fanout<1, 1, 4> : k_s1_fanout<1, 2, 4>;
@@ -523,9 +527,9 @@ int rnvp_s1_fanout_prepare(rnvp_net_step* steps, int n, int* klass, int* grid, i
     return RNVP_OK;
 }
 
-int rnvp_s1_fanout_launch(const rnvp_net_step* steps, int n, int klass, int grid, int lds_bytes, hipStream_t s) {
+int rnvp_s1_fanout_launch(const rnvp_group_kargs& g, int klass, int grid, int lds_bytes, hipStream_t s) {
     const FanKernel k = fan_kernel((klass >> 4) & 15, klass & 15);
-    hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds_bytes, s, steps, n);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds_bytes, s, g);
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
 }

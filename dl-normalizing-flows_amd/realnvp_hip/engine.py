@@ -174,7 +174,8 @@ def plan_launches(steps, device, rw=None):
     a run of mutually independent 1x1 convs (rw[i] = (buffers read, buffers
     written) of step i) that rnvp_net_group_prepare accepts becomes one
     grouped launch (rnvp_net_group); the rest stay single launches.
-    Returns [("group", i0, i1, klass, grid, lds, device table) | ("single", i)]."""
+    Returns [("group", i0, i1, klass, grid, lds, host table) | ("single", i)];
+    the host table (a NetStep array) travels by value in the kernel arguments."""
     L = _lib.lib()
     out = []
     n = len(steps)
@@ -195,7 +196,7 @@ def plan_launches(steps, device, rw=None):
                 j += 1
             if best is not None:
                 j, arr, k, g, lb = best
-                out.append(("group", i, j, k, g, lb, upload(bytes(arr), device)))
+                out.append(("group", i, j, k, g, lb, arr))
                 i = j
                 continue
         out.append(("single", i))
@@ -467,7 +468,7 @@ class CouplingEngine:
                 _, i0, i1, klass, grid, lds, tab = g
                 nb = sum(args[i][1] for i in range(i0, i1))
                 fl = sum(args[i][2] for i in range(i0, i1))
-                _launch("conv_fwd", nb, fl, L.net_group, tab.data_ptr(), i1 - i0, dt, klass, grid, lds, s)
+                _launch("conv_fwd", nb, fl, L.net_group, C.addressof(tab), i1 - i0, dt, klass, grid, lds, s)
 
     def _fwd_args(self, T, sv, ws, training):
         ar = sv["arena"]
@@ -784,7 +785,7 @@ class CouplingEngine:
                 _, i0, i1, klass, grid, lds, tab = g
                 nb = sum(items[i][2] for i in range(i0, i1))
                 fl = sum(items[i][3] for i in range(i0, i1))
-                _launch("conv_dgrad", nb, fl, L.net_group, tab.data_ptr(), i1 - i0, dt, klass, grid, lds, s)
+                _launch("conv_dgrad", nb, fl, L.net_group, C.addressof(tab), i1 - i0, dt, klass, grid, lds, s)
         # in_bn backward closes the critical path (dL/dx of the coupling) ...
         a.gh0, a.cs_gh0 = sar.ptr("g:h0"), chan_stride(self.P.buf_ch["h0"])
         a.in_bwd_sums = sar.ptr("in_bwd_sums")

@@ -361,10 +361,14 @@ typedef struct rnvp_net_step {
  * Steps are rnvp_net_step with kind RNVP_STEP_CONV (rnvp_conv2d semantics,
  * with or without the BN prologue).  rnvp_net_group_prepare (host) validates
  * and fills the derived fields (RNVP_E_UNSUPPORTED: no grouped form -- launch
- * them one by one); rnvp_net_group launches the device copy. */
+ * them one by one); rnvp_net_group launches the filled HOST table: the
+ * members travel by value in the kernel arguments (pointers read from the
+ * argument segment address global memory; read from a device table they
+ * would be generic, flat operations).  The table may be reused or freed as
+ * soon as the call returns (stream capture records the arguments). */
 #define RNVP_NET_GROUP_MAX 8
 int rnvp_net_group_prepare(rnvp_net_step* steps_host, int n, int* klass, int* grid, int* lds_bytes);
-int rnvp_net_group(const rnvp_net_step* steps_device, int n, int dtype, int klass, int grid, int lds_bytes,
+int rnvp_net_group(const rnvp_net_step* steps_host, int n, int dtype, int klass, int grid, int lds_bytes,
                    void* stream);
 
 /* misc */

@@ -116,7 +116,7 @@ def test_group_c_abi_two_skip_convs():
     and torch"""
     from realnvp_hip import _lib
     from realnvp_hip._lib import BNSrc, ConvArgs, NetStep
-    from realnvp_hip.engine import stat_shards, upload
+    from realnvp_hip.engine import stat_shards
     L = _lib.lib()
     B, H, W, Cc = 64, 4, 4, 512
     M = B * H * W
@@ -151,8 +151,7 @@ def test_group_c_abi_two_skip_convs():
                 st.kind, st.conv, st.dgamma_off, st.dbeta_off = 0, a, -1, -1
             k, g, lb = C.c_int(), C.c_int(), C.c_int()
             assert L.net_group_prepare(steps, 2, C.byref(k), C.byref(g), C.byref(lb)) == 0
-            tab = upload(bytes(steps), DEV)
-            L.net_group(tab.data_ptr(), 2, 0, k.value, g.value, lb.value, s)
+            L.net_group(C.addressof(steps), 2, 0, k.value, g.value, lb.value, s)
         else:
             L.conv2d(C.byref(a1), s)
             L.conv2d(C.byref(a2), s)
