@@ -285,7 +285,9 @@ int launch_s1(const rnvp_conv_args* a, hipStream_t s) {
             n = 1;
         return n;
     }();
-    long long grid = (ntiles + 3) / 4;
+    // RNVP_S1_TPW: tiles per wave (A/B knob; 1 = every wave one tile)
+    static const int tpw = [] { const char* e = getenv("RNVP_S1_TPW"); const int v = e ? atoi(e) : 1; return v < 1 ? 1 : v; }();
+    long long grid = (ntiles + 4LL * tpw - 1) / (4LL * tpw);
     if (grid > 256LL * per_cu) grid = 256LL * per_cu;
     k_conv_s1<NT, NKS, TW, NOPS><<<(unsigned)grid, 256, 0, s>>>(*a, rnvp_stat_shards(M));
     RNVP_LAUNCH_CHECK();
