@@ -276,6 +276,9 @@ int rnvp_deep_auto_cfg(const rnvp_conv_args* a) {
     const int kc = a->dtype == RNVP_F32 ? 16 : 32;   // channels per k-step
     if (M <= 1024) return a->cs_in % (8 * kc) == 0 ? 4 : 0;
     if (dgrad) return 0;
+    // RNVP_DEEP_FWD32=1: 32-channel tiles for the forward convs as well (A/B)
+    static const int fwd32 = [] { const char* e = getenv("RNVP_DEEP_FWD32"); return e ? atoi(e) : 0; }();
+    if (fwd32) return a->cs_in % (8 * kc) == 0 ? 4 : 0;
     return a->cs_in % (8 * kc) == 0 ? 5 : 1;
 }
 
