@@ -21,6 +21,7 @@ MI355X-specific structure:
   * optimizer state converts to / from torch.optim.Adam.state_dict() format
     (train.py:139-154, 249-250 checkpoints).
 """
+import gc
 import math
 import os
 
@@ -130,6 +131,7 @@ class FlowTrainer:
             raise ValueError("reduce_dtype must be 'fp32' or 'bf16'")
         self.comm, self.reduce_dtype = comm, reduce_dtype
         self._reduce_pg = None
+        self._comm_off = False
         self.comm_events = None
         self.comm_stream = None
         if self.pg is not None and comm == "overlap":
@@ -283,7 +285,10 @@ class FlowTrainer:
             self.reduce_buf = torch.empty(self.n, device=self.dev, dtype=torch.bfloat16)
 
     def _reduce_bucket(self, lo, hi):
-        """Average grad[lo:hi) over the process group (on the current stream)."""
+        """Average grad[lo:hi) over the process group (on the current stream).
+        No-op during capture()'s warm-up steps (see capture)."""
+        if self._comm_off:
+            return
         from .dist import average_slice
         pg = self._reduce_pg if self._reduce_pg is not None else self.pg
         average_slice(self.grad, lo, hi, pg, self.reduce_buf)
@@ -524,17 +529,51 @@ class FlowTrainer:
         Single process, and data parallel with comm="overlap": ONE graph
         holds forward, backward, the bucketed all-reduces on the
         communication stream and Adam.  comm="split": forward/backward graph,
-        eager all-reduce, optimizer graph."""
+        eager all-reduce, optimizer graph.
+
+        Nothing but the captured step's own work runs while a capture is
+        open (the round-4 abort: SIGABRT from a thread without a Python
+        frame in the middle of a capture):
+          * the warm-up steps issue no collective (their state is restored,
+            so with a process group restore must be True);
+          * the captured all-reduces use a capture-only group (_capture_group);
+          * unreachable objects are collected and their HIP teardown drained
+            before the capture, and the garbage collector is off during it,
+            so no graph / event / stream of another object is destroyed
+            mid-capture.
+        tools/probe/capture_watchdog.py showed that a c10d watchdog polling a
+        finished eager all-reduce during a thread-local capture does NOT
+        abort on this stack, so a pending watchdog entry alone is not the
+        cause; the construction above removes every other thread-visible
+        event of the window."""
+        if self.pg is not None and not restore:
+            raise ValueError("with a process group, capture() must restore the warm-up state: its warm-up "
+                             "steps issue no all-reduce (see capture)")
         snap = self._snapshot() if restore else None
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            for _ in range(warmup):
-                self.step_eager()
+        # The warm-up steps issue NO collective: their state is discarded
+        # (restore) and a collective issued here would sit on its group's
+        # watchdog list when the capture opens (see _wait_collectives_retired)
+        self._comm_off = True
+        try:
+            with torch.cuda.stream(side):
+                for _ in range(warmup):
+                    self.step_eager()
+        finally:
+            self._comm_off = False
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
+        # Destroy unreachable objects (earlier trainers' graphs, events,
+        # streams) NOW and let the HIP work their destruction queues drain,
+        # and run no garbage collection while the capture is open: a cyclic
+        # collection triggered by any allocation inside the capture would
+        # otherwise destroy HIP graphs / events / streams of other objects in
+        # the middle of it (see capture's note on the round-4 abort)
+        gc.collect()
+        torch.cuda.synchronize()
         # the captured all-reduces go through a group of their own (see
-        # _capture_group); warm-up and eager collectives stay on self.pg
+        # _capture_group); eager collectives stay on self.pg
         if before_capture is not None:
             before_capture()
         self.graph = torch.cuda.CUDAGraph()
@@ -544,20 +583,26 @@ class FlowTrainer:
         # against our capture (HIP still refuses an event query meanwhile,
         # hence the drain above)
         mode = "thread_local"
-        if self.pg is None or self.comm_stream is not None:
-            try:
-                self._reduce_pg = self._cap_pg
+        gc_on = gc.isenabled()
+        gc.disable()
+        try:
+            if self.pg is None or self.comm_stream is not None:
+                try:
+                    self._reduce_pg = self._cap_pg
+                    with torch.cuda.graph(self.graph, capture_error_mode=mode):
+                        self._fwd_bwd()
+                        self._optimizer()
+                finally:
+                    self._reduce_pg = None
+            else:
                 with torch.cuda.graph(self.graph, capture_error_mode=mode):
                     self._fwd_bwd()
+                self.graph_opt = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.graph_opt, capture_error_mode=mode):
                     self._optimizer()
-            finally:
-                self._reduce_pg = None
-        else:
-            with torch.cuda.graph(self.graph, capture_error_mode=mode):
-                self._fwd_bwd()
-            self.graph_opt = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph_opt, capture_error_mode=mode):
-                self._optimizer()
+        finally:
+            if gc_on:
+                gc.enable()
         torch.cuda.synchronize()
         if snap is not None:
             self._restore(snap)

@@ -192,6 +192,27 @@ def test_process_group_step_matches_single_process(nccl_world1, comm, graph, sid
     np.testing.assert_allclose(tr.mean_logll(1), ref.mean_logll(1), rtol=1e-6)
 
 
+def test_capture_issues_no_eager_collective(nccl_world1, monkeypatch):
+    """capture() warm-up steps issue no all-reduce, and the captured ones go
+    over the capture-only group: no eager collective can be on a watchdog's
+    list while the capture is open (trainer._wait_collectives_retired)."""
+    import realnvp_hip.dist as D
+    from realnvp_hip.trainer import FlowTrainer
+    calls = []
+    real = D.average_slice
+
+    def spy(flat, lo, hi, group=None, buf=None):
+        calls.append((group, torch.cuda.is_current_stream_capturing()))
+        return real(flat, lo, hi, group, buf)
+    monkeypatch.setattr(D, "average_slice", spy)
+    tr = FlowTrainer(make_model(32, 8, 1), 4, dtype="fp32", process_group=nccl_world1, bucket_mb=1)
+    tr.set_pixels(pixels(4, 3, 32, seed=5).to(DEV))
+    tr.capture(warmup=2)
+    assert calls and all(cap and g is tr._cap_pg for g, cap in calls), calls
+    with pytest.raises(ValueError):
+        tr.capture(warmup=1, restore=False)
+
+
 def test_process_group_bf16_reduction(nccl_world1):
     ref, _ = _one_step(make_model(32, 8, 1))
     tr, _ = _one_step(make_model(32, 8, 1), pg=nccl_world1, comm="overlap", reduce_dtype="bf16", bucket_mb=1)

@@ -1,0 +1,39 @@
+#!/bin/bash
+# Round-5 GPU jobs, one per call: bash tools/gpu_r5.sh <job> [TAG]
+# Every GPU step runs under its own limit; the job stops at the first failure.
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+JOB=$1
+O=gpurun_out/${2:-r5_$JOB}
+mkdir -p $O
+R=$GRAFT_REPO_ROOT
+step() { local log=$1; shift; "$@" > $O/$log 2>&1; local rc=$?; echo "$log rc=$rc"; tail -${TAILN:-4} $O/$log; if [ $rc -ne 0 ]; then exit $rc; fi; }
+PYT="python -u -m pytest -m gpu -q -rf --timeout 300 --timeout-method thread"
+bench() { step bench$1.log timeout -k 10 300 python3 -u bench.py --steps ${STEPS:-30} --warmup 5 --no-cpu-baseline --no-secondary; }
+trace() {
+  step prof.log timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof -o run -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-secondary
+  local f=$(find $O/prof -name '*kernel_trace.csv' | head -1)
+  TAILN=${TRACEN:-60} step step.txt python3 tools/step_dump.py $f
+  cp $O/prof/run_kernel_stats.csv $O/kernel_stats.csv 2>/dev/null; rm -rf $O/prof
+}
+case $JOB in
+  watchdog)
+    # capture fix: probe (drained), the whole trainer module, bench + trace; then the
+    # un-drained probe LAST (the hypothesis is that it aborts)
+    step probe_drained.log timeout -k 10 120 python3 -u tools/probe/capture_watchdog.py drained
+    TAILN=8 step pytest_trainer.log timeout -k 10 900 $PYT tests/test_gpu_trainer.py
+    bench
+    trace
+    TAILN=30 step probe_pending.log timeout -k 10 120 python3 -u tools/probe/capture_watchdog.py pending
+    ;;
+  tests)
+    TAILN=8 step pytest.log timeout -k 10 900 $PYT ${TFILES:-tests} ${TK:+-k "$TK"}
+    ;;
+  iter)
+    [ -n "$TFILES" ] && TAILN=8 step pytest.log timeout -k 10 900 $PYT $TFILES ${TK:+-k "$TK"}
+    bench
+    [ -n "$TRACE" ] && trace
+    ;;
+  *) echo "unknown job $JOB"; exit 2;;
+esac
+exit 0
