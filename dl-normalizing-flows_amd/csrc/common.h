@@ -77,6 +77,29 @@ __device__ __forceinline__ void st4(bf16_t* p, const float* v) {
     *(uint2*)p = t;
 }
 
+// store through a global-memory view (pointers read from descriptor tables)
+__device__ __forceinline__ void stg(float* p, float v) { *(RNVP_GLOBAL float*)p = v; }
+__device__ __forceinline__ void stg(bf16_t* p, float v) { *(RNVP_GLOBAL bf16_t*)p = f2bf(v); }
+
+// one element of torch.optim.Adam (single-tensor form, coupled L2 weight
+// decay, train.py:134); f = 2 adds the 5e-5 * weight_scale regulariser's
+// gradient 2*reg*p (train.py:194).  m, v updated in place; returns p'.
+// step_size = lr / (1 - b1^t), inv_bc2s = 1 / sqrt(1 - b2^t).
+// Every multiply-add is an explicit fmaf and no other product feeds an
+// addition, so no FMA contraction is left to the compiler: the kernels that
+// inline this (k_adam, k_adam_gather, k_wn_adam) compute bitwise the same
+// update from the same operands.
+__device__ __forceinline__ float adam_elem(float p, float g, float& m, float& v, int f, float b1, float b2, float eps,
+                                           float wd, float reg, float step_size, float inv_bc2s) {
+    float gr = fmaf(wd, p, g);
+    if (f == 2) gr = fmaf(2.f * reg, p, gr);
+    m = fmaf(1.f - b1, gr - m, m);
+    const float t = (1.f - b2) * gr;
+    v = fmaf(v, b2, t * gr);
+    const float den = fmaf(sqrtf(v), inv_bc2s, eps);
+    return p - (step_size * m) / den;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

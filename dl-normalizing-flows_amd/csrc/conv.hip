@@ -1495,9 +1495,9 @@ __global__ __launch_bounds__(256) void k_wn_norm(const rnvp_wn_desc* __restrict_
 #pragma unroll
         for (int u = 0; u < 8; ++u) x[u] = v[i + u * 64];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) ss += (double)x[u] * x[u];
+        for (int u = 0; u < 8; ++u) ss = fma((double)x[u], (double)x[u], ss);
     }
-    for (; i < kr; i += 64) ss += (double)v[i] * v[i];
+    for (; i < kr; i += 64) ss = fma((double)v[i], (double)v[i], ss);
     ss = wave_sum(ss);
     if (lane == 0) d.norm[co] = (float)sqrt(ss);
 }
@@ -1684,7 +1684,7 @@ __global__ void k_wn_bwd(const rnvp_wn_desc* __restrict__ descs, int n_desc, flo
         for (int j = 0; j < PT; ++j) {
             const int i = threadIdx.x + j * 256;
             dr[j] = i < kr ? rowbuf[i] : 0.f;
-            dot += (double)dr[j] * vr[j];
+            dot = fma((double)dr[j], (double)vr[j], dot);
         }
         dot = block_sum(dot, red);
         RNVP_GLOBAL float* dv = (RNVP_GLOBAL float*)(gbase + d.dv_off + (long long)co * kr);
@@ -1695,7 +1695,7 @@ __global__ void k_wn_bwd(const rnvp_wn_desc* __restrict__ descs, int n_desc, flo
 #pragma unroll
             for (int j = 0; j < PT; ++j) {
                 const int i = threadIdx.x + j * 256;
-                if (i < kr) dv[i] = gs * (dr[j] - proj * vr[j]);
+                if (i < kr) dv[i] = gs * fmaf(-proj, vr[j], dr[j]);
             }
             if (threadIdx.x == 0 && d.dg_off >= 0) gbase[d.dg_off + co] = (float)(dot / nrm);
         } else {
@@ -1723,14 +1723,14 @@ __global__ void k_wn_bwd(const rnvp_wn_desc* __restrict__ descs, int n_desc, flo
         return dw_at(tap * d.cs_in + ci);
     };
     double dot = 0;
-    for (int i = threadIdx.x; i < kr; i += blockDim.x) dot += (double)dwv(i) * v[i];
+    for (int i = threadIdx.x; i < kr; i += blockDim.x) dot = fma((double)dwv(i), (double)v[i], dot);
     dot = block_sum(dot, red);
     float* dv = gbase + d.dv_off + (long long)co * kr;
     if (d.g) {
         const float nrm = d.norm[co];
         const float gs = d.g[co] / nrm;
         const float proj = (float)(dot / ((double)nrm * nrm));
-        for (int i = threadIdx.x; i < kr; i += blockDim.x) dv[i] = gs * (dwv(i) - proj * v[i]);
+        for (int i = threadIdx.x; i < kr; i += blockDim.x) dv[i] = gs * fmaf(-proj, v[i], dwv(i));
         if (threadIdx.x == 0 && d.dg_off >= 0) gbase[d.dg_off + co] = (float)(dot / nrm);
     } else {
         for (int i = threadIdx.x; i < kr; i += blockDim.x) dv[i] = dwv(i);

@@ -420,12 +420,7 @@ __global__ void k_adam(float4* __restrict__ p, const float4* __restrict__ g, flo
         for (int j = 0; j < 4; ++j) {
             const uint32_t f = (mk >> (8 * j)) & 0xff;
             if (f == 0) continue;                      // frozen parameter
-            float gr = ga[j] + wd * pa[j];
-            if (f == 2) gr += 2.f * reg * pa[j];       // weight_scale regulariser
-            ma[j] = ma[j] + (1.f - b1) * (gr - ma[j]);
-            va[j] = va[j] * b2 + (1.f - b2) * gr * gr;
-            float den = sqrtf(va[j]) * inv_bc2s + eps;
-            pa[j] = pa[j] - step_size * ma[j] / den;
+            pa[j] = adam_elem(pa[j], ga[j], ma[j], va[j], (int)f, b1, b2, eps, wd, reg, step_size, inv_bc2s);
         }
         p[i] = pp; m[i] = mm; v[i] = vv;
     }

@@ -62,7 +62,14 @@ class WNDesc(C.Structure):
                 ("dw", vp), ("dv_off", i64), ("dg_off", i64),
                 ("cout", i32), ("cin", i32), ("ks", i32), ("cs_in", i32), ("kp_f", i32),
                 ("cs_out", i32), ("kp_d", i32), ("row0", i32), ("tile0", i32),
-                ("nz", i32), ("dbp", vp), ("db_off", i64), ("zero_after", i32)]
+                ("nz", i32), ("dbp", vp), ("db_off", i64), ("zero_after", i32), ("blk0", i32)]
+
+
+class AdamArgs(C.Structure):
+    _fields_ = [("param", vp), ("grad", vp), ("exp_avg", vp), ("exp_avg_sq", vp), ("mask", vp),
+                ("step", vp), ("step_add", i64),
+                ("lr", f32), ("beta1", f32), ("beta2", f32), ("eps", f32), ("weight_decay", f32),
+                ("reg_coef", f32)]
 
 
 WGRAD_GROUP_MAX = 24
@@ -132,6 +139,9 @@ _SIGS = {
     "rnvp_weight_norm_fwd": (i32, [vp, i32, i32, i32, i32, vp]),
     "rnvp_weight_norm_tiles": (i32, [i32, i32, i32]),
     "rnvp_weight_norm_bwd": (i32, [vp, i32, i32, vp, vp, i64, vp, i64, vp]),
+    "rnvp_weight_norm_opt_blocks": (i32, [i32, i32, i32]),
+    "rnvp_weight_norm_bwd_adam": (i32, [vp, i32, i32, i32, i32, C.POINTER(AdamArgs), vp, i64, vp, i64, vp]),
+    "rnvp_adam_gather": (i32, [C.POINTER(AdamArgs), vp, i64, vp]),
     "rnvp_coupling_in_fwd": (i32, [C.POINTER(CouplingArgs), vp]),
     "rnvp_coupling_out_fwd": (i32, [C.POINTER(CouplingArgs), vp]),
     "rnvp_coupling_reverse": (i32, [C.POINTER(CouplingArgs), vp]),
@@ -162,7 +172,7 @@ class _Lib:
             fn.restype = res
             fn.argtypes = args
             raw = name in ("rnvp_version", "rnvp_stat_shards", "rnvp_wgrad_slabs", "rnvp_wgrad_replicas",
-                           "rnvp_weight_norm_tiles",
+                           "rnvp_weight_norm_tiles", "rnvp_weight_norm_opt_blocks",
                            "rnvp_net_group_prepare") or res is not i32
             setattr(self, name[len("rnvp_"):], fn if raw else self._wrap(name, fn))
 

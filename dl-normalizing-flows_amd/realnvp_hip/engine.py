@@ -264,7 +264,7 @@ class CouplingEngine:
             ar.add("norm:" + name, spec.cout * 4)
         ar.alloc(dev, zero=True)   # zero padding of the packed images, once
         descs = []
-        row0 = tile0 = 0
+        row0 = tile0 = blk0 = 0
         for name, spec in self.P.convs.items():
             cs_in, cs_out, kp_f, kp_d = geo[name]
             vn, gn, _ = self._conv_names(spec)
@@ -279,12 +279,19 @@ class CouplingEngine:
                 spec.cout, spec.cin, spec.ks, cs_in, kp_f, cs_out, kp_d, row0)
             d.nz = 1
             d.tile0 = tile0
+            _, _, bname = self._conv_names(spec)
+            d.db_off = self.layout[bname][0] if bname else -1
+            d.blk0 = blk0
+            nb = int(_lib.lib().weight_norm_opt_blocks(spec.cout, spec.cin, spec.ks))
+            blk0 = blk0 + nb if (nb > 0 and blk0 >= 0) else -1
             row0 += spec.cout
             tile0 += wn_tiles(spec.cout, spec.cin, spec.ks)
             descs.append(d)
         table = (WNDesc * len(descs))(*descs)
         dtab = upload(bytes(table), dev)
-        ws = dict(key=key, arena=ar, geo=geo, descs=descs, table=dtab, rows=row0, tiles=tile0, dtype=dtype)
+        # blocks < 0: some conv's rows do not fit the fused parameter pass
+        ws = dict(key=key, arena=ar, geo=geo, descs=descs, table=dtab, rows=row0, tiles=tile0, dtype=dtype,
+                  blocks=blk0)
         self._weights[dtype] = ws
         return ws
 
@@ -348,6 +355,15 @@ class CouplingEngine:
         if len(pool) < 2:
             pool.append(sv)
 
+    def scratch_checked(self, B, H, W, dtype, device):
+        """scratch() rebuilt when the weight set moved since it was made (its
+        weight-norm table points into the packed-weight arena)."""
+        sc = self.scratch(B, H, W, dtype, device)
+        if sc["wn_key"] != self.weights(dtype)["key"]:
+            self._scratch.pop((B, H, W, dtype, str(device)))
+            sc = self.scratch(B, H, W, dtype, device)
+        return sc
+
     def scratch(self, B, H, W, dtype, device):
         key = (B, H, W, dtype, str(device))
         sc = self._scratch.get(key)
@@ -401,14 +417,14 @@ class CouplingEngine:
             e.nz = nrep
             _, _, bname = self._conv_names(spec)
             e.dbp = wbase + 4 * ob if ob is not None else None
-            e.db_off = self.layout[bname][0] if ob is not None else 0
+            e.db_off = self.layout[bname][0] if ob is not None else -1
             e.zero_after = int(nrep < nz)
             descs.append(e)
         tab = (WNDesc * len(descs))(*descs)
         nmax = max(max(chan_stride(s.cin), chan_stride(s.cout)) for s in self.P.convs.values())
         wse = splitk_elems(M, nmax)
         sc = dict(arena=ar, zero=zr, wn_table=upload(bytes(tab), device),
-                  wn_key=wsz["key"], wn_rows=wsz["rows"], n_wn=len(descs), shards=sh,
+                  wn_key=wsz["key"], wn_rows=wsz["rows"], wn_blocks=wsz["blocks"], n_wn=len(descs), shards=sh,
                   ws=splitk_workspace(device, wse) if wse else None, ws_elems=wse,
                   wg=wg, wg_nz=nz, wg_nrep=nrep, wg_ws=wgws)
         self._scratch[key] = sc
@@ -534,6 +550,11 @@ class CouplingEngine:
         if ldj_sample is None:
             ldj_sample = torch.zeros(B, device=dev, dtype=torch.float32)
         ldj_full = torch.empty_like(x) if full_ldj else None
+        if in_done and zero_sums:
+            # the previous coupling's chained out launch already wrote this
+            # coupling's in_sums (closed form, shard 0); zeroing them here
+            # would silently corrupt the in_bn backward
+            raise ValueError("forward(in_done=True) requires zero_sums=False")
         if training and zero_sums:
             s0, e0 = ar.range_bytes("in_sums", list(ar.slots)[-1])
             ar.buf[s0:e0].zero_()
@@ -673,7 +694,7 @@ class CouplingEngine:
         return items, groups, wg_bytes, wg_flops
 
     def backward(self, sv, gz, gl_full, gl_sample, grad_block, gx=None, side=None, after=None, zero_at_end=False,
-                 defer=None, chain_prev=None, sums_ready=False):
+                 defer=None, chain_prev=None, sums_ready=False, opt=None):
         """Returns dL/dx; parameter gradients are written into grad_block
         (flat fp32, zeroed by the caller; scale/shift grads accumulate).
 
@@ -695,7 +716,12 @@ class CouplingEngine:
         zero_at_end: the backward sums are zero on entry (not re-zeroed here)
         and the weight-norm backward launch leaves the forward's batch sums
         zero for the next step too (persistent arenas).  Either way the
-        shared backward scratch is left zero."""
+        shared backward scratch is left zero.
+
+        opt: an AdamArgs over this coupling's block of the trainer's arenas:
+        the weight-norm backward becomes the fused row-local parameter pass
+        (rnvp_weight_norm_bwd_adam: dv/dg/dbias, Adam on every conv row, the
+        new norms and the next step's packed images)."""
         L = _lib.lib()
         x = sv["x"]
         B, H, W, dtype, training = sv["B"], sv["H"], sv["W"], sv["dtype"], sv["training"]
@@ -704,10 +730,7 @@ class CouplingEngine:
         s = stream_ptr()
         T = self._tensors()
         ws = self.weights(dtype)
-        sc = self.scratch(B, H, W, dtype, x.device)
-        if sc["wn_key"] != ws["key"]:
-            self._scratch.pop((B, H, W, dtype, str(x.device)))
-            sc = self.scratch(B, H, W, dtype, x.device)
+        sc = self.scratch_checked(B, H, W, dtype, x.device)
         ar, sar, war = sv["arena"], sc["arena"], ws["arena"]
         z0, z1 = sc["zero"]
         if not zero_at_end:
@@ -794,7 +817,9 @@ class CouplingEngine:
             peng, psv = chain_prev
             pv = peng._coupling_args(peng._tensors(), psv["x"], B, H, W, dtype, training)
             pv.u, pv.out_sums = psv["arena"].ptr("u"), psv["arena"].ptr("out_sums")
-            pv.bwd_sums = peng.scratch(B, H, W, dtype, x.device)["arena"].ptr("bwd_sums")
+            # the previous coupling's backward resolves its scratch the same
+            # way (scratch_checked), so these sums land where it reads them
+            pv.bwd_sums = peng.scratch_checked(B, H, W, dtype, x.device)["arena"].ptr("bwd_sums")
             pv.gl_sample = gl_sample.data_ptr() if gl_sample is not None else None
             # reduction: x, gh0; apply: x, gx (r + w), gh0, and the previous coupling's u
             _launch("coupling", 20 * n_el + 2 * esz * B * H * W * a.cs_gh0, 0.0, L.coupling_in_bwd_chain,
@@ -824,7 +849,11 @@ class CouplingEngine:
                 zr = (ar.base + f0, f1 - f0, sar.base + z0, z1 - z0)
             else:
                 zr = (None, 0, sar.base + z0, z1 - z0)
-            L.weight_norm_bwd(sc["wn_table"].data_ptr(), sc["n_wn"], sc["wn_rows"], gbase, *zr, ss)
+            if opt is not None:
+                L.weight_norm_bwd_adam(sc["wn_table"].data_ptr(), sc["n_wn"], sc["wn_blocks"], 1, dt, C.byref(opt),
+                                       *zr, ss)
+            else:
+                L.weight_norm_bwd(sc["wn_table"].data_ptr(), sc["n_wn"], sc["wn_rows"], gbase, *zr, ss)
             if after is not None:
                 after()
 

@@ -102,7 +102,7 @@ def bucket_plan(model, bucket_elems, n_total):
 class FlowTrainer:
     def __init__(self, model, batch_size, lr=5e-4, weight_decay=5e-5, betas=(0.9, 0.999), eps=1e-8,
                  scale_reg=5e-5, dtype="bf16", seed=0, process_group=None, bucket_mb=25, overlap=False,
-                 comm="overlap", reduce_dtype="fp32"):
+                 comm="overlap", reduce_dtype="fp32", param_pass="fused"):
         self.model = model
         self.dev = next(model.parameters()).device
         if self.dev.type != "cuda":
@@ -147,6 +147,9 @@ class FlowTrainer:
         # (each cross-stream edge of a replayed HIP graph costs a barrier
         # packet between hardware queues)
         self.side_group = int(os.environ.get("RNVP_SIDE_GROUP", "0")) if (overlap and process_group is None) else 0
+        if param_pass not in ("fused", "separate"):
+            raise ValueError("param_pass must be 'fused' or 'separate'")
+        self._build_param_pass(param_pass)
         self._build_adam_ranges()
         self._build_buckets()
         self._cap_pg = self._capture_group()
@@ -248,6 +251,103 @@ class FlowTrainer:
     def _wn_fwd(self, table):
         wn_forward(table, self.dtype)
 
+    # ------------------------------------------------------- parameter pass
+    def _build_param_pass(self, mode):
+        """The fused row-local parameter pass (rnvp_weight_norm_bwd_adam).
+
+        Single process: each coupling's weight-norm backward launch also runs
+        Adam on its conv rows (v, g, bias) and writes the new norms and both
+        packed weight images, so the step has no separate Adam pass over the
+        convs and no weight-norm forward (the images the forward reads were
+        written by the previous step).  Data parallel: the per-coupling
+        weight-norm backward stays (the all-reduce comes between it and Adam)
+        and ONE model-wide launch does Adam + norms + images after the
+        all-reduce.  The arena elements outside the convs (BatchNorm affines,
+        coupling scales: 0.3 % of config 1's parameters) get a gather-Adam.
+        The images are re-derived eagerly (two weight-norm launches) when the
+        parameters changed outside the trainer's own kernels (_packed_token).
+        mode 'separate' keeps weight_norm_fwd + weight_norm_bwd + adam_step."""
+        self.fused = False
+        self._packed_token = None
+        if mode != "fused":
+            return
+        from ._lib import AdamArgs, WNDesc
+        import ctypes as C
+        mask = self.mask.cpu().numpy()
+        covered = np.zeros(self.n, dtype=bool)
+        base = self.grad.data_ptr()
+        model_descs, blk0 = [], 0
+        self._opt_args = {}
+        for st in self.stages:
+            if st[0] != "coupling":
+                continue
+            eng, block = st[2], st[6]
+            off = (block.data_ptr() - base) // 4
+            ws = eng.weights(self.dtype)
+            if ws["blocks"] < 0:
+                return
+            for d in ws["descs"]:
+                kr = d.cin * d.ks * d.ks
+                a = off + d.dv_off
+                if not (mask[a:a + d.cout * kr] == 1).all():
+                    return
+                covered[a:a + d.cout * kr] = True
+                if d.g and d.dg_off >= 0:
+                    covered[off + d.dg_off:off + d.dg_off + d.cout] = True
+                if d.db_off >= 0:
+                    covered[off + d.db_off:off + d.db_off + d.cout] = True
+                e = WNDesc()
+                C.memmove(C.addressof(e), C.addressof(d), C.sizeof(WNDesc))
+                e.dv_off += off
+                e.dg_off = e.dg_off + off if e.dg_off >= 0 else -1
+                e.db_off = e.db_off + off if e.db_off >= 0 else -1
+                e.blk0 += blk0
+                model_descs.append(e)
+            blk0 += ws["blocks"]
+            self._opt_args[id(eng)] = self._adam_args(off)
+        from .engine import upload
+        self._opt_table = (upload(bytes((WNDesc * len(model_descs))(*model_descs)), self.dev), len(model_descs),
+                           blk0)
+        rest = np.nonzero((mask > 0) & ~covered)[0].astype(np.int64)
+        self._opt_rest = torch.from_numpy(rest).to(self.dev)
+        self._opt_all = self._adam_args(0)
+        self._vparams = [p for _, p in self.model.named_parameters()]
+        self.fused = True
+
+    def _adam_args(self, off):
+        from ._lib import AdamArgs
+        a = AdamArgs()
+        a.param, a.grad = self.param.data_ptr() + 4 * off, self.grad.data_ptr() + 4 * off
+        a.exp_avg, a.exp_avg_sq = self.exp_avg.data_ptr() + 4 * off, self.exp_avg_sq.data_ptr() + 4 * off
+        a.mask, a.step, a.step_add = self.mask.data_ptr() + off, self.step_t.data_ptr(), 1
+        a.lr, a.beta1, a.beta2, a.eps = self.lr, self.betas[0], self.betas[1], self.eps
+        a.weight_decay, a.reg_coef = self.wd, self.reg
+        return a
+
+    def _refresh_adam_args(self):
+        """lr / betas / eps / weight decay changed (load_optimizer_state_dict)"""
+        if not self.fused:
+            return
+        for a in list(self._opt_args.values()) + [self._opt_all]:
+            a.lr, a.beta1, a.beta2, a.eps = self.lr, self.betas[0], self.betas[1], self.eps
+            a.weight_decay, a.reg_coef = self.wd, self.reg
+
+    def _token(self):
+        return (self.param._version, sum(p._version for p in self._vparams))
+
+    def _ensure_packed(self):
+        """Fused pass: the packed weight images and norms are the previous
+        step's output; re-derive them (eagerly) when the parameters were
+        changed by anything else (first step, capture's restore,
+        load_state_dict, a caller writing the parameters)."""
+        if not self.fused:
+            return
+        tok = self._token()
+        if tok != self._packed_token:
+            for t in self.wn_tables:
+                self._wn_fwd(t)
+            self._packed_token = tok
+
     def _build_adam_ranges(self):
         """Per-coupling optimizer ranges [ru4(off_i), ru4(off_next)) of the flat
         arena (float4 granules).  A granule straddling two couplings belongs to
@@ -256,7 +356,7 @@ class FlowTrainer:
         when its update runs.  Disabled (one update at the end) unless the
         backward visits couplings in descending arena offset."""
         self.adam_ranges = None
-        if self.pg is not None or not self.overlap:
+        if self.pg is not None or not self.overlap or self.fused:
             return
         blocks = [st[6] for st in self.stages if st[0] == "coupling"]
         base = self.grad.data_ptr()
@@ -356,7 +456,9 @@ class FlowTrainer:
                         self.logdet.data_ptr(), B, n, s)
         self.ldj.zero_()
         late_ready = None
-        if len(self.wn_tables) > 1 and self.side is not None:
+        if self.fused:
+            pass    # the packed images are the previous step's (_ensure_packed)
+        elif len(self.wn_tables) > 1 and self.side is not None:
             ev = torch.cuda.Event()
             ev.record()
             self.side.wait_event(ev)
@@ -413,10 +515,11 @@ class FlowTrainer:
                     lo, hi = self.adam_ranges[ci]
                     after = (lambda lo=lo, hi=hi: self._adam_range(lo, hi))
                 prv = self.stages[i - 1] if self.chain.get(i - 1) is not None else None
+                opt = self._opt_args[id(eng)] if (self.fused and self.pg is None) else None
                 eng.backward(sv, self._g(z), None, self.g_lp, block, gx=self._g(x), side=self.side, after=after,
                              zero_at_end=True, defer=pending if self.side_group else None,
                              chain_prev=None if prv is None else (prv[2], prv[5]),
-                             sums_ready=self.chain[i] is not None)
+                             sums_ready=self.chain[i] is not None, opt=opt)
                 if self.side_group and (len(pending) >= self.side_group or ci == 0):
                     self._flush_side(pending)
                 if self.comm_stream is not None:
@@ -469,6 +572,18 @@ class FlowTrainer:
                                self.mask.data_ptr() + lo, self.reg, stream_ptr())
 
     def _optimizer(self):
+        if self.fused:
+            L = _lib.lib()
+            s = stream_ptr()
+            import ctypes as C
+            if self.pg is not None:
+                # data parallel: the conv rows' Adam + norms + images, after the all-reduce
+                t, n, nblk = self._opt_table
+                L.weight_norm_bwd_adam(t.data_ptr(), n, nblk, 0, 1 if self.dtype == "bf16" else 0,
+                                       C.byref(self._opt_all), None, 0, None, 0, s)
+            L.adam_gather(C.byref(self._opt_all), self._opt_rest.data_ptr(), self._opt_rest.numel(), s)
+            L.step_increment(self.step_t.data_ptr(), s)
+            return
         if self.adam_ranges is not None:
             # the per-coupling updates already ran (side stream, t = step + 1)
             _lib.lib().step_increment(self.step_t.data_ptr(), stream_ptr())
@@ -496,6 +611,7 @@ class FlowTrainer:
             torch.cuda.current_stream().wait_stream(self.comm_stream)
 
     def step_eager(self):
+        self._ensure_packed()
         self._fwd_bwd()
         self._allreduce()
         self._optimizer()
@@ -615,6 +731,7 @@ class FlowTrainer:
     def step(self):
         if self.graph is None:
             return self.step_eager()
+        self._ensure_packed()
         self.graph.replay()
         if self.graph_opt is not None:
             self._allreduce()
@@ -692,6 +809,7 @@ class FlowTrainer:
             raise ValueError("per-parameter Adam step counts differ: %s" % sorted(steps))
         self.step_t.fill_(int(steps.pop()) if steps else 0)
         self.lr, self.betas, self.eps, self.wd = g0["lr"], tuple(g0["betas"]), g0["eps"], g0["weight_decay"]
+        self._refresh_adam_args()
         if self.graph is not None:
             self.drop_graph()    # lr / betas are baked into the captured launches
 

@@ -208,6 +208,7 @@ typedef struct rnvp_wn_desc {
     float* dbp;                        /* bias partials [nz][cout] or NULL */
     long long db_off;                  /* bias gradient offset (elements) */
     int zero_after;                    /* re-zero dw / dbp after use (atomic accumulation) */
+    int blk0;                          /* first row block (prefix sum of rnvp_weight_norm_opt_blocks) */
 } rnvp_wn_desc;
 /* fwd, for any number of convs (a whole model): one launch computes every
  * row norm, one writes both packed images on [32 co] x [32 ci] tiles
@@ -222,6 +223,36 @@ int rnvp_weight_norm_fwd(const rnvp_wn_desc* descs_device, int n_desc, int total
  * left zero for the next step once the coupling's backward has consumed them */
 int rnvp_weight_norm_bwd(const rnvp_wn_desc* descs_device, int n_desc, int total_rows, float* grad_base,
                          void* zero0, long long zero0_bytes, void* zero1, long long zero1_bytes, void* stream);
+
+/* Row-local parameter pass (weight-norm backward + Adam + next weight norm).
+ * One launch per coupling replaces rnvp_weight_norm_bwd + that coupling's
+ * share of rnvp_adam_step + the next step's rnvp_weight_norm_fwd: for every
+ * output row co of every conv in the table, with dv_off / dg_off / db_off
+ * indexing the adam arenas (param, grad, exp_avg, exp_avg_sq, mask):
+ *   from_slabs = 1: dW = sum of the nz slabs, dv / dg / dbias as
+ *     rnvp_weight_norm_bwd (also stored into grad); from_slabs = 0: dv / dg /
+ *     dbias read from grad (data parallel, after the all-reduce);
+ *   Adam (rnvp_adam_update semantics, t = *step + step_add) on the row of v
+ *     (mask 1 assumed: the caller checks), g[co] (when dg_off >= 0) and the
+ *     bias (db_off >= 0; db_off < 0 = no bias), with their mask bytes;
+ *   norm[co] = ||v'||, and both packed images (rnvp_weight_norm_fwd layout)
+ *     of w' = g' v' / ||v'|| for the next step.
+ * blk0: prefix sums of rnvp_weight_norm_opt_blocks(cout, cin, ks) (negative:
+ * the row does not fit the kernel's LDS -- use the unfused calls).
+ * zero0 / zero1 as rnvp_weight_norm_bwd.  Replaces modules_realnvp.py:53-59
+ * (weight_norm) and train.py:134, 200 (Adam) for the s/t convs. */
+typedef struct rnvp_adam_args {
+    float* param; float* grad; float* exp_avg; float* exp_avg_sq; const uint8_t* mask;
+    const long long* step; long long step_add;
+    float lr, beta1, beta2, eps, weight_decay, reg_coef;
+} rnvp_adam_args;
+int rnvp_weight_norm_opt_blocks(int cout, int cin, int ks);
+int rnvp_weight_norm_bwd_adam(const rnvp_wn_desc* descs_device, int n_desc, int total_blocks, int from_slabs,
+                              int dtype, const rnvp_adam_args* adam, void* zero0, long long zero0_bytes,
+                              void* zero1, long long zero1_bytes, void* stream);
+/* Adam on the arena elements idx[0..n) (the parameters outside the convs:
+ * BatchNorm affines, coupling scales, ...), rnvp_adam_update semantics */
+int rnvp_adam_gather(const rnvp_adam_args* adam, const long long* idx, long long n, void* stream);
 
 /* ---- affine coupling (modules_realnvp.py:239-370) -----------------------
  * kind 0 = CheckerboardAffineCoupling, 1 = ChannelwiseAffineCoupling.

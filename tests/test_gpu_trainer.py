@@ -555,3 +555,93 @@ def test_chained_couplings_match_unchained(shape, dtype):
     assert float(((a1 - a0).abs() / a0.abs()).max()) < 1e-3
     assert d(r1, r0) < 1e-3, d(r1, r0)
     assert np.linalg.norm(n1 - n0) / np.linalg.norm(n0) < 6e-2
+
+# ---------------------------------------------------------------------------
+# fused row-local parameter pass (rnvp_weight_norm_bwd_adam) vs the separate
+# weight-norm backward / Adam / weight-norm forward launches
+def _pp_run(mode, dtype, steps=3, pg=None, overlap=False, graph=False, edit_at=None, size=32, bd=8, rb=1):
+    from realnvp_hip.trainer import FlowTrainer
+    tr = FlowTrainer(make_model(size, bd, rb), 4, dtype=dtype, param_pass=mode, process_group=pg, overlap=overlap,
+                     bucket_mb=1)
+    assert tr.fused == (mode == "fused")
+    tr.set_pixels(pixels(4, 3, size, seed=5).to(DEV))
+    if graph:
+        tr.capture(warmup=1)
+    for k in range(steps):
+        if edit_at == k:
+            # a change behind the trainer's back: the packed images must follow
+            with torch.no_grad():
+                for p in tr.model.parameters():
+                    if p.requires_grad:
+                        p.mul_(0.97)
+        tr.step()
+    torch.cuda.synchronize()
+    return tr
+
+
+def _packed_images(tr):
+    out = []
+    for st in tr.stages:
+        if st[0] != "coupling":
+            continue
+        ws = st[2].weights(tr.dtype)
+        dt = torch.bfloat16 if tr.dtype == "bf16" else torch.float32
+        for name in ws["geo"]:
+            for kind in ("wf:", "wd:"):
+                out.append(ws["arena"].view(kind + name, dt).float().clone())
+            out.append(ws["arena"].view("norm:" + name, torch.float32).clone())
+    return out
+
+
+def _rel(a, b):
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def _check_fused_vs_separate(fu, se, se2, what):
+    # summation-order noise of the grouped wgrad's replica atomics, amplified by
+    # Adam's sign flips of near-zero gradients: bounded by the separate path's
+    # own run-to-run scatter (se2 vs se), as test_side_stream_overlap_...
+    for name in ("param", "exp_avg", "exp_avg_sq", "grad"):
+        a, b, b2 = getattr(fu, name), getattr(se, name), getattr(se2, name)
+        assert _rel(a, b) < max(2e-5 if name != "grad" else 1e-4, 8 * _rel(b2, b)), (what, name, _rel(a, b),
+                                                                                      _rel(b2, b))
+    assert int(fu.step_t.item()) == int(se.step_t.item())
+    # the images the next forward reads = weight_norm_fwd of the final parameters
+    img = _packed_images(fu)
+    for t in fu.wn_tables:
+        fu._wn_fwd(t)
+    torch.cuda.synchronize()
+    ref = _packed_images(fu)
+    tol = 1e-6 if fu.dtype == "fp32" else 8e-3    # bf16: 1-ulp flips where the norm's last bit differs
+    for a, b in zip(img, ref):
+        assert float((a - b).abs().max()) <= tol * max(1.0, float(b.abs().max())), what
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("variant", ["eager", "hipgraph", "sidestream", "edited"])
+def test_fused_param_pass_matches_separate(dtype, variant):
+    kw = dict(graph=variant == "hipgraph", overlap=variant == "sidestream", edit_at=1 if variant == "edited" else None)
+    fu = _pp_run("fused", dtype, **kw)
+    se = _pp_run("separate", dtype, **kw)
+    se2 = _pp_run("separate", dtype, **kw)
+    _check_fused_vs_separate(fu, se, se2, (dtype, variant))
+
+
+def test_fused_param_pass_config1_shape():
+    """Config 1's convs (64x64, R4, D32: 3x3 rows of 4,608, 512-channel 1x1s,
+    row blocks of 4 and 8) at batch 4, bf16."""
+    kw = dict(size=64, bd=32, rb=4, steps=2)
+    fu = _pp_run("fused", "bf16", **kw)
+    se = _pp_run("separate", "bf16", **kw)
+    se2 = _pp_run("separate", "bf16", **kw)
+    _check_fused_vs_separate(fu, se, se2, "config1")
+
+
+def test_fused_param_pass_data_parallel(nccl_world1):
+    """Data parallel: per-coupling weight-norm backward, all-reduce, then ONE
+    model-wide Adam + norms + images launch (from_slabs = 0)."""
+    for graph in (False, True):
+        fu = _pp_run("fused", "fp32", pg=nccl_world1, graph=graph)
+        se = _pp_run("separate", "fp32", pg=nccl_world1, graph=graph)
+        se2 = _pp_run("separate", "fp32", pg=nccl_world1, graph=graph)
+        _check_fused_vs_separate(fu, se, se2, ("dp", graph))
