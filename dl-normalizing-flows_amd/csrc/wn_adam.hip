@@ -29,7 +29,22 @@ typedef float floatx2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int WA_THREADS = 512;
-constexpr int WA_LDS = 76 * 1024;      // two workgroups per CU
+#ifndef WA_LDS_KB
+#define WA_LDS_KB 38
+#endif
+#ifndef WA_U
+#define WA_U 2
+#endif
+#ifndef WA_UV
+#define WA_UV 1
+#endif
+#ifndef WA_UD
+#define WA_UD 4
+#endif
+#ifndef WA_WPE
+#define WA_WPE 6
+#endif
+constexpr int WA_LDS = WA_LDS_KB * 1024;   // four workgroups per CU
 
 // LDS floats per tap: a 3x3 row keeps its taps cs_in + 4 apart (banks of the
 // v-order accesses tap*P + ci skew by 4 per tap; rows stay 16-byte aligned)
@@ -102,7 +117,7 @@ __device__ __forceinline__ void wd_runs(const rnvp_wn_desc& d, const float* tile
 }
 
 template <typename T, bool SLABS>
-__global__ __launch_bounds__(WA_THREADS) void k_wn_adam(const rnvp_wn_desc* __restrict__ descs, int n_desc,
+__global__ __launch_bounds__(WA_THREADS) __attribute__((amdgpu_waves_per_eu(WA_WPE, 8))) void k_wn_adam(const rnvp_wn_desc* __restrict__ descs, int n_desc,
                                                         rnvp_adam_args ad, int nblk, double* z0, long long n0,
                                                         double* z1, long long n1) {
     if ((int)blockIdx.x >= nblk) {   // extra workgroups: zero the caller's sums ranges
@@ -144,16 +159,30 @@ __global__ __launch_bounds__(WA_THREADS) void k_wn_adam(const rnvp_wn_desc* __re
     const float rkk = 1.0f / (float)kk;
     const int nz = d.nz > 0 ? d.nz : 1;
     const long long zs = (long long)d.cout * d.kp_f;
-    // ---- phase 0: dW row (sum of the nz replica slabs) into LDS, packed-k order
+    // ---- phase 0: dW row (sum of the nz replica slabs) into LDS, packed-k order.
+    // Loops below issue U iterations' loads before using any of them (loads
+    // past the end are clamped to the iteration's first element and their
+    // results -- identical -- stored twice), so every lane keeps several
+    // memory round trips in flight; no load sits under a branch.
+    constexpr int U = WA_U;
     if (SLABS && live) {
         const int K4 = kk * d.cs_in / 4;           // cs_in % 8 == 0: a chunk never straddles a tap
         const float rcs = 1.0f / (float)d.cs_in;
         const RNVP_GLOBAL floatx4* src = (const RNVP_GLOBAL floatx4*)(d.dw + (long long)co * d.kp_f);
-        for (int q4 = tr; q4 < K4; q4 += tpr) {
-            floatx4 t = src[q4];
-            for (int z = 1; z < nz; ++z) t += src[q4 + z * zs / 4];
-            const int k = 4 * q4, tap = fdiv_small(k, rcs), ci = k - tap * d.cs_in;
-            *(floatx4*)(trow + tap * P + ci) = t;
+        for (int q0 = tr; q0 < K4; q0 += U * tpr) {
+            floatx4 t[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) t[u] = src[q0 + u * tpr < K4 ? q0 + u * tpr : q0];
+            for (int z = 1; z < nz; ++z) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) t[u] += src[(q0 + u * tpr < K4 ? q0 + u * tpr : q0) + z * zs / 4];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int q4 = q0 + u * tpr < K4 ? q0 + u * tpr : q0;
+                const int k = 4 * q4, tap = fdiv_small(k, rcs), ci = k - tap * d.cs_in;
+                *(floatx4*)(trow + tap * P + ci) = t[u];
+            }
         }
     }
     __syncthreads();
@@ -168,12 +197,21 @@ __global__ __launch_bounds__(WA_THREADS) void k_wn_adam(const rnvp_wn_desc* __re
     const int lane = threadIdx.x & 63, pw = (threadIdx.x >> 6) % wpr;
     double dot = 0.0;
     if (SLABS && d.g) {
+        constexpr int UD = WA_UD;
         for (int vw = pw; vw < 4; vw += wpr) {
             double acc = 0.0;
             if (live) {
-                for (int i = lane + 64 * vw; i < kr; i += 256) {
-                    const int ci = fdiv_small(i, rkk), tap = i - ci * kk;
-                    acc = fma((double)trow[tap * P + ci], (double)pv[i], acc);
+                for (int i0 = lane + 64 * vw; i0 < kr; i0 += 256 * UD) {
+                    float x[UD];
+#pragma unroll
+                    for (int u = 0; u < UD; ++u) x[u] = pv[i0 + 256 * u < kr ? i0 + 256 * u : i0];
+#pragma unroll
+                    for (int u = 0; u < UD; ++u) {
+                        const int i = i0 + 256 * u < kr ? i0 + 256 * u : i0;
+                        const int ci = fdiv_small(i, rkk), tap = i - ci * kk;
+                        const double t = fma((double)trow[tap * P + ci], (double)x[u], acc);
+                        acc = i0 + 256 * u < kr ? t : acc;
+                    }
                 }
             }
             acc = wave_sum(acc);
@@ -183,28 +221,80 @@ __global__ __launch_bounds__(WA_THREADS) void k_wn_adam(const rnvp_wn_desc* __re
         dot = 0.0;
         for (int vw = 0; vw < 4; ++vw) dot += red[r * 4 + vw];
     }
-    // ---- phase 1b: dv, Adam, v' into LDS
+    // ---- phase 1b: dv, Adam, v' into LDS.  Element-wise (any mapping gives
+    // the same bits): the 16-byte-aligned body of the row in float4 chunks,
+    // the 0-3 element head and tail (the arenas' rows need not be aligned)
+    // one element per lane
     if (live) {
         const float gs = gold / nrm;
         const float proj = (float)(dot / ((double)nrm * nrm));
-        for (int i = tr; i < kr; i += tpr) {
+        auto elem = [&](int i, float p, float gin, float& m, float& v2, float dwv, float& g) {
+            g = SLABS ? (d.g ? gs * fmaf(-proj, p, dwv) : dwv) : gin;
+            return adam_elem(p, g, m, v2, 1, ad.beta1, ad.beta2, ad.eps, ad.weight_decay, ad.reg_coef, step_size,
+                             inv_bc2s);
+        };
+        auto lds_at = [&](int i) {
             const int ci = fdiv_small(i, rkk), tap = i - ci * kk;
-            const float p = pv[i];
-            float g;
-            if (SLABS) {
-                const float dw = trow[tap * P + ci];
-                g = d.g ? gs * fmaf(-proj, p, dw) : dw;
-                gv[i] = g;
-            } else {
-                g = gv[i];
-            }
-            float m = mv[i], s = sv[i];
-            const float pn = adam_elem(p, g, m, s, 1, ad.beta1, ad.beta2, ad.eps, ad.weight_decay, ad.reg_coef,
-                                       step_size, inv_bc2s);
+            return tap * P + ci;
+        };
+        const int h = min(kr, (int)((4 - (vrow & 3)) & 3));
+        const int nb4 = (kr - h) >> 2, t0 = h + 4 * nb4;
+        if (tr < h + (kr - t0)) {     // head / tail: at most 6 scalar elements
+            const int i = tr < h ? tr : t0 + (tr - h);
+            const int l = lds_at(i);
+            float m = mv[i], v2 = sv[i], g = SLABS ? 0.f : gv[i];
+            const float pn = elem(i, pv[i], g, m, v2, SLABS ? trow[l] : 0.f, g);
+            if (SLABS) gv[i] = g;
             pv[i] = pn;
             mv[i] = m;
-            sv[i] = s;
-            trow[tap * P + ci] = pn;
+            sv[i] = v2;
+            trow[l] = pn;
+        }
+        RNVP_GLOBAL floatx4* p4 = (RNVP_GLOBAL floatx4*)(pv + h);
+        RNVP_GLOBAL floatx4* g4 = (RNVP_GLOBAL floatx4*)(gv + h);
+        RNVP_GLOBAL floatx4* m4 = (RNVP_GLOBAL floatx4*)(mv + h);
+        RNVP_GLOBAL floatx4* s4 = (RNVP_GLOBAL floatx4*)(sv + h);
+        constexpr int UV = WA_UV;
+        for (int c0 = tr; c0 < nb4; c0 += UV * tpr) {
+            // every operand (LDS dW included) is read before the first store:
+            // a clamped duplicate must see the old values
+            floatx4 P4[UV], M4[UV], S4[UV], G4[UV];
+            float DW[UV][4];
+#pragma unroll
+            for (int u = 0; u < UV; ++u) {
+                const int c = c0 + u * tpr < nb4 ? c0 + u * tpr : c0;
+                P4[u] = p4[c];
+                M4[u] = m4[c];
+                S4[u] = s4[c];
+                if (!SLABS) G4[u] = g4[c];
+            }
+            if (SLABS) {
+#pragma unroll
+                for (int u = 0; u < UV; ++u) {
+                    const int c = c0 + u * tpr < nb4 ? c0 + u * tpr : c0;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) DW[u][e] = trow[lds_at(h + 4 * c + e)];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < UV; ++u) {
+                const int c = c0 + u * tpr < nb4 ? c0 + u * tpr : c0;
+                floatx4 pn, go;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float m = M4[u][e], v2 = S4[u][e], g;
+                    pn[e] = elem(h + 4 * c + e, P4[u][e], SLABS ? 0.f : G4[u][e], m, v2, SLABS ? DW[u][e] : 0.f, g);
+                    M4[u][e] = m;
+                    S4[u][e] = v2;
+                    go[e] = g;
+                }
+                if (SLABS) g4[c] = go;
+                p4[c] = pn;
+                m4[c] = M4[u];
+                s4[c] = S4[u];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) trow[lds_at(h + 4 * c + e)] = pn[e];
+            }
         }
     }
     __syncthreads();

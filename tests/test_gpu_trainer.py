@@ -597,14 +597,26 @@ def _rel(a, b):
     return float((a - b).norm() / b.norm().clamp_min(1e-30))
 
 
-def _check_fused_vs_separate(fu, se, se2, what):
-    # summation-order noise of the grouped wgrad's replica atomics, amplified by
-    # Adam's sign flips of near-zero gradients: bounded by the separate path's
-    # own run-to-run scatter (se2 vs se), as test_side_stream_overlap_...
-    for name in ("param", "exp_avg", "exp_avg_sq", "grad"):
-        a, b, b2 = getattr(fu, name), getattr(se, name), getattr(se2, name)
-        assert _rel(a, b) < max(2e-5 if name != "grad" else 1e-4, 8 * _rel(b2, b)), (what, name, _rel(a, b),
-                                                                                      _rel(b2, b))
+def _check_fused_vs_separate(fu, se, se2, what, steps=3):
+    """bf16: the separate path is deterministic (its weight gradients are
+    plain stores) and the fused pass computes every quantity in the separate
+    kernels' operation order (explicit FMAs, the same reduction orders), so
+    the two trajectories must agree BITWISE.  fp32: the grouped weight
+    gradient adds slab partials with atomics, so gradients that are zero in
+    exact arithmetic (a conv bias followed by a BatchNorm) are rounding noise
+    whose sign Adam turns into +-lr steps: the checks are those of
+    test_side_stream_overlap_matches_single_stream."""
+    if fu.dtype == "bf16":
+        for name in ("param", "exp_avg", "exp_avg_sq", "grad"):
+            a, b, b2 = getattr(fu, name), getattr(se, name), getattr(se2, name)
+            assert torch.equal(b2, b), (what, name, "separate bf16 path not deterministic")
+            assert torch.equal(a, b), (what, name, _rel(a, b), int((a != b).sum()))
+    else:
+        for name in ("exp_avg", "grad"):
+            a, b, b2 = getattr(fu, name), getattr(se, name), getattr(se2, name)
+            assert _rel(a, b) < max(1e-2, 8 * _rel(b2, b)), (what, name, _rel(a, b), _rel(b2, b))
+        assert float((fu.param - se.param).abs().max()) <= steps * 2 * se.lr * 1.01, what
+        assert _rel(fu.param, se.param) < max(1e-3, 4 * _rel(se2.param, se.param)), what
     assert int(fu.step_t.item()) == int(se.step_t.item())
     # the images the next forward reads = weight_norm_fwd of the final parameters
     img = _packed_images(fu)
@@ -612,9 +624,8 @@ def _check_fused_vs_separate(fu, se, se2, what):
         fu._wn_fwd(t)
     torch.cuda.synchronize()
     ref = _packed_images(fu)
-    tol = 1e-6 if fu.dtype == "fp32" else 8e-3    # bf16: 1-ulp flips where the norm's last bit differs
     for a, b in zip(img, ref):
-        assert float((a - b).abs().max()) <= tol * max(1.0, float(b.abs().max())), what
+        assert torch.equal(a, b), what
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
@@ -634,14 +645,15 @@ def test_fused_param_pass_config1_shape():
     fu = _pp_run("fused", "bf16", **kw)
     se = _pp_run("separate", "bf16", **kw)
     se2 = _pp_run("separate", "bf16", **kw)
-    _check_fused_vs_separate(fu, se, se2, "config1")
+    _check_fused_vs_separate(fu, se, se2, "config1", steps=2)
 
 
 def test_fused_param_pass_data_parallel(nccl_world1):
     """Data parallel: per-coupling weight-norm backward, all-reduce, then ONE
     model-wide Adam + norms + images launch (from_slabs = 0)."""
-    for graph in (False, True):
-        fu = _pp_run("fused", "fp32", pg=nccl_world1, graph=graph)
-        se = _pp_run("separate", "fp32", pg=nccl_world1, graph=graph)
-        se2 = _pp_run("separate", "fp32", pg=nccl_world1, graph=graph)
-        _check_fused_vs_separate(fu, se, se2, ("dp", graph))
+    for dtype in ("bf16", "fp32"):
+        for graph in (False, True):
+            fu = _pp_run("fused", dtype, pg=nccl_world1, graph=graph)
+            se = _pp_run("separate", dtype, pg=nccl_world1, graph=graph)
+            se2 = _pp_run("separate", dtype, pg=nccl_world1, graph=graph)
+            _check_fused_vs_separate(fu, se, se2, ("dp", dtype, graph))

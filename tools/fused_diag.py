@@ -1,7 +1,7 @@
 """GPU diagnostic: the fused parameter pass against the separate launches, one
 step at a time, per named parameter and per packed image.
 
-    python3 tools/fused_diag.py [size bd rb dtype steps]
+    python3 tools/fused_diag.py [size bd rb dtype steps [graph]]
 """
 import os
 import sys
@@ -47,7 +47,11 @@ def main():
     size, bd, rb = (int(a) for a in sys.argv[1:4]) if len(sys.argv) > 3 else (64, 32, 4)
     dtype = sys.argv[4] if len(sys.argv) > 4 else "bf16"
     steps = int(sys.argv[5]) if len(sys.argv) > 5 else 1
+    graph = len(sys.argv) > 6 and sys.argv[6] == "graph"
     fu, se = make(size, bd, rb, dtype, "fused"), make(size, bd, rb, dtype, "separate")
+    if graph:
+        fu.capture(warmup=1)
+        se.capture(warmup=1)
     names = [n for n, _ in fu.model.named_parameters()]
     for step in range(steps):
         fu.step()
@@ -72,6 +76,9 @@ def main():
             fu._wn_fwd(t)
         torch.cuda.synchronize()
         imr = images(fu)
+        ims = images(se)
+        nd = sum(1 for k, (a, b) in enumerate(zip(imr.values(), ims.values())) if not torch.equal(a, b))
+        print("images: wn_fwd(fused params) vs separate's own:", nd, "differ")
         nb = 0
         for key in imf:
             d = (imf[key] - imr[key]).abs()
