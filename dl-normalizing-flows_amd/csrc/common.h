@@ -302,6 +302,39 @@ __device__ __forceinline__ void shard_finish(const ShardLoads<U>& L, int nc, dou
     __syncthreads();
 }
 
+// shard_finish without zeroing and without LDS atomics: every thread parks
+// its loaded entries in tab (2 * U * blockDim.x doubles of LDS) at their
+// entry index h * nc + c, ONE barrier, then thread c < nc adds channel c's
+// shards in shard order into s1[c] / s2[c] (deterministic).  No branch and no
+// loop sits between the shard loads and their first use, so the wait for
+// them counts only the loads issued before them (the tile loads a kernel
+// issued after them stay in flight).  The sums are left for the SAME thread
+// (block_bn_finish_aff reads entry threadIdx.x): no trailing barrier.
+// Needs nc <= blockDim.x and shard_fits(nc, shards, U).
+template <int U>
+__device__ __forceinline__ void shard_sum_tab(const ShardLoads<U>& L, int nc, int shards, double* tab, double* s1,
+                                              double* s2) {
+    const int n = U * blockDim.x;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int t = u * blockDim.x + threadIdx.x;
+        tab[t] = L.v1[u];
+        tab[n + t] = L.v2[u];
+    }
+    __syncthreads();
+    const int i = threadIdx.x;
+    if (i < nc) {
+        const int hs = shards < 1 ? 1 : shards;
+        double a = 0.0, b = 0.0;
+        for (int h = 0; h < hs; ++h) {
+            a += tab[h * nc + i];
+            b += tab[n + h * nc + i];
+        }
+        s1[i] = a;
+        s2[i] = b;
+    }
+}
+
 // Affine parameters of channel c0 + threadIdx.x, loaded into registers with
 // a prologue's other loads (bn_aff_issue) so that the table finish below
 // waits on no global load.  No branch: an absent gamma / beta reads `any` (a

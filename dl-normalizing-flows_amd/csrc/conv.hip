@@ -1127,16 +1127,12 @@ int launch_band(const rnvp_conv_args* a, hipStream_t s) {
     const size_t shm = band_lds_bytes<T>(a->cs_in, a->n, a->W, KSZ);
     const int sh = rnvp_stat_shards(M);
     // eight waves for the 3x3 (64 channels: 23.76 vs 24.03 ms per step; 32
-    // channels: 23.71 vs 23.79); RNVP_BAND_NH / RNVP_BAND_NH2 = 1 keep four
-    static const int nh_env = [] { const char* e = getenv("RNVP_BAND_NH"); return e ? atoi(e) : 2; }();
-    static const int nh2_env = [] { const char* e = getenv("RNVP_BAND_NH2"); return e ? atoi(e) : 2; }();
+    // channels: 23.71 vs 23.79)
     if constexpr ((NT == 4 || NT == 2) && KSZ == 3) {
-        if ((NT == 4 ? nh_env : nh2_env) == 2) {
-            if (a->pro_bn_relu) k_conv_band<T, NT, KSZ, true, 2><<<grid, 512, shm, s>>>(*a, sh);
-            else k_conv_band<T, NT, KSZ, false, 2><<<grid, 512, shm, s>>>(*a, sh);
-            RNVP_LAUNCH_CHECK();
-            return RNVP_OK;
-        }
+        if (a->pro_bn_relu) k_conv_band<T, NT, KSZ, true, 2><<<grid, 512, shm, s>>>(*a, sh);
+        else k_conv_band<T, NT, KSZ, false, 2><<<grid, 512, shm, s>>>(*a, sh);
+        RNVP_LAUNCH_CHECK();
+        return RNVP_OK;
     }
     if (a->pro_bn_relu) k_conv_band<T, NT, KSZ, true, 1><<<grid, 256, shm, s>>>(*a, sh);
     else k_conv_band<T, NT, KSZ, false, 1><<<grid, 256, shm, s>>>(*a, sh);
@@ -1180,10 +1176,8 @@ int dispatch_conv(const rnvp_conv_args* a, hipStream_t s) {
         }
     }
     const bool tuned = a->variant != 1;
-    // bf16 1x1 convs of the wide scales: the register-pipelined stream kernel
-    // (conv_s1.hip; RNVP_CONV_STREAM=0 restores the round-2 stream kernel)
-    static const int smode = [] { const char* e = getenv("RNVP_CONV_STREAM"); return e ? atoi(e) : 1; }();
-    if (tuned && smode && a->dtype == RNVP_BF16 && a->ks == 1) {
+    // bf16 1x1 convs of the wide scales: the register-pipelined stream kernel (conv_s1.hip)
+    if (tuned && a->dtype == RNVP_BF16 && a->ks == 1) {
         const int r = rnvp_conv_s1_launch(a, s);
         if (r != RNVP_E_UNSUPPORTED) return r;
     }
@@ -1775,10 +1769,8 @@ extern "C" int rnvp_conv2d_wgrad_grouped(const rnvp_wgrad_group* gin, void* stre
     if (gin->dtype != RNVP_F32 && gin->dtype != RNVP_BF16) return RNVP_E_INVALID;
     if (gin->B < 0 || gin->H <= 0 || gin->W <= 0) return RNVP_E_INVALID;
     if (gin->B == 0) return RNVP_OK;
-    // bf16: the tap-shared kernel (wgrad_tap.hip) where it applies;
-    // RNVP_WGRAD=0 forces the per-tap kernel below (A/B diagnostics)
-    static const int wmode = [] { const char* e = getenv("RNVP_WGRAD"); return e ? atoi(e) : 1; }();
-    if (wmode == 1 && gin->dtype == RNVP_BF16) {
+    // bf16: the tap-shared kernel (wgrad_tap.hip) where it applies
+    if (gin->dtype == RNVP_BF16) {
         for (int c = 0; c < gin->n_conv; ++c) {
             const rnvp_wgrad_conv& v = gin->conv[c];
             if (!v.x || !v.dy || !v.ws) return RNVP_E_INVALID;

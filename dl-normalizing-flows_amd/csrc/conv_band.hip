@@ -469,13 +469,11 @@ int dispatch_band2_cs(const rnvp_conv_args* a, hipStream_t s) {
     // only); 256-pixel bands while that leaves >= 2 bands per workgroup.
     // 64 outputs: wave pairs split the channels, weights read from LDS per
     // step (in registers they would take 144 VGPRs).
-    static const int tm64 = [] { const char* e = getenv("RNVP_BAND2_TM64"); return e ? atoi(e) : 2; }();
     constexpr bool WR = CS <= 32;   // 36-72 VGPRs of weights (64 channels: 144)
     if (a->n <= 32) {
         if (b256 >= 512) return launch_band2<T, 2, 2, CS, 1, WR>(a, s);
         return launch_band2<T, 2, 1, CS, 1, WR>(a, s);
     }
-    if (tm64 == 4) return launch_band2<T, 4, 4, CS, 2, false>(a, s);
     return launch_band2<T, 4, 2, CS, 2, false>(a, s);
 }
 
@@ -495,8 +493,6 @@ int dispatch_band2(const rnvp_conv_args* a, hipStream_t s) {
 // 3x3, 17..64 outputs, cs_in <= 64 with a fixed chunk column per thread,
 // 32k <= M < 2^21: the persistent band kernel (RNVP_E_UNSUPPORTED otherwise)
 int rnvp_conv_band2_launch(const rnvp_conv_args* a, hipStream_t s) {
-    static const int mode = [] { const char* e = getenv("RNVP_BAND2"); return e ? atoi(e) : 1; }();
-    if (!mode) return RNVP_E_UNSUPPORTED;
     const long long M = (long long)a->B * a->H * a->W;
     if (a->ks != 3 || a->n <= 16 || a->n > 64 || a->cs_in > 64 || a->cs_out > 64) return RNVP_E_UNSUPPORTED;
     if (M < 32768 || M >= (1ll << 21)) return RNVP_E_UNSUPPORTED;

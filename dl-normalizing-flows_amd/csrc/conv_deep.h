@@ -347,10 +347,8 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
 // bytes (xa activation tiles + xb weight slices) are smallest: that is what
 // one XCD's L2 has to bring in.
 inline void xcd_blocks(const rnvp_conv_args* a, int gm, int gn, int bn, int esz, int* xa, int* xb) {
-    static const int mode = [] { const char* e = getenv("RNVP_DEEP_XMAP"); return e ? atoi(e) : 2; }();
-    *xa = mode == 0 ? 0 : -1;
+    *xa = -1;
     *xb = 1;
-    if (mode != 2) return;
     const long long per = (long long)gm * gn / 8;
     const int hal = (a->ks / 2) * (a->W + 1);
     const double act = (double)(DEEP_BM + 2 * hal) * a->cs_in * esz;

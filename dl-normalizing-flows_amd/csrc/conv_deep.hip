@@ -261,13 +261,10 @@ extern "C" int rnvp_net_group(const rnvp_net_step* steps, int n, int dtype, int 
 // Round 3 (prologue loads trimmed): 1x1 up to M = 4096 and 3x3 up to
 // M = 16384 as well -- step 26.47 -> 26.03 ms (profiles/r3_dispatch_ab.txt);
 // 1x1 up to 16384 later (23.70 -> 23.64 ms, three alternating pairs).
-// RNVP_DEEP_MAXM1 / RNVP_DEEP_MAXM3: the largest M the family takes for 1x1
-// (cfg 0 up to 1024, cfg 1 above) / 3x3 convs (A/B of the dispatch limits)
+// The family takes 1x1 and 3x3 convs up to M = 16384 pixels.
 int rnvp_deep_auto_cfg(const rnvp_conv_args* a) {
-    static const long long max1 = [] { const char* e = getenv("RNVP_DEEP_MAXM1"); return e ? atoll(e) : 16384ll; }();
-    static const long long max3 = [] { const char* e = getenv("RNVP_DEEP_MAXM3"); return e ? atoll(e) : 16384ll; }();
     const long long M = (long long)a->B * a->H * a->W;
-    if (M > (a->ks == 3 ? max3 : max1)) return -1;
+    if (M > 16384) return -1;
     // per-shape choice from tools/conv_microbench.py --deep
     // (profiles/r3_deep_microbench_cfgs.txt): the 8-wave tiles at M <= 1024;
     // 32-channel tiles for the data gradients above (more workgroups); the
@@ -276,9 +273,8 @@ int rnvp_deep_auto_cfg(const rnvp_conv_args* a) {
     const int kc = a->dtype == RNVP_F32 ? 16 : 32;   // channels per k-step
     if (M <= 1024) return a->cs_in % (8 * kc) == 0 ? 4 : 0;
     if (dgrad) return 0;
-    // RNVP_DEEP_FWD32=1: 32-channel tiles for the forward convs as well (A/B)
-    static const int fwd32 = [] { const char* e = getenv("RNVP_DEEP_FWD32"); return e ? atoi(e) : 0; }();
-    if (fwd32) return a->cs_in % (8 * kc) == 0 ? 4 : 0;
+    // (32-channel tiles for the forward convs as well measured slower in the
+    // step, profiles/r4_step_ab.txt)
     return a->cs_in % (8 * kc) == 0 ? 5 : 1;
 }
 

@@ -26,11 +26,20 @@ namespace {
 template <int NT, int NKS, int NOPS>
 constexpr int s1_min_blocks() { return (NKS == 2 && (NOPS == 3 || (NT == 4 && NOPS == 2))) ? 1 : 2; }
 
-template <int NT, int NKS, int TW, int NOPS>
+// TP: every BN table of the launch comes from batch sums whose shards fit
+// shard_issue<4> (checked on the host): the tables' shard loads go out first
+// and are summed by shard_sum_tab, and the kernel holds no other table path
+// -- with both paths in one function the compiler's wait tracking merges
+// them and waits for every load in flight (the first tile's included)
+// before the table sums.
+template <int NT, int NKS, int TW, int NOPS, bool TP>
 __global__ __launch_bounds__(256, (s1_min_blocks<NT, NKS, NOPS>())) void k_conv_s1(rnvp_conv_args a, int shards) {
     constexpr int CH = 8, KS = 32;            // bf16: 8 channels per 16-B chunk, 32 per k-step
     constexpr int NC = 16 * NT;
-    __shared__ double red[4][NC][2];
+    // shard table of the BN prologue / epilogue tables (shard_sum_tab), and
+    // the per-wave statistic partials at the end: one buffer
+    __shared__ double tabred[(2 * 4 * 256 > 4 * NC * 2) ? 2 * 4 * 256 : 4 * NC * 2];
+    double (*red)[NC][2] = (double (*)[NC][2])tabred;
     __shared__ double tmp[2 * 64];
     __shared__ __attribute__((aligned(16))) float bnp[2 * 64];
     __shared__ float etab[4 * NC];
@@ -44,8 +53,8 @@ __global__ __launch_bounds__(256, (s1_min_blocks<NT, NKS, NOPS>())) void k_conv_
     // weight and tile loads (vmcnt completes in issue order)
     ShardLoads<4> pro_l, epi_l;
     const int pnv = min(cs, a.cin);
-    const bool pro_pre = pro && a.pro.sums && shard_fits(pnv, a.pro.shards, 4);
-    const bool epi_pre = epi_bn && a.epi.sums && shard_fits(min(NC, N), a.epi.shards, 4);
+    const bool pro_pre = TP && pro;
+    const bool epi_pre = TP && epi_bn;
     if (pro_pre) shard_issue<4>(a.pro.sums, a.cin, a.pro.shards, 0, pnv, pro_l);
     if (epi_pre) shard_issue<4>(a.epi.sums, N, a.epi.shards, 0, min(NC, N), epi_l);
     // the tables' affine parameters in the same batch (cs, NC <= 64 < 256)
@@ -216,21 +225,18 @@ __global__ __launch_bounds__(256, (s1_min_blocks<NT, NKS, NOPS>())) void k_conv_
 
     // ---- tables (every thread: block-wide reductions), their loads in flight
     // behind the weights and the first tile's ----
-    if (pro) {
-        if (pro_pre) {
-            shard_finish<4>(pro_l, cs, tmp, tmp + cs);
+    if constexpr (TP) {
+        if (pro) {
+            shard_sum_tab<4>(pro_l, pnv, a.pro.shards, tabred, tmp, tmp + cs);
             block_bn_finish_aff(a.pro, a.cin, 0, cs, bnp, bnp + 64, nullptr, nullptr, tmp, pro_a);
-        } else {
-            block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + 64, nullptr, nullptr, tmp);
         }
-    }
-    if (epi_bn) {
-        if (epi_pre) {
-            shard_finish<4>(epi_l, NC, tmp, tmp + NC);
+        if (epi_bn) {
+            shard_sum_tab<4>(epi_l, min(NC, N), a.epi.shards, tabred, tmp, tmp + NC);
             block_bn_finish_aff(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp, epi_a);
-        } else {
-            block_bn_table(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp);
         }
+    } else {
+        if (pro) block_bn_table(a.pro, a.cin, 0, cs, bnp, bnp + 64, nullptr, nullptr, tmp);
+        if (epi_bn) block_bn_table(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp);
     }
     __syncthreads();
 
@@ -272,26 +278,38 @@ __global__ __launch_bounds__(256, (s1_min_blocks<NT, NKS, NOPS>())) void k_conv_
     }
 }
 
-template <int NT, int NKS, int TW, int NOPS>
+template <int NT, int NKS, int TW, int NOPS, bool TP>
 int launch_s1(const rnvp_conv_args* a, hipStream_t s) {
     const long long M = (long long)a->B * a->H * a->W;
     const long long ntiles = (M + 16 * TW - 1) / (16 * TW);
-    // one resident wave of workgroups, each wave walking several tiles with
-    // the next one in flight (a second round of workgroups would restart the
-    // pipeline)
+    // one resident wave of workgroups, one tile per wave and step with the
+    // next one in flight (a second round of workgroups would restart the
+    // pipeline; more tiles per wave measured slower, profiles/r4_step_ab.txt)
     static const int per_cu = [] {
         int n = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_conv_s1<NT, NKS, TW, NOPS>, 256, 0) != hipSuccess || n < 1)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_conv_s1<NT, NKS, TW, NOPS, TP>, 256, 0) != hipSuccess ||
+            n < 1)
             n = 1;
         return n;
     }();
-    // RNVP_S1_TPW: tiles per wave (A/B knob; 1 = every wave one tile)
-    static const int tpw = [] { const char* e = getenv("RNVP_S1_TPW"); const int v = e ? atoi(e) : 1; return v < 1 ? 1 : v; }();
-    long long grid = (ntiles + 4LL * tpw - 1) / (4LL * tpw);
+    long long grid = (ntiles + 3) / 4;
     if (grid > 256LL * per_cu) grid = 256LL * per_cu;
-    k_conv_s1<NT, NKS, TW, NOPS><<<(unsigned)grid, 256, 0, s>>>(*a, rnvp_stat_shards(M));
+    k_conv_s1<NT, NKS, TW, NOPS, TP><<<(unsigned)grid, 256, 0, s>>>(*a, rnvp_stat_shards(M));
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
+}
+
+// every BN table from batch sums whose shards fit shard_issue<4> (256 threads)
+inline bool s1_tables_pre(const rnvp_conv_args* a, int NC) {
+    auto fits = [](int nc, int shards) { return (long long)nc * (shards < 1 ? 1 : shards) <= 4LL * 256; };
+    if (a->pro_bn_relu && !(a->pro.sums && fits(a->cs_in < a->cin ? a->cs_in : a->cin, a->pro.shards))) return false;
+    if (a->epi_relu_bn_bwd && !(a->epi.sums && fits(NC < a->n ? NC : a->n, a->epi.shards))) return false;
+    return true;
+}
+
+template <int NT, int NKS, int TW, int NOPS>
+int launch_s1(const rnvp_conv_args* a, hipStream_t s) {
+    return s1_tables_pre(a, 16 * NT) ? launch_s1<NT, NKS, TW, NOPS, true>(a, s) : launch_s1<NT, NKS, TW, NOPS, false>(a, s);
 }
 
 template <int NT, int NKS, int TW>
@@ -491,8 +509,7 @@ FanKernel fan_kernel(int nt, int nks) {
 // validates, fills the members' shard counts and returns klass = 1 << 12 |
 // NT << 4 | NKS, the grid and the LDS bytes (RNVP_E_UNSUPPORTED: no such form)
 int rnvp_s1_fanout_prepare(rnvp_net_step* steps, int n, int* klass, int* grid, int* lds_bytes) {
-    static const int mode = [] { const char* e = getenv("RNVP_FANOUT"); return e ? atoi(e) : 1; }();
-    if (!mode || n < 2 || n > FAN_MAX) return RNVP_E_UNSUPPORTED;
+    if (n < 2 || n > FAN_MAX) return RNVP_E_UNSUPPORTED;
     const rnvp_conv_args& a0 = steps[0].conv;
     const long long M = (long long)a0.B * a0.H * a0.W;
     if (a0.dtype != RNVP_BF16 || M <= 16384 || M * 64 * 2 >= (1ll << 31)) return RNVP_E_UNSUPPORTED;
@@ -516,13 +533,13 @@ int rnvp_s1_fanout_prepare(rnvp_net_step* steps, int n, int* klass, int* grid, i
     const int NC = 16 * nt, KL = lds_mfma_pitch(nks * 32, 8);
     const size_t lds = (size_t)n * NC * KL * 2 + (size_t)n * 128 * 4 + (size_t)n * NC * 4 + 4 * NC * 2 * 8 + 128 * 8;
     if (lds > 64 * 1024) return RNVP_E_UNSUPPORTED;
-    const FanKernel k = fan_kernel(nt, nks);
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+    // host-only (no HIP call): the grid is one wave per tile here; the
+    // launch caps it to one resident round of workgroups (occupancy queried
+    // there, once per kernel)
     const int tw = nt == 4 ? 2 : 4;
     const long long ntiles = (M + 16 * tw - 1) / (16 * tw);
-    long long gr = (ntiles + 3) / 4;
-    if (gr > 256LL * per_cu) gr = 256LL * per_cu;
+    const long long gr = (ntiles + 3) / 4;
+    if (gr >= (1ll << 31)) return RNVP_E_UNSUPPORTED;
     *klass = (1 << 12) | (nt << 4) | nks;
     *grid = (int)gr;
     *lds_bytes = (int)lds;
@@ -530,8 +547,21 @@ int rnvp_s1_fanout_prepare(rnvp_net_step* steps, int n, int* klass, int* grid, i
 }
 
 int rnvp_s1_fanout_launch(const rnvp_group_kargs& g, int klass, int grid, int lds_bytes, hipStream_t s) {
-    const FanKernel k = fan_kernel((klass >> 4) & 15, klass & 15);
-    hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds_bytes, s, g);
+    const int nt = (klass >> 4) & 15, nks = klass & 15;
+    const FanKernel k = fan_kernel(nt, nks);
+    // resident workgroups per CU of this kernel at this LDS size (cached per
+    // kernel and LDS size; the members' weights make the LDS size vary)
+    static int cache_lds[3][2] = {{-1, -1}, {-1, -1}, {-1, -1}}, cache_n[3][2];
+    const int ti = nt == 1 ? 0 : (nt == 2 ? 1 : 2), ki = nks == 1 ? 0 : 1;
+    if (cache_lds[ti][ki] != lds_bytes) {
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, lds_bytes) != hipSuccess || per_cu < 1)
+            per_cu = 1;
+        cache_n[ti][ki] = per_cu;
+        cache_lds[ti][ki] = lds_bytes;
+    }
+    const long long cap = 256LL * cache_n[ti][ki];
+    hipLaunchKernelGGL(k, dim3((unsigned)(grid < cap ? grid : cap)), dim3(256), lds_bytes, s, g);
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
 }

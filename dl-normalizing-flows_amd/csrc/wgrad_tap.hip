@@ -512,20 +512,10 @@ long long wt_tasks(const rnvp_wgrad_conv& v, int cls) {
 }
 
 // tile class of a conv: by channel count (the widest tiles, fewest operand
-// re-reads).  RNVP_WT_POLICY=1: the deep scales' convs (M <= 16k pixels,
-// nz <= 8 slabs) take the 32 x 32 (3x3) / 64 x 64 (1x1) tiles when the wide
-// ones leave a conv under 256 workgroups (faster alone, slower in the
-// grouped step launch: profiles/r4_wgrad_ab.txt).
-int wt_class(const rnvp_wgrad_conv& v, int H, int W) {
-    static const int policy = [] { const char* e = getenv("RNVP_WT_POLICY"); return e ? atoi(e) : 0; }();
-    const int c = wt_class_base(v.ks, v.cs_in, v.cs_dy);
-    if (policy == 0) return c;
-    const int small = v.ks == 3 ? 2 : 3;
-    if (c != small && wt_tasks(v, c) < 256 && wt_stage_fits(small, H, W) &&
-        wt_lds_bytes(small, H, W, false) <= 160 * 1024)
-        return small;
-    return c;
-}
+// re-reads; the 32 x 32 / 64 x 64 tiles for the deep scales' small convs
+// were faster alone and slower in the grouped step launch,
+// profiles/r4_wgrad_ab.txt)
+int wt_class(const rnvp_wgrad_conv& v, int H, int W) { return wt_class_base(v.ks, v.cs_in, v.cs_dy); }
 
 }  // namespace
 
@@ -554,49 +544,26 @@ int rnvp_wgrad_tap_launch(rnvp_wgrad_group* g, hipStream_t s) {
         v.tk = (v.cs_in + wt_tci(cls) - 1) / wt_tci(cls);
         if (wt_tasks(v, cls) <= 0 || wt_tasks(v, cls) > (1ll << 28)) return RNVP_E_INVALID;
     }
-    // default: ONE launch for the group -- the class kernel (its own register
-    // budget) when every conv has the same class, else the all-class kernel
-    // (the largest class's 207 VGPRs for every task).  Splitting a mixed group
-    // into one launch per class serialises the launches on the stream and
-    // measured 0.3 ms/step slower (profiles/r4_wgrad_split.txt);
-    // RNVP_WT_SPLIT=1 keeps that variant for A/B.
-    static const int split = [] { const char* e = getenv("RNVP_WT_SPLIT"); return e ? atoi(e) : 0; }();
-    // the conflict-free k order where every conv's wider rows fit LDS
-    // (RNVP_WT_KO=0: the identity order everywhere)
-    static const int ko_env = [] { const char* e = getenv("RNVP_WT_KO"); return e ? atoi(e) : 1; }();
-    bool ko = ko_env != 0;
+    // ONE launch for the group -- the class kernel (its own register budget)
+    // when every conv has the same class, else the all-class kernel (the
+    // largest class's 207 VGPRs for every task).  One launch per class
+    // serialises the launches on the stream and measured 0.3 ms/step slower
+    // (profiles/r4_wgrad_split.txt).  The conflict-free k order where every
+    // conv's wider rows fit LDS.
+    bool ko = true;
     for (int c = 0; c < g->n_conv; ++c) ko = ko && wt_lds_bytes(g->conv[c].cls, H, W, true) <= 160 * 1024;
     bool one_class = true;
     for (int c = 1; c < g->n_conv; ++c) one_class = one_class && g->conv[c].cls == g->conv[0].cls;
-    if (!split || one_class) {
-        long long tasks = 0;
-        size_t shm = 0;
-        for (int c = 0; c < g->n_conv; ++c) {
-            rnvp_wgrad_conv& v = g->conv[c];
-            v.task0 = (int)tasks;
-            tasks += wt_tasks(v, v.cls);
-            shm = wt_lds_bytes(v.cls, H, W, ko) > shm ? wt_lds_bytes(v.cls, H, W, ko) : shm;
-        }
-        if (tasks > (1ll << 30)) return RNVP_E_INVALID;
-        hipLaunchKernelGGL(wt_kernel(one_class ? g->conv[0].cls : -1, ko), dim3((unsigned)tasks), dim3(WT_NT), shm, s, *g);
-        RNVP_LAUNCH_CHECK();
-        return RNVP_OK;
+    long long tasks = 0;
+    size_t shm = 0;
+    for (int c = 0; c < g->n_conv; ++c) {
+        rnvp_wgrad_conv& v = g->conv[c];
+        v.task0 = (int)tasks;
+        tasks += wt_tasks(v, v.cls);
+        shm = wt_lds_bytes(v.cls, H, W, ko) > shm ? wt_lds_bytes(v.cls, H, W, ko) : shm;
     }
-    for (int cls = 0; cls < 4; ++cls) {
-        rnvp_wgrad_group sub = *g;
-        sub.n_conv = 0;
-        long long tasks = 0;
-        for (int c = 0; c < g->n_conv; ++c) {
-            if (g->conv[c].cls != cls) continue;
-            rnvp_wgrad_conv v = g->conv[c];
-            v.task0 = (int)tasks;
-            tasks += wt_tasks(v, cls);
-            sub.conv[sub.n_conv++] = v;
-        }
-        if (sub.n_conv == 0) continue;
-        if (tasks > (1ll << 30)) return RNVP_E_INVALID;
-        hipLaunchKernelGGL(wt_kernel(cls, ko), dim3((unsigned)tasks), dim3(WT_NT), wt_lds_bytes(cls, H, W, ko), s, sub);
-        RNVP_LAUNCH_CHECK();
-    }
+    if (tasks > (1ll << 30)) return RNVP_E_INVALID;
+    hipLaunchKernelGGL(wt_kernel(one_class ? g->conv[0].cls : -1, ko), dim3((unsigned)tasks), dim3(WT_NT), shm, s, *g);
+    RNVP_LAUNCH_CHECK();
     return RNVP_OK;
 }

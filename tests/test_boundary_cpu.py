@@ -182,6 +182,13 @@ def test_net_group_prepare_rejections():
     assert prep(step(), step(x=fake + 4))[0] == -1               # misaligned operand
     assert prep(step(), step(x=0))[0] == -1                      # NULL operand
     assert prep(*[step() for _ in range(_lib.NET_GROUP_MAX + 1)])[0] == -1   # too many members
+    # the wide-scale fan-out form (bf16, M > 16384, <= 64 channels, members
+    # read the same input) -- also host-only: its grid is one wave per
+    # 32-pixel tile, capped to the resident workgroups at launch
+    wide = dict(B=64, H=32, W=32, cs=64, n=64, dtype=1)
+    rc, k, g, lb, arr = prep(step(**wide), step(**wide))
+    assert rc == 0 and k >> 12 == 1 and g == 64 * 32 * 32 // 128 and 0 < lb <= 64 * 1024
+    assert prep(step(**wide), step(**dict(wide, x=fake + 256)))[0] == -2   # members read different inputs
 
 
 def test_factor_out_refuses_non_canonical_order_matrix():

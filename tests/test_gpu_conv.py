@@ -188,6 +188,13 @@ CASES = [
     ("s1_out_band", 8, 64, 64, 32, 6, 1, dict(pro=True)),
     ("s2_1x1_band_odd", 32, 32, 32, 60, 40, 1, dict(pro=True, stats=True)),
     ("band_ragged_m", 9, 61, 61, 24, 16, 3, dict(pro=True, stats=True)),                 # M % 256 != 0, odd W
+    # the persistent band kernel (bf16, 17-64 outputs, 32k <= M < 2^21): a
+    # partial last band, odd / non-power-of-2 widths (halo crossing rows), N
+    # not a multiple of 16 (zeroed padding channels, sums for n < N)
+    ("band2_ragged_n24", 9, 61, 61, 24, 24, 3, dict(pro=True, stats=True)),
+    ("band2_ragged_n40", 9, 61, 61, 24, 40, 3, dict(pro=True, stats=True)),
+    ("band2_dgrad_res_acc_ragged", 9, 61, 61, 40, 40, 3, dict(dgrad=True, residual=True, acc=True, bias=False)),
+    ("band2_w48_n20_cs16", 16, 48, 48, 13, 20, 3, dict(pro=True, stats=True)),
     # config 3's widest convs (mid 1024 at 2x2 / 4x4)
     ("c3_1024_3x3_pro_stats", 16, 2, 2, 1024, 1024, 3, dict(pro=True, stats=True, bias=False)),
     ("c3_1024_1x1_pro_res", 16, 4, 4, 1024, 1024, 1, dict(pro=True, residual=True, stats=True)),
@@ -298,6 +305,18 @@ def test_band_matches_stream(case):
     b, _, _, _, _ = run_case(B, H, W, cin, cout, ks, "fp32", variant=1, **fl)
     assert rel(a, b) < 2e-6
     assert rel(b, ref) < 1e-5
+
+
+@pytest.mark.parametrize("case", BAND, ids=[c[0] for c in BAND])
+def test_band_bf16_matches_generic(case):
+    """bf16: the default wide-scale 3x3 path (the persistent band kernel where
+    it applies) vs the generic LDS-tiled kernel (variant 1), both against the
+    float64 restatement"""
+    name, B, H, W, cin, cout, ks, fl = case
+    a, ref, _, _, _ = run_case(B, H, W, cin, cout, ks, "bf16", variant=0, **fl)
+    b, _, _, _, _ = run_case(B, H, W, cin, cout, ks, "bf16", variant=1, **fl)
+    assert rel(a, ref) < 4e-3 and rel(b, ref) < 4e-3, (rel(a, ref), rel(b, ref))
+    assert rel(a, b) < 6e-3, rel(a, b)
 
 
 # deep-scale family (conv_deep.hip): every configuration against the float64

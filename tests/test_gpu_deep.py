@@ -270,17 +270,31 @@ def check_projections_vs_truth(P, Pref, Ptrue, band=8e-2, tail=0.02):
                                                                          float((err / allow).max()))
 
 
-def _trainer_step_check(dtype, lp_tol, norm_tol=None):
+def _trainer(model, B, dtype, chain):
+    """FlowTrainer with consecutive couplings chained (the default,
+    rnvp_coupling_out_in_fwd / _in_bwd_chain) or every coupling's in and out
+    parts launched on their own (chain=0)"""
+    from realnvp_hip import trainer as TM
+    old = TM.CHAIN_COUPLING
+    TM.CHAIN_COUPLING = chain
+    try:
+        tr = TM.FlowTrainer(model, B, dtype=dtype)
+    finally:
+        TM.CHAIN_COUPLING = old
+    assert any(v is not None for v in tr.chain.values()) == bool(chain)
+    return tr
+
+
+def _trainer_step_check(dtype, lp_tol, norm_tol=None, chain=1):
     """One fused-trainer step (the code bench.py times) on the golden batch:
     per-sample log-prob, loss and the gradient arena (+ the regulariser term
     the fused Adam folds in) against the reference -- norms, projection
     checksums of every tensor, the 10 largest tensors element by element and
     dL/dx."""
     from formula_init import projection_matrix
-    from realnvp_hip.trainer import FlowTrainer
     g = load_golden("model_m64_d32_r4_b64.npz")
     model = make_model(64, 32, 4)
-    tr = FlowTrainer(model, 64, dtype=dtype)
+    tr = _trainer(model, 64, dtype, chain)
     x, logdet = model_inputs(64, 64)
     tr.set_input(x.to(DEV), logdet.to(DEV))
     p0 = tr.param.clone()
@@ -318,11 +332,15 @@ def _trainer_step_check(dtype, lp_tol, norm_tol=None):
     return r.max(), rel(norms, g["grad_norms"])
 
 
-def test_trainer_config1_full_batch_fp32():
-    _trainer_step_check("fp32", 1e-5)
+@pytest.mark.parametrize("chain", [1, 0], ids=["chained", "unchained"])
+def test_trainer_config1_full_batch_fp32(chain):
+    """both coupling schedules pinned to the float64 truth (the chained one is
+    the default; each is held to the same allowance, not to the other)"""
+    _trainer_step_check("fp32", 1e-5, chain=chain)
 
 
-def test_trainer_config1_full_batch_bf16():
+@pytest.mark.parametrize("chain", [1, 0], ids=["chained", "unchained"])
+def test_trainer_config1_full_batch_bf16(chain):
     """The benchmarked step itself (config 1, B = 64, bf16 s/t net) pinned to
     a bf16-faithful CPU golden (tools/make_bf16_golden.py): the oracle with
     the engine's bf16 rounding points (stored conv outputs, packed operands
@@ -340,11 +358,10 @@ def test_trainer_config1_full_batch_bf16():
     large gradient tensor moves the vector past it.)"""
     from formula_init import projection_matrix
     from realnvp_bf16emu import Emu
-    from realnvp_hip.trainer import FlowTrainer
     g = load_golden("bf16emu_model_m64_d32_r4_b64.npz")
     refs = ("fp32", "emu", "emu_wide")
     model = make_model_chirp(64, 32, 4)
-    tr = FlowTrainer(model, 64, dtype="bf16")
+    tr = _trainer(model, 64, "bf16", chain)
     x, logdet = model_inputs(64, 64)
     tr.set_input(x.to(DEV), logdet.to(DEV))
     p0 = tr.param.clone()

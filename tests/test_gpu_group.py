@@ -15,6 +15,8 @@ the C ABI.
 """
 import ctypes as C
 
+import numpy as np
+
 import pytest
 import torch
 
@@ -29,6 +31,97 @@ def rel(a, b):
     return float((a - b).norm() / max(float(b.norm()), 1e-30))
 
 
+def _inputs(kind, cio, mid, size, B, seed=0):
+    """the coupling module (formula weights, chirp style) and its x, gy, gl on the host"""
+    import modules_realnvp as MR
+    import utils
+    torch.manual_seed(seed)
+    hp = utils.Hyperparameters(32, 4, True, True, True, True)
+    mod = MR.CheckerboardAffineCoupling(cio, mid, size, 1.0, hp) if kind == "ckbd" else \
+        MR.ChannelwiseAffineCoupling(cio, mid, 0.0, hp)
+    mod.load_state_dict(formula_state(mod, style="chirp"))
+    g = torch.Generator().manual_seed(seed + 1)
+    x = torch.randn(B, cio, size, size, generator=g)
+    gy = torch.randn(B, cio, size, size, generator=g)
+    gl = torch.randn(B, cio, size, size, generator=g)
+    return mod, x, gy, gl
+
+
+_ORACLE = {}
+
+
+def _oracle(case, mode):
+    """The CPU oracle of the same coupling step: mode "f64" (the truth),
+    "f32" (the reference's own precision), "emu" / "emu_wide" (the engine's
+    bf16 rounding points, fp32 / fp64 conv accumulation).  Returns (y, ldj,
+    dL/dx, {name: gradient}) in float64."""
+    key = (case, mode)
+    if key not in _ORACLE:
+        import realnvp_oracle as O
+        from realnvp_bf16emu import Emu, _R
+        _, kind, cio, mid, size, B = case
+        mod, x, gy, gl = _inputs(kind, cio, mid, size, B)
+        dt = torch.float64 if mode == "f64" else torch.float32
+        S = {k: (v.to(dt) if v.is_floating_point() else v) for k, v in mod.state_dict().items()}
+        names = [n for n, p in mod.named_parameters() if p.requires_grad]
+        for n in names:
+            S[n].requires_grad_(True)
+        hp = O.HP(32, 4)
+        saved = O.residual_module
+        if mode.startswith("emu"):
+            emu = Emu(mode == "emu_wide")
+            O.residual_module = lambda S_, p, h, tr, rb, bn, sk: emu.module(S_, p, _R.apply(h), tr, hp)
+        try:
+            xx = x.to(dt).requires_grad_(True)
+            fn = O.checkerboard_coupling if kind == "ckbd" else O.channelwise_coupling
+            y, ldj = fn(S, "", xx, 1.0 if kind == "ckbd" else 0.0, hp, training=True)
+            grads = torch.autograd.grad((y * gy.to(dt) + ldj * gl.to(dt)).sum(), [xx] + [S[n] for n in names],
+                                        allow_unused=True)
+        finally:
+            O.residual_module = saved
+        gd = {n: (g if g is not None else torch.zeros_like(S[n])).detach().double() for g, n in zip(grads[1:], names)}
+        _ORACLE[key] = (y.detach().double(), ldj.detach().double(), grads[0].double(), gd)
+    return _ORACLE[key]
+
+
+def _check_vs_oracle(case, dtype, got):
+    """Every gradient tensor and dL/dx of one launch schedule against the
+    oracle, with test_deep_coupling_vs_reference's allowance: fp32 -- within
+    5e-3 of the float64 truth or 3x the fp32 reference's own error, at most
+    5 % of the tensors beyond (ReLU-kink decisions), none 10x; bf16 -- the
+    bf16 emulation as the target and twice the largest scatter of the three
+    CPU references (fp32 oracle, emulation with fp32 / fp64 conv sums: the
+    engine keeps the BN statistics of the unrounded conv outputs, the
+    emulation those of the stored bf16 values) as the allowance, the rule of
+    test_trainer_config1_full_batch_bf16, same exception rule.
+    Zero-expectation gradients (a bias feeding a BatchNorm) are measured
+    against 1e-3 (bf16: 1e-2) of the largest gradient norm."""
+    y, ldj, gx, grads = got
+    if dtype == "fp32":
+        tgt, others, k, floor = _oracle(case, "f64"), [_oracle(case, "f32")], 3.0, 1e-3
+    else:
+        tgt, others, k, floor = _oracle(case, "emu"), [_oracle(case, "emu_wide"), _oracle(case, "f32")], 2.0, 1e-2
+    ty, tl, tgx, tg = tgt
+    gmax = max(float(v.norm()) for v in tg.values())
+    ratio, info = [], []
+    pairs = [("dL/dx", gx, tgx, [o[2] for o in others])] + [(n, grads[n], tg[n], [o[3][n] for o in others])
+                                                            for n in tg]
+    for n, a, t, os_ in pairs:
+        a = a.detach().double().cpu()
+        err, tn = float((a - t).norm()), float(t.norm())
+        oerr = max(float((o - t).norm()) for o in os_)
+        if len(os_) > 1:
+            oerr = max(oerr, float((os_[0] - os_[1]).norm()))
+        ratio.append(err / max(5e-3 * tn + floor * (gmax if n != "dL/dx" else tn), k * oerr))
+        info.append((n, err / max(tn, 1e-30), oerr / max(tn, 1e-30)))
+    ratio = np.array(ratio)
+    for i in np.argsort(-ratio)[:6]:
+        print("%.2f  %-45s ours %.3g  other %.3g" % ((ratio[i],) + info[i]))
+    assert (ratio > 1).mean() <= 0.05 and ratio.max() < 10, (float((ratio > 1).mean()), float(ratio.max()))
+    fy = float((y.double().cpu() - ty).norm() / ty.norm())
+    assert fy < (1e-5 if dtype == "fp32" else 1e-2), fy
+
+
 def _run_coupling(kind, cio, mid, size, B, dtype, group, seed=0):
     import modules_realnvp as MR
     import utils
@@ -36,17 +129,11 @@ def _run_coupling(kind, cio, mid, size, B, dtype, group, seed=0):
     old = engine.NET_GROUP
     engine.NET_GROUP = int(group)
     try:
-        torch.manual_seed(seed)
-        hp = utils.Hyperparameters(32, 4, True, True, True, True)
-        mod = MR.CheckerboardAffineCoupling(cio, mid, size, 1.0, hp) if kind == "ckbd" else \
-            MR.ChannelwiseAffineCoupling(cio, mid, 0.0, hp)
-        mod.load_state_dict(formula_state(mod, style="chirp"))
+        mod, x, gy, gl = _inputs(kind, cio, mid, size, B, seed)
         mod = mod.to(DEV).train()
         mod.compute_dtype = dtype
-        g = torch.Generator().manual_seed(seed + 1)
-        x = torch.randn(B, cio, size, size, generator=g).to(DEV).requires_grad_(True)
-        gy = torch.randn(B, cio, size, size, generator=g).to(DEV)
-        gl = torch.randn(B, cio, size, size, generator=g).to(DEV)
+        x = x.to(DEV).requires_grad_(True)
+        gy, gl = gy.to(DEV), gl.to(DEV)
         y, ldj = mod(x)
         (y * gy + ldj * gl).sum().backward()
         torch.cuda.synchronize()
@@ -92,22 +179,13 @@ def test_grouped_matches_single_launches(case, dtype):
     assert sum(p[0] == "group" for p in f1) >= 3, [p[:3] for p in f1]
     assert any(p[0] == "group" and p[2] - p[1] >= 5 for p in b1), [p[:3] for p in b1]
     # a group runs its first conv's tile configuration for every member, so
-    # a member can sum K in another order than its single launch: fp32
-    # rounding, amplified in the backward by ReLU-kink decisions (~1e-3 per
-    # flip, tests/test_gpu_deep.py); bf16: flipped bf16 roundings of stored
-    # activations
+    # a member can sum K in another order than its single launch: the
+    # forward agrees to rounding (bf16: flipped bf16 roundings of stored
+    # activations); the backward of EACH schedule is pinned to the oracle
     fw = 1e-5 if dtype == "fp32" else 1e-2
-    bw = 3e-3 if dtype == "fp32" else 5e-2
     assert rel(y1, y0) < fw and rel(l1, l0) < fw, (rel(y1, y0), rel(l1, l0))
-    assert rel(gx1, gx0) < bw, rel(gx1, gx0)
-    # biases of convs that feed only a BatchNorm have a zero gradient in exact
-    # arithmetic: errors are measured against the largest gradient norm
-    # (bf16: flipped roundings make those zero-expectation gradients noise of
-    # ~1 % of the largest norm)
-    gmax = max(float(g0[n].norm()) for n in g0)
-    floor = 1e-3 if dtype == "fp32" else 3e-2
-    worst = max((float((g1[n] - g0[n]).norm()) / (float(g0[n].norm()) + floor * gmax), n) for n in g0)
-    assert worst[0] < 10 * bw, worst
+    for y, l, gx, g in ((y0, l0, gx0, g0), (y1, l1, gx1, g1)):
+        _check_vs_oracle(case, dtype, (y, l, gx, g))
 
 
 def test_group_c_abi_two_skip_convs():
