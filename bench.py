@@ -306,7 +306,16 @@ def secondary(args, dev):
     dt = timed(loop_step, 3, 1)
     out["drop_in_loop"] = dict(value=round(3 * B / dt, 2), unit="images/sec", ms_per_step=round(dt / 3 * 1e3, 3),
                                dtype="fp32", steps=3,
-                               note="model(x) + loss.backward() + torch.optim.Adam, eager (train.py:176-200)")
+                               note="model(x) + loss.backward() + torch.optim.Adam, eager (train.py:176-200); "
+                                    "torch's default (foreach) Adam over the 1,960 parameter tensors alone takes "
+                                    "~12.8 ms/step (tools/probe/adam_probe.py)")
+    # the same loop with the s/t net in bf16 (set_precision, the trainer's mode)
+    model.set_precision("bf16")
+    dt = timed(loop_step, 3, 1)
+    out["drop_in_loop_bf16"] = dict(value=round(3 * B / dt, 2), unit="images/sec",
+                                    ms_per_step=round(dt / 3 * 1e3, 3), dtype="bf16", steps=3,
+                                    note="as drop_in_loop, s/t net in bf16")
+    model.set_precision("fp32")
     del opt
 
     # generation: RealNVP.sample(n) + logit_transform(reverse=True), eval mode (train.py:253-259)

@@ -77,7 +77,9 @@ __device__ __forceinline__ void st4(bf16_t* p, const float* v) {
     *(uint2*)p = t;
 }
 
-// store through a global-memory view (pointers read from descriptor tables)
+// load / store through a global-memory view (pointers read from descriptor tables)
+__device__ __forceinline__ float ldg(const RNVP_GLOBAL float* p) { return *p; }
+__device__ __forceinline__ float ldg(const RNVP_GLOBAL bf16_t* p) { return bf2f(*p); }
 __device__ __forceinline__ void stg(float* p, float v) { *(RNVP_GLOBAL float*)p = v; }
 __device__ __forceinline__ void stg(bf16_t* p, float v) { *(RNVP_GLOBAL bf16_t*)p = f2bf(v); }
 

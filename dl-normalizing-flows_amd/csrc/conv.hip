@@ -1576,6 +1576,59 @@ __global__ __launch_bounds__(256) void k_wn_pack(const rnvp_wn_desc* __restrict_
     }
 }
 
+// The data-gradient image from the forward image: wd[ci][tp*cs_out + co] =
+// wf[co][(ks*ks-1-tp)*cs_in + ci], on k_wn_pack's tiles (the same XCD order
+// and LDS tile, read from the forward image instead of v -- the values are
+// already g v / ||v|| rounded to T, so the two images stay bitwise what
+// k_wn_pack writes).  Used after the fused parameter pass (wn_adam.hip),
+// which writes the forward image row by row: a row of wd spans every output
+// channel, so writing it from one row block would be RB-element scatter.
+template <typename T>
+__global__ __launch_bounds__(256) void k_wn_wd(const rnvp_wn_desc* __restrict__ descs, int n_desc) {
+    constexpr int TP = WN_TCI * 9 + 1;
+    __shared__ float tile[WN_TCO * TP];
+    const int nb = gridDim.x, b = blockIdx.x;
+    const int q8 = nb / 8, r8 = nb % 8, xcd = b % 8;
+    const int tg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
+    const rnvp_wn_desc& d = descs[find_tile(descs, n_desc, tg)];
+    if (!d.wd) return;
+    const int t = tg - d.tile0;
+    const int tci = wn_tci(d.ks);
+    const int nci = (d.cin + tci - 1) / tci;
+    const int co0 = (t / nci) * WN_TCO, ci0 = (t % nci) * tci;
+    const int kk = d.ks * d.ks;
+    const int nco = min(WN_TCO, d.cout - co0), ncc = min(tci, d.cin - ci0);
+    // tile[c][ci * kk + tap] (k_wn_pack's layout) from the forward image rows
+    const float r_kc = 1.0f / (float)(kk * ncc), r_c = 1.0f / (float)ncc;
+    const RNVP_GLOBAL T* wf = (const RNVP_GLOBAL T*)d.wf;
+    for (int q = threadIdx.x; q < nco * kk * ncc; q += 256) {
+        const int c = fdiv_small(q, r_kc), r = q - c * (kk * ncc), tap = fdiv_small(r, r_c), ci = r - tap * ncc;
+        tile[c * TP + ci * kk + tap] = ldg(wf + (long long)(co0 + c) * d.kp_f + tap * d.cs_in + ci0 + ci);
+    }
+    __syncthreads();
+    // 8 consecutive output channels per item: one 16-byte store (bf16)
+    const int mg = (nco + 7) / 8;
+    const float r_kmg = 1.0f / (float)(kk * mg), r_mg = 1.0f / (float)mg;
+    for (int q = threadIdx.x; q < ncc * kk * mg; q += 256) {
+        const int ci = fdiv_small(q, r_kmg), r = q - ci * (kk * mg), tp = fdiv_small(r, r_mg), o8 = (r - tp * mg) * 8;
+        const int tap = kk - 1 - tp;
+        float w[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) w[e] = o8 + e < nco ? tile[(o8 + e) * TP + ci * kk + tap] : 0.f;
+        T* dst = (T*)d.wd + (long long)(ci0 + ci) * d.kp_d + tp * d.cs_out + co0 + o8;
+        if (o8 + 8 <= nco) {
+            if constexpr (sizeof(T) == 2) {
+                *(RNVP_GLOBAL u32x4*)dst = pack(w, T());
+            } else {
+                *(RNVP_GLOBAL u32x4*)dst = pack(w, T());
+                *(RNVP_GLOBAL u32x4*)(dst + 4) = pack(w + 4, T());
+            }
+        } else {
+            for (int e = 0; e < 8 && o8 + e < nco; ++e) stg(dst + e, w[e]);
+        }
+    }
+}
+
 // one block per output row co: dW row = sum of the nz partial slabs, gathered
 // into LDS in v's [ci][tap] order (coalesced over the packed k), then the
 // weight-norm backward and the bias partial sum.
@@ -1856,6 +1909,16 @@ extern "C" int rnvp_weight_norm_fwd(const rnvp_wn_desc* d, int n_desc, int total
     RNVP_LAUNCH_CHECK();
     if (dtype == RNVP_F32) k_wn_pack<float><<<total_tiles, 256, 0, s>>>(d, n_desc);
     else k_wn_pack<bf16_t><<<total_tiles, 256, 0, s>>>(d, n_desc);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+extern "C" int rnvp_weight_norm_transpose(const rnvp_wn_desc* d, int n_desc, int total_tiles, int dtype, void* stream) {
+    if (!d || n_desc <= 0 || total_tiles <= 0) return RNVP_E_INVALID;
+    if (dtype != RNVP_F32 && dtype != RNVP_BF16) return RNVP_E_INVALID;
+    hipStream_t s = (hipStream_t)stream;
+    if (dtype == RNVP_F32) k_wn_wd<float><<<total_tiles, 256, 0, s>>>(d, n_desc);
+    else k_wn_wd<bf16_t><<<total_tiles, 256, 0, s>>>(d, n_desc);
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
 }

@@ -11,10 +11,11 @@
 // <dW, v>, ||v||, g[co], the bias, Adam's element-wise update and the new
 // ||v'|| -- so one workgroup owns RB consecutive output rows of one conv,
 // keeps them in LDS (fp32, packed-k order) and writes the next step's
-// forward image wf[co][tap*cs_in+ci] row by row and the data-gradient image
-// wd[ci][tp*cs_out+co] in runs of RB output channels.  Consecutive row
-// blocks run on one XCD, so the 128-byte lines of wd that RB-channel runs
-// of neighbouring blocks fill complete in that XCD's L2 before write-back.
+// forward image wf[co][tap*cs_in+ci] row by row.  The transposed
+// data-gradient image wd[ci][tp*cs_out+co] spans all output channels of a
+// conv per row: it is derived from wf by rnvp_weight_norm_transpose, once
+// per step for the whole model (RB-channel runs of wd written from here
+// measured a third of the launch: 49 of 143 us at config 1's scale 5).
 //
 // from_slabs = 1 (single process): dW is the sum of the grouped wgrad's nz
 // replica slabs (rnvp_conv2d_wgrad_grouped); dv/dg/dbias are computed here
@@ -41,6 +42,9 @@ constexpr int WA_THREADS = 512;
 #ifndef WA_UD
 #define WA_UD 4
 #endif
+#ifndef WA_SKIP
+#define WA_SKIP 0
+#endif
 #ifndef WA_WPE
 #define WA_WPE 6
 #endif
@@ -66,54 +70,6 @@ __device__ __forceinline__ int find_blk(const rnvp_wn_desc* d, int n, int b) {
         else hi = mid - 1;
     }
     return lo;
-}
-
-template <typename T> struct RunStore;
-template <> struct RunStore<float> {
-    template <int RB> __device__ static void st(float* p, const float* v) {
-        if constexpr (RB == 8) {
-            *(RNVP_GLOBAL floatx4*)p = floatx4{v[0], v[1], v[2], v[3]};
-            *(RNVP_GLOBAL floatx4*)(p + 4) = floatx4{v[4], v[5], v[6], v[7]};
-        } else if constexpr (RB == 4) {
-            *(RNVP_GLOBAL floatx4*)p = floatx4{v[0], v[1], v[2], v[3]};
-        } else if constexpr (RB == 2) {
-            *(RNVP_GLOBAL floatx2*)p = floatx2{v[0], v[1]};
-        } else {
-            *(RNVP_GLOBAL float*)p = v[0];
-        }
-    }
-};
-template <> struct RunStore<bf16_t> {
-    template <int RB> __device__ static void st(bf16_t* p, const float* v) {
-        uint32_t w[4];
-#pragma unroll
-        for (int i = 0; i < (RB + 1) / 2; ++i)
-            w[i] = (uint32_t)f2bf(v[2 * i]) | (RB > 2 * i + 1 ? ((uint32_t)f2bf(v[2 * i + 1]) << 16) : 0u);
-        if constexpr (RB == 8) *(RNVP_GLOBAL u32x4*)p = u32x4{w[0], w[1], w[2], w[3]};
-        else if constexpr (RB == 4) *(RNVP_GLOBAL u32x2*)p = u32x2{w[0], w[1]};
-        else if constexpr (RB == 2) *(RNVP_GLOBAL uint32_t*)p = w[0];
-        else *(RNVP_GLOBAL bf16_t*)p = f2bf(v[0]);
-    }
-};
-
-template <typename T, int RB>
-__device__ __forceinline__ void wd_runs(const rnvp_wn_desc& d, const float* tile, const float* scl, int co0, int nr,
-                                        int RP, int P) {
-    const int kk = d.ks * d.ks, n = d.cin * kk;
-    const float rcin = 1.0f / (float)d.cin;
-    for (int q = threadIdx.x; q < n; q += WA_THREADS) {
-        const int tp = fdiv_small(q, rcin), ci = q - tp * d.cin;   // consecutive lanes: consecutive ci
-        const int off = (kk - 1 - tp) * P + ci;
-        float v[RB];
-#pragma unroll
-        for (int r = 0; r < RB; ++r) v[r] = r < nr ? scl[r] * tile[r * RP + off] : 0.f;
-        T* dst = (T*)d.wd + (long long)ci * d.kp_d + tp * d.cs_out + co0;
-        if (nr == RB) {
-            RunStore<T>::template st<RB>(dst, v);
-        } else {
-            for (int r = 0; r < nr; ++r) stg(dst + r, v[r]);
-        }
-    }
 }
 
 template <typename T, bool SLABS>
@@ -165,7 +121,7 @@ __global__ __launch_bounds__(WA_THREADS) __attribute__((amdgpu_waves_per_eu(WA_W
     // results -- identical -- stored twice), so every lane keeps several
     // memory round trips in flight; no load sits under a branch.
     constexpr int U = WA_U;
-    if (SLABS && live) {
+    if (SLABS && live && WA_SKIP != 2) {
         const int K4 = kk * d.cs_in / 4;           // cs_in % 8 == 0: a chunk never straddles a tap
         const float rcs = 1.0f / (float)d.cs_in;
         const RNVP_GLOBAL floatx4* src = (const RNVP_GLOBAL floatx4*)(d.dw + (long long)co * d.kp_f);
@@ -196,7 +152,7 @@ __global__ __launch_bounds__(WA_THREADS) __attribute__((amdgpu_waves_per_eu(WA_W
     // bitwise (a near-cancelling <dW, v> is order-sensitive in its last bits)
     const int lane = threadIdx.x & 63, pw = (threadIdx.x >> 6) % wpr;
     double dot = 0.0;
-    if (SLABS && d.g) {
+    if (SLABS && d.g && WA_SKIP != 3) {
         constexpr int UD = WA_UD;
         for (int vw = pw; vw < 4; vw += wpr) {
             double acc = 0.0;
@@ -225,7 +181,7 @@ __global__ __launch_bounds__(WA_THREADS) __attribute__((amdgpu_waves_per_eu(WA_W
     // the same bits): the 16-byte-aligned body of the row in float4 chunks,
     // the 0-3 element head and tail (the arenas' rows need not be aligned)
     // one element per lane
-    if (live) {
+    if (live && WA_SKIP != 4) {
         const float gs = gold / nrm;
         const float proj = (float)(dot / ((double)nrm * nrm));
         auto elem = [&](int i, float p, float gin, float& m, float& v2, float dwv, float& g) {
@@ -372,7 +328,7 @@ __global__ __launch_bounds__(WA_THREADS) __attribute__((amdgpu_waves_per_eu(WA_W
     }
     __syncthreads();
     // ---- phase 2: the next step's packed images from the LDS rows
-    if (live) {   // forward image: row co, CH consecutive ci per store
+    if (live && WA_SKIP != 1) {   // forward image: row co, CH consecutive ci per store
         constexpr int CH = 16 / sizeof(T);
         const int ng = (d.cin + CH - 1) / CH;
         const float rng = 1.0f / (float)ng;
@@ -395,14 +351,8 @@ __global__ __launch_bounds__(WA_THREADS) __attribute__((amdgpu_waves_per_eu(WA_W
             }
         }
     }
-    if (d.wd) {
-        switch (rb) {
-            case 8: wd_runs<T, 8>(d, tile, scl, co0, nr, RP, P); break;
-            case 4: wd_runs<T, 4>(d, tile, scl, co0, nr, RP, P); break;
-            case 2: wd_runs<T, 2>(d, tile, scl, co0, nr, RP, P); break;
-            default: wd_runs<T, 1>(d, tile, scl, co0, nr, RP, P); break;
-        }
-    }
+    // (the data-gradient image follows from the forward image:
+    // rnvp_weight_norm_transpose, one launch for the whole model)
 }
 
 // leftover trainable elements (BatchNorm affines, coupling scales, ...)

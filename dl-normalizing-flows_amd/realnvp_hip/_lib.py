@@ -142,6 +142,7 @@ _SIGS = {
     "rnvp_weight_norm_opt_blocks": (i32, [i32, i32, i32]),
     "rnvp_weight_norm_bwd_adam": (i32, [vp, i32, i32, i32, i32, C.POINTER(AdamArgs), vp, i64, vp, i64, vp]),
     "rnvp_adam_gather": (i32, [C.POINTER(AdamArgs), vp, i64, vp]),
+    "rnvp_weight_norm_transpose": (i32, [vp, i32, i32, i32, vp]),
     "rnvp_coupling_in_fwd": (i32, [C.POINTER(CouplingArgs), vp]),
     "rnvp_coupling_out_fwd": (i32, [C.POINTER(CouplingArgs), vp]),
     "rnvp_coupling_reverse": (i32, [C.POINTER(CouplingArgs), vp]),

@@ -581,6 +581,10 @@ class FlowTrainer:
                 t, n, nblk = self._opt_table
                 L.weight_norm_bwd_adam(t.data_ptr(), n, nblk, 0, 1 if self.dtype == "bf16" else 0,
                                        C.byref(self._opt_all), None, 0, None, 0, s)
+            # the data-gradient images from the forward images the row kernels wrote
+            dt = 1 if self.dtype == "bf16" else 0
+            for t, n, _, tiles in self.wn_tables:
+                L.weight_norm_transpose(t.data_ptr(), n, tiles, dt, s)
             L.adam_gather(C.byref(self._opt_all), self._opt_rest.data_ptr(), self._opt_rest.numel(), s)
             L.step_increment(self.step_t.data_ptr(), s)
             return

@@ -235,8 +235,9 @@ int rnvp_weight_norm_bwd(const rnvp_wn_desc* descs_device, int n_desc, int total
  *   Adam (rnvp_adam_update semantics, t = *step + step_add) on the row of v
  *     (mask 1 assumed: the caller checks), g[co] (when dg_off >= 0) and the
  *     bias (db_off >= 0; db_off < 0 = no bias), with their mask bytes;
- *   norm[co] = ||v'||, and both packed images (rnvp_weight_norm_fwd layout)
- *     of w' = g' v' / ||v'|| for the next step.
+ *   norm[co] = ||v'||, and the forward packed image (rnvp_weight_norm_fwd
+ *     layout) of w' = g' v' / ||v'|| for the next step; the data-gradient
+ *     image then follows from rnvp_weight_norm_transpose.
  * blk0: prefix sums of rnvp_weight_norm_opt_blocks(cout, cin, ks) (negative:
  * the row does not fit the kernel's LDS -- use the unfused calls).
  * zero0 / zero1 as rnvp_weight_norm_bwd.  Replaces modules_realnvp.py:53-59
@@ -250,6 +251,11 @@ int rnvp_weight_norm_opt_blocks(int cout, int cin, int ks);
 int rnvp_weight_norm_bwd_adam(const rnvp_wn_desc* descs_device, int n_desc, int total_blocks, int from_slabs,
                               int dtype, const rnvp_adam_args* adam, void* zero0, long long zero0_bytes,
                               void* zero1, long long zero1_bytes, void* stream);
+/* wd from wf (the transposed, flipped data-gradient image from the forward
+ * image; bitwise what rnvp_weight_norm_fwd writes for the same weights), on
+ * rnvp_weight_norm_fwd's tiles (tile0 / total_tiles) */
+int rnvp_weight_norm_transpose(const rnvp_wn_desc* descs_device, int n_desc, int total_tiles, int dtype,
+                               void* stream);
 /* Adam on the arena elements idx[0..n) (the parameters outside the convs:
  * BatchNorm affines, coupling scales, ...), rnvp_adam_update semantics */
 int rnvp_adam_gather(const rnvp_adam_args* adam, const long long* idx, long long n, void* stream);
