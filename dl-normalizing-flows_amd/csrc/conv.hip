@@ -25,8 +25,11 @@
 #include "common.h"
 #include "conv_common.h"
 
+#ifndef RNVP_SHARD_PX
+#define RNVP_SHARD_PX 8192
+#endif
 extern "C" int rnvp_stat_shards(long long M) {
-    long long s = M / 8192;
+    long long s = M / RNVP_SHARD_PX;
     int r = 1;
     while (r < 32 && r * 2 <= s) r *= 2;
     return r;

@@ -355,6 +355,15 @@ __global__ __launch_bounds__(WA_THREADS) __attribute__((amdgpu_waves_per_eu(WA_W
     // rnvp_weight_norm_transpose, one launch for the whole model)
 }
 
+// zero a table of byte ranges (8-byte multiples): blockIdx.y = range
+__global__ void k_zero_ranges(const rnvp_range* __restrict__ r) {
+    const rnvp_range q = r[blockIdx.y];
+    RNVP_GLOBAL double* p = (RNVP_GLOBAL double*)q.p;
+    const long long n = q.bytes / 8;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        p[i] = 0.0;
+}
+
 // leftover trainable elements (BatchNorm affines, coupling scales, ...)
 __global__ void k_adam_gather(rnvp_adam_args ad, const long long* __restrict__ idx, long long n) {
     __shared__ float coef[2];
@@ -418,6 +427,17 @@ extern "C" int rnvp_adam_gather(const rnvp_adam_args* ad, const long long* idx, 
     if (!ad->param || !ad->grad || !ad->exp_avg || !ad->exp_avg_sq || !ad->step) return RNVP_E_INVALID;
     if (n == 0) return RNVP_OK;
     k_adam_gather<<<rnvp_grid(n, 256, 1024), 256, 0, (hipStream_t)stream>>>(*ad, idx, n);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+extern "C" int rnvp_zero_ranges(const rnvp_range* ranges_device, int n, long long max_bytes, void* stream) {
+    if (n < 0 || max_bytes < 0 || (n > 0 && !ranges_device)) return RNVP_E_INVALID;
+    if (n == 0 || max_bytes == 0) return RNVP_OK;
+    if (n > 65535) return RNVP_E_UNSUPPORTED;
+    const long long per = (max_bytes / 8 + 255) / 256;
+    const unsigned bx = (unsigned)(per < 16 ? per : 16);
+    k_zero_ranges<<<dim3(bx, (unsigned)n), 256, 0, (hipStream_t)stream>>>(ranges_device);
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
 }

@@ -65,6 +65,10 @@ class WNDesc(C.Structure):
                 ("nz", i32), ("dbp", vp), ("db_off", i64), ("zero_after", i32), ("blk0", i32)]
 
 
+class Range(C.Structure):
+    _fields_ = [("p", vp), ("bytes", i64)]
+
+
 class AdamArgs(C.Structure):
     _fields_ = [("param", vp), ("grad", vp), ("exp_avg", vp), ("exp_avg_sq", vp), ("mask", vp),
                 ("step", vp), ("step_add", i64),
@@ -143,6 +147,7 @@ _SIGS = {
     "rnvp_weight_norm_bwd_adam": (i32, [vp, i32, i32, i32, i32, C.POINTER(AdamArgs), vp, i64, vp, i64, vp]),
     "rnvp_adam_gather": (i32, [C.POINTER(AdamArgs), vp, i64, vp]),
     "rnvp_weight_norm_transpose": (i32, [vp, i32, i32, i32, vp]),
+    "rnvp_zero_ranges": (i32, [vp, i32, i64, vp]),
     "rnvp_coupling_in_fwd": (i32, [C.POINTER(CouplingArgs), vp]),
     "rnvp_coupling_out_fwd": (i32, [C.POINTER(CouplingArgs), vp]),
     "rnvp_coupling_reverse": (i32, [C.POINTER(CouplingArgs), vp]),

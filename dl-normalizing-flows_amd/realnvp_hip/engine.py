@@ -355,6 +355,18 @@ class CouplingEngine:
         if len(pool) < 2:
             pool.append(sv)
 
+    def param_pass_info(self, sv, dtype):
+        """(host weight-norm descs with this coupling's wgrad slabs, [(ptr,
+        bytes)] ranges its deferred parameter pass must leave zero: the
+        forward batch sums of the saved arena sv and the backward reductions
+        of the scratch) -- what backward(opt="defer") skips."""
+        B, H, W = sv["B"], sv["H"], sv["W"]
+        sc = self.scratch_checked(B, H, W, dtype, sv["arena"].buf.device)
+        ar, sar = sv["arena"], sc["arena"]
+        f0, f1 = ar.range_bytes("in_sums", list(ar.slots)[-1])
+        z0, z1 = sc["zero"]
+        return sc["wn_descs"], [(ar.base + f0, f1 - f0), (sar.base + z0, z1 - z0)]
+
     def scratch_checked(self, B, H, W, dtype, device):
         """scratch() rebuilt when the weight set moved since it was made (its
         weight-norm table points into the packed-weight arena)."""
@@ -423,7 +435,7 @@ class CouplingEngine:
         tab = (WNDesc * len(descs))(*descs)
         nmax = max(max(chan_stride(s.cin), chan_stride(s.cout)) for s in self.P.convs.values())
         wse = splitk_elems(M, nmax)
-        sc = dict(arena=ar, zero=zr, wn_table=upload(bytes(tab), device),
+        sc = dict(arena=ar, zero=zr, wn_table=upload(bytes(tab), device), wn_descs=descs,
                   wn_key=wsz["key"], wn_rows=wsz["rows"], wn_blocks=wsz["blocks"], n_wn=len(descs), shards=sh,
                   ws=splitk_workspace(device, wse) if wse else None, ws_elems=wse,
                   wg=wg, wg_nz=nz, wg_nrep=nrep, wg_ws=wgws)
@@ -721,7 +733,9 @@ class CouplingEngine:
         opt: an AdamArgs over this coupling's block of the trainer's arenas:
         the weight-norm backward becomes the fused row-local parameter pass
         (rnvp_weight_norm_bwd_adam: dv/dg/dbias, Adam on every conv row, the
-        new norms and the next step's packed images)."""
+        new norms and the next step's packed images); "defer": only the
+        weight gradients run here -- the caller runs the parameter pass over
+        this coupling's slabs later (param_pass_info) and zeroes its sums."""
         L = _lib.lib()
         x = sv["x"]
         B, H, W, dtype, training = sv["B"], sv["H"], sv["W"], sv["dtype"], sv["training"]
@@ -849,7 +863,9 @@ class CouplingEngine:
                 zr = (ar.base + f0, f1 - f0, sar.base + z0, z1 - z0)
             else:
                 zr = (None, 0, sar.base + z0, z1 - z0)
-            if opt is not None:
+            if isinstance(opt, str):
+                pass    # "defer": the caller's model-wide parameter pass reads the slabs
+            elif opt is not None:
                 L.weight_norm_bwd_adam(sc["wn_table"].data_ptr(), sc["n_wn"], sc["wn_blocks"], 1, dt, C.byref(opt),
                                        *zr, ss)
             else:

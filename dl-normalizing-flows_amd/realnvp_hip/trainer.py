@@ -271,21 +271,37 @@ class FlowTrainer:
         self._packed_token = None
         if mode != "fused":
             return
-        from ._lib import AdamArgs, WNDesc
+        from ._lib import Range, WNDesc
         import ctypes as C
         mask = self.mask.cpu().numpy()
         covered = np.zeros(self.n, dtype=bool)
         base = self.grad.data_ptr()
         model_descs, blk0 = [], 0
-        self._opt_args = {}
+        slab_descs, ranges = [], []
+
+        def rebased(d, off, b0):
+            e = WNDesc()
+            C.memmove(C.addressof(e), C.addressof(d), C.sizeof(WNDesc))
+            e.dv_off += off
+            e.dg_off = e.dg_off + off if e.dg_off >= 0 else -1
+            e.db_off = e.db_off + off if e.db_off >= 0 else -1
+            e.blk0 += b0
+            return e
         for st in self.stages:
             if st[0] != "coupling":
                 continue
-            eng, block = st[2], st[6]
+            eng, sv, block = st[2], st[5], st[6]
             off = (block.data_ptr() - base) // 4
             ws = eng.weights(self.dtype)
             if ws["blocks"] < 0:
                 return
+            if self.pg is None:
+                # single process: every coupling's pass is deferred to ONE launch
+                # at the end of the backward over the couplings' (persistent)
+                # weight-gradient slabs
+                sdescs, rg = eng.param_pass_info(sv, self.dtype)
+                slab_descs += [rebased(d, off, blk0) for d in sdescs]
+                ranges += rg
             for d in ws["descs"]:
                 kr = d.cin * d.ks * d.ks
                 a = off + d.dv_off
@@ -296,18 +312,17 @@ class FlowTrainer:
                     covered[off + d.dg_off:off + d.dg_off + d.cout] = True
                 if d.db_off >= 0:
                     covered[off + d.db_off:off + d.db_off + d.cout] = True
-                e = WNDesc()
-                C.memmove(C.addressof(e), C.addressof(d), C.sizeof(WNDesc))
-                e.dv_off += off
-                e.dg_off = e.dg_off + off if e.dg_off >= 0 else -1
-                e.db_off = e.db_off + off if e.db_off >= 0 else -1
-                e.blk0 += blk0
-                model_descs.append(e)
+                model_descs.append(rebased(d, off, blk0))
             blk0 += ws["blocks"]
-            self._opt_args[id(eng)] = self._adam_args(off)
         from .engine import upload
         self._opt_table = (upload(bytes((WNDesc * len(model_descs))(*model_descs)), self.dev), len(model_descs),
                            blk0)
+        self._slab_table = None
+        if slab_descs:
+            self._slab_table = (upload(bytes((WNDesc * len(slab_descs))(*slab_descs)), self.dev), len(slab_descs),
+                                blk0)
+            rt = (Range * len(ranges))(*[Range(p, b) for p, b in ranges])
+            self._zero_table = (upload(bytes(rt), self.dev), len(ranges), max(b for _, b in ranges))
         rest = np.nonzero((mask > 0) & ~covered)[0].astype(np.int64)
         self._opt_rest = torch.from_numpy(rest).to(self.dev)
         self._opt_all = self._adam_args(0)
@@ -328,7 +343,7 @@ class FlowTrainer:
         """lr / betas / eps / weight decay changed (load_optimizer_state_dict)"""
         if not self.fused:
             return
-        for a in list(self._opt_args.values()) + [self._opt_all]:
+        for a in (self._opt_all,):
             a.lr, a.beta1, a.beta2, a.eps = self.lr, self.betas[0], self.betas[1], self.eps
             a.weight_decay, a.reg_coef = self.wd, self.reg
 
@@ -515,7 +530,7 @@ class FlowTrainer:
                     lo, hi = self.adam_ranges[ci]
                     after = (lambda lo=lo, hi=hi: self._adam_range(lo, hi))
                 prv = self.stages[i - 1] if self.chain.get(i - 1) is not None else None
-                opt = self._opt_args[id(eng)] if (self.fused and self.pg is None) else None
+                opt = "defer" if (self.fused and self.pg is None) else None
                 eng.backward(sv, self._g(z), None, self.g_lp, block, gx=self._g(x), side=self.side, after=after,
                              zero_at_end=True, defer=pending if self.side_group else None,
                              chain_prev=None if prv is None else (prv[2], prv[5]),
@@ -581,6 +596,15 @@ class FlowTrainer:
                 t, n, nblk = self._opt_table
                 L.weight_norm_bwd_adam(t.data_ptr(), n, nblk, 0, 1 if self.dtype == "bf16" else 0,
                                        C.byref(self._opt_all), None, 0, None, 0, s)
+            else:
+                # single process: every coupling's slabs -> dv / dg / dbias, Adam,
+                # norms and forward images in ONE launch (small couplings' rows fill
+                # the big ones' gaps), then their batch sums left zero
+                t, n, nblk = self._slab_table
+                L.weight_norm_bwd_adam(t.data_ptr(), n, nblk, 1, 1 if self.dtype == "bf16" else 0,
+                                       C.byref(self._opt_all), None, 0, None, 0, s)
+                zt, nz, zb = self._zero_table
+                L.zero_ranges(zt.data_ptr(), nz, zb, s)
             # the data-gradient images from the forward images the row kernels wrote
             dt = 1 if self.dtype == "bf16" else 0
             for t, n, _, tiles in self.wn_tables:

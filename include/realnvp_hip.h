@@ -256,6 +256,11 @@ int rnvp_weight_norm_bwd_adam(const rnvp_wn_desc* descs_device, int n_desc, int 
  * rnvp_weight_norm_fwd's tiles (tile0 / total_tiles) */
 int rnvp_weight_norm_transpose(const rnvp_wn_desc* descs_device, int n_desc, int total_tiles, int dtype,
                                void* stream);
+/* zero n byte ranges (8-byte multiples and alignment; max_bytes >= every
+ * range's size): the batch-statistic sums a deferred parameter pass leaves
+ * zero for the next step */
+typedef struct rnvp_range { void* p; long long bytes; } rnvp_range;
+int rnvp_zero_ranges(const rnvp_range* ranges_device, int n, long long max_bytes, void* stream);
 /* Adam on the arena elements idx[0..n) (the parameters outside the convs:
  * BatchNorm affines, coupling scales, ...), rnvp_adam_update semantics */
 int rnvp_adam_gather(const rnvp_adam_args* adam, const long long* idx, long long n, void* stream);

@@ -53,7 +53,7 @@ def main():
         sc = eng.scratch_checked(B, H, W, "bf16", dev)
         ws = eng.weights("bf16")
         nparam = sum(d.cout * d.cin * d.ks * d.ks for d in ws["descs"])
-        opt = tr._opt_args[id(eng)]
+        opt = tr._adam_args((block.data_ptr() - tr.grad.data_ptr()) // 4)
         fused = timeit(lambda: L.weight_norm_bwd_adam(sc["wn_table"].data_ptr(), sc["n_wn"], sc["wn_blocks"], 1, 1,
                                                       C.byref(opt), None, 0, None, 0, stream_ptr()))
         off = ((block.data_ptr() - tr.grad.data_ptr()) // 4 + 3) // 4 * 4
