@@ -1810,9 +1810,12 @@ extern "C" int rnvp_conv2d(const rnvp_conv_args* a, void* stream) {
     return a->dtype == RNVP_F32 ? dispatch_conv<float>(a, s) : dispatch_conv<bf16_t>(a, s);
 }
 
+#ifndef RNVP_SLAB_PX
+#define RNVP_SLAB_PX 2048
+#endif
 extern "C" int rnvp_wgrad_slabs(long long M) {
     // ~2048 pixels per slab (32 stages of 64), at most 128 slabs
-    long long z = M / 2048;
+    long long z = M / RNVP_SLAB_PX;
     if (z > 128) z = 128;
     if (z < 1) z = 1;
     return (int)z;

@@ -317,6 +317,12 @@ class FlowTrainer:
         from .engine import upload
         self._opt_table = (upload(bytes((WNDesc * len(model_descs))(*model_descs)), self.dev), len(model_descs),
                            blk0)
+        # algorithmic bytes of the parameter pass (bench.py kernel families):
+        # dW replicas + v twice + m + v^2 read, grad + v + m + v^2 + wf written
+        esz = 2 if self.dtype == "bf16" else 4
+        n_w = sum(d.cout * d.cin * d.ks * d.ks for d in model_descs)
+        nrep = sum(d.cout * d.cin * d.ks * d.ks * max(d.nz, 1) for d in slab_descs) if slab_descs else 0
+        self._param_bytes = (4 * (nrep if slab_descs else n_w) + 32 * n_w + esz * n_w, 2 * esz * n_w)
         self._slab_table = None
         if slab_descs:
             self._slab_table = (upload(bytes((WNDesc * len(slab_descs))(*slab_descs)), self.dev), len(slab_descs),
@@ -588,27 +594,30 @@ class FlowTrainer:
 
     def _optimizer(self):
         if self.fused:
+            from .engine import _launch
             L = _lib.lib()
             s = stream_ptr()
             import ctypes as C
+            dt = 1 if self.dtype == "bf16" else 0
+            pb, tb = self._param_bytes
             if self.pg is not None:
                 # data parallel: the conv rows' Adam + norms + images, after the all-reduce
                 t, n, nblk = self._opt_table
-                L.weight_norm_bwd_adam(t.data_ptr(), n, nblk, 0, 1 if self.dtype == "bf16" else 0,
-                                       C.byref(self._opt_all), None, 0, None, 0, s)
+                _launch("param", pb, 0.0, L.weight_norm_bwd_adam, t.data_ptr(), n, nblk, 0, dt,
+                        C.byref(self._opt_all), None, 0, None, 0, s)
             else:
                 # single process: every coupling's slabs -> dv / dg / dbias, Adam,
                 # norms and forward images in ONE launch (small couplings' rows fill
                 # the big ones' gaps), then their batch sums left zero
                 t, n, nblk = self._slab_table
-                L.weight_norm_bwd_adam(t.data_ptr(), n, nblk, 1, 1 if self.dtype == "bf16" else 0,
-                                       C.byref(self._opt_all), None, 0, None, 0, s)
+                _launch("param", pb, 0.0, L.weight_norm_bwd_adam, t.data_ptr(), n, nblk, 1, dt,
+                        C.byref(self._opt_all), None, 0, None, 0, s)
                 zt, nz, zb = self._zero_table
                 L.zero_ranges(zt.data_ptr(), nz, zb, s)
             # the data-gradient images from the forward images the row kernels wrote
-            dt = 1 if self.dtype == "bf16" else 0
             for t, n, _, tiles in self.wn_tables:
-                L.weight_norm_transpose(t.data_ptr(), n, tiles, dt, s)
+                _launch("param", tb / len(self.wn_tables), 0.0, L.weight_norm_transpose, t.data_ptr(), n, tiles, dt,
+                        s)
             L.adam_gather(C.byref(self._opt_all), self._opt_rest.data_ptr(), self._opt_rest.numel(), s)
             L.step_increment(self.step_t.data_ptr(), s)
             return

@@ -34,6 +34,13 @@ case $JOB in
     bench
     [ -n "$TRACE" ] && trace
     ;;
+  evidence)
+    # the round's evidence tables on this tree (tools/gpu_evidence.sh: -m gpu suite, smoke, PMC traffic /
+    # MFMA, rocprof families, kernel stats, the default bench line), then a 2-rank gloo rehearsal of the
+    # data-parallel bench path (eager, ranks sharing the one GPU)
+    TAG=${2:-r5ev} bash tools/gpu_evidence.sh || exit $?
+    step gloo2.log env RNVP_BENCH_BACKEND=gloo timeout -k 10 600 python3 -u bench.py --gpus 2 --steps 2 --warmup 1 --no-secondary --no-cpu-baseline
+    ;;
   *) echo "unknown job $JOB"; exit 2;;
 esac
 exit 0
