@@ -1601,12 +1601,22 @@ __global__ __launch_bounds__(256) void k_wn_wd(const rnvp_wn_desc* __restrict__ 
     const int co0 = (t / nci) * WN_TCO, ci0 = (t % nci) * tci;
     const int kk = d.ks * d.ks;
     const int nco = min(WN_TCO, d.cout - co0), ncc = min(tci, d.cin - ci0);
-    // tile[c][ci * kk + tap] (k_wn_pack's layout) from the forward image rows
-    const float r_kc = 1.0f / (float)(kk * ncc), r_c = 1.0f / (float)ncc;
+    // tile[c][ci * kk + tap] (k_wn_pack's layout) from the forward image rows,
+    // 8 input channels per item: ci0 and cs_in are multiples of 8 and a row's
+    // channel padding (up to cs_in) is in bounds, so every group is one
+    // aligned 16-byte (bf16) or two (fp32) loads
+    const int ng = (ncc + 7) / 8;
+    const float r_kg = 1.0f / (float)(kk * ng), r_g = 1.0f / (float)ng;
     const RNVP_GLOBAL T* wf = (const RNVP_GLOBAL T*)d.wf;
-    for (int q = threadIdx.x; q < nco * kk * ncc; q += 256) {
-        const int c = fdiv_small(q, r_kc), r = q - c * (kk * ncc), tap = fdiv_small(r, r_c), ci = r - tap * ncc;
-        tile[c * TP + ci * kk + tap] = ldg(wf + (long long)(co0 + c) * d.kp_f + tap * d.cs_in + ci0 + ci);
+    for (int q = threadIdx.x; q < nco * kk * ng; q += 256) {
+        const int c = fdiv_small(q, r_kg), r = q - c * (kk * ng), tap = fdiv_small(r, r_g), c8 = (r - tap * ng) * 8;
+        const RNVP_GLOBAL T* src = wf + (long long)(co0 + c) * d.kp_f + tap * d.cs_in + ci0 + c8;
+        float f[8];
+        unpack(*(const RNVP_GLOBAL u32x4*)src, f, T());
+        if constexpr (sizeof(T) == 4) unpack(*(const RNVP_GLOBAL u32x4*)(src + 4), f + 4, T());
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            if (c8 + e < ncc) tile[c * TP + (c8 + e) * kk + tap] = f[e];
     }
     __syncthreads();
     // 8 consecutive output channels per item: one 16-byte store (bf16)

@@ -243,25 +243,45 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
 
     // The whole K sequence of the wave is static (taps x NC channel chunks):
     // ring slots, tap offsets and the per-tap zero-row select are resolved at
-    // compile time or once per tap, and every A fragment of a step is read
-    // from LDS before its MFMAs.
+    // compile time.  DBUF: the A fragments are double-buffered -- step st+1's
+    // LDS reads are issued before step st's MFMAs, and scheduling barriers
+    // keep the compiler from sinking them (or the weight ring's refills) back
+    // to their use; left alone it reused one fragment register, i.e. waited
+    // for every LDS read right before its MFMAs.  The 8-wave 3x3 tiles with
+    // the larger register footprints keep the single-buffered loop (the second
+    // buffer would spill there).
+    constexpr bool DBUF = NW == 4 || KSZ == 1 || (BN == 32 ? NC <= 2 : NC == 1);
+    auto aload = [&](int st, u32x4* dst) {
+        const int tp = st / NC, ch = st - (st / NC) * NC;
+        const int toff = ((tp / KSZ - PAD) * W + (tp % KSZ - PAD)) * pitch + wk * KS + ch * WK * KS;
 #pragma unroll
-    for (int tp = 0; tp < KSZ * KSZ; ++tp) {
-        const int toff = ((tp / KSZ - PAD) * W + (tp % KSZ - PAD)) * pitch + wk * KS;
-        const T* base[TMW];
+        for (int i = 0; i < TMW; ++i)
+            dst[i] = *(const u32x4*)(((tvm[i] >> tp) & 1u) ? act + rowoff[i] + toff : zrow + ch * WK * KS);
+    };
+    if constexpr (DBUF) {
+        u32x4 avb[2][TMW];
+        aload(0, avb[0]);
 #pragma unroll
-        for (int i = 0; i < TMW; ++i) base[i] = ((tvm[i] >> tp) & 1u) ? act + rowoff[i] + toff : zrow;
+        for (int st = 0; st < NSTEP; ++st) {
+            if (st + 1 < NSTEP) aload(st + 1, avb[(st + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int ch = 0; ch < NC; ++ch) {
-            const int st = tp * NC + ch;
+            for (int i = 0; i < TMW; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) Mf<T>::step(rb[st % DK][j], avb[st & 1][i], acc[i][j]);
+            // refill this ring slot after its MFMAs (no register copies)
+            if (st + DK < NSTEP) bload(st + DK);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    } else {
+#pragma unroll
+        for (int st = 0; st < NSTEP; ++st) {
             u32x4 av[TMW];
-#pragma unroll
-            for (int i = 0; i < TMW; ++i) av[i] = *(const u32x4*)(base[i] + ch * WK * KS);
+            aload(st, av);
 #pragma unroll
             for (int i = 0; i < TMW; ++i)
 #pragma unroll
                 for (int j = 0; j < TN; ++j) Mf<T>::step(rb[st % DK][j], av[i], acc[i][j]);
-            // refill this ring slot after its MFMAs (no register copies)
             if (st + DK < NSTEP) bload(st + DK);
         }
     }

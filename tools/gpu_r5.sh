@@ -41,6 +41,18 @@ case $JOB in
     TAG=${2:-r5ev} bash tools/gpu_evidence.sh || exit $?
     step gloo2.log env RNVP_BENCH_BACKEND=gloo timeout -k 10 600 python3 -u bench.py --gpus 2 --steps 2 --warmup 1 --no-secondary --no-cpu-baseline
     ;;
+  ab)
+    # library A/B: optional tests, the conv microbench cases ${MB} and the step, HEAD build vs $BASE
+    [ -n "$TFILES" ] && TAILN=8 step pytest.log timeout -k 10 900 $PYT $TFILES ${TK:+-k "$TK"}
+    if [ -n "$MB" ]; then
+      TAILN=40 step mb_new.log timeout -k 10 300 python3 -u tools/conv_microbench.py $MB
+      TAILN=40 step mb_base.log env RNVP_LIB_PATH=$R/${BASE:-tools/variants/lib_base.so} timeout -k 10 300 python3 -u tools/conv_microbench.py $MB
+    fi
+    STEPS=${STEPS:-30} bench _new
+    step bench_base.log env RNVP_LIB_PATH=$R/${BASE:-tools/variants/lib_base.so} timeout -k 10 300 python3 -u bench.py --steps ${STEPS:-30} --warmup 5 --no-cpu-baseline --no-secondary
+    STEPS=${STEPS:-30} bench _new2
+    [ -n "$TRACE" ] && trace
+    ;;
   *) echo "unknown job $JOB"; exit 2;;
 esac
 exit 0
