@@ -1612,8 +1612,12 @@ __global__ __launch_bounds__(256) void k_wn_wd(const rnvp_wn_desc* __restrict__ 
         const int c = fdiv_small(q, r_kg), r = q - c * (kk * ng), tap = fdiv_small(r, r_g), c8 = (r - tap * ng) * 8;
         const RNVP_GLOBAL T* src = wf + (long long)(co0 + c) * d.kp_f + tap * d.cs_in + ci0 + c8;
         float f[8];
-        unpack(*(const RNVP_GLOBAL u32x4*)src, f, T());
-        if constexpr (sizeof(T) == 4) unpack(*(const RNVP_GLOBAL u32x4*)(src + 4), f + 4, T());
+        const u32x4 v0 = *(const RNVP_GLOBAL u32x4*)src;
+        unpack(v0, f, T());
+        if constexpr (sizeof(T) == 4) {
+            const u32x4 v1 = *(const RNVP_GLOBAL u32x4*)(src + 4);
+            unpack(v1, f + 4, T());
+        }
 #pragma unroll
         for (int e = 0; e < 8; ++e)
             if (c8 + e < ncc) tile[c * TP + (c8 + e) * kk + tap] = f[e];

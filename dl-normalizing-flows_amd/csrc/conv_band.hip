@@ -335,6 +335,9 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
         static_for<NSTEP>([&](auto STC) {
             constexpr int st = decltype(STC)::value;
             if constexpr (st + 1 < NSTEP) frag(std::integral_constant<int, st + 1>{}, (st + 1) & 1);
+            // keep the reads ahead: unfenced, the scheduler sank them to their
+            // MFMAs (an LDS drain before ~40 % of the MFMAs)
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -342,6 +345,7 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
                     if constexpr (WREG) Mf<T>::step(wr[st][j], av[st & 1][i], acc[i][j]);
                     else Mf<T>::step(wf[st & 1][j], av[st & 1][i], acc[i][j]);
                 }
+            __builtin_amdgcn_sched_barrier(0);
         });
         if ((band - b0) < 6) BAND_STAMP(3 + 2 * (band - b0));
         // epilogue: lane owns channels j*16 + 4g .. +3 of its pixels

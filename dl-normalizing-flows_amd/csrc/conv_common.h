@@ -283,6 +283,20 @@ __device__ __forceinline__ void bn_bwd_run(const rnvp_bn_bwd_args& a, double* ds
 #pragma unroll
         for (int j = 0; j < 2; ++j) gpre[j] = a.bn.gamma[min((int)threadIdx.x + j * (int)blockDim.x, C - 1)];
     }
+    // the thread's first data chunk is loaded before the statistic tables, so
+    // its latency overlaps theirs instead of following the reduction (at the
+    // deep scales that is every chunk of the thread); the optional operands
+    // through a pointer select -- no branch around the loads
+    const T* G = (const T*)a.g;
+    const T* X = (const T*)a.x;
+    const T* R = (const T*)a.residual;
+    T* DX = (T*)a.dx;
+    const int cpr = cs / CH;
+    const long long nch = a.M * cpr;
+    const long long q0 = blk * (long long)blockDim.x + threadIdx.x, qs = (long long)nblk * blockDim.x;
+    const long long of = (q0 < nch ? q0 : 0) * CH;
+    const u32x4 fg = *(const u32x4*)(G + of), fx = *(const u32x4*)(X + of);
+    const u32x4 fr = *(const u32x4*)((R ? R : G) + of), fd = *(const u32x4*)((a.accumulate ? (const T*)DX : G) + of);
     // both shard reductions (forward BN stats, backward g-sums): every load
     // issued up front, without branches, when the tables fit one pass
     // (ShardLoads); otherwise the looping block reduction
@@ -350,23 +364,14 @@ __device__ __forceinline__ void bn_bwd_run(const rnvp_bn_bwd_args& a, double* ds
     }
     for (int c = threadIdx.x + 2 * blockDim.x; c < cs; c += blockDim.x) entry(c, GAM ? a.bn.gamma[c] : 1.f);
     __syncthreads();
-    const T* G = (const T*)a.g;
-    const T* X = (const T*)a.x;
-    const T* R = (const T*)a.residual;
-    T* DX = (T*)a.dx;
-    const int cpr = cs / CH;
-    const long long nch = a.M * cpr;
-    const long long q0 = blk * (long long)blockDim.x + threadIdx.x, qs = (long long)nblk * blockDim.x;
     // the grid stride is a multiple of the chunks per pixel in practice: the
     // channel chunk of a thread is then fixed (no 64-bit modulo per chunk)
     const bool fixed = qs % cpr == 0;
     int c0 = (int)(q0 % cpr) * CH;
-    for (long long q = q0; q < nch; q += qs) {
-        const long long o = q * CH;
-        if (!fixed) c0 = (int)(q % cpr) * CH;
+    auto apply = [&](long long o, const u32x4& vg, const u32x4& vx, const u32x4& vr, const u32x4& vd) {
         float g[CH], x[CH], d[CH];
-        unpack(*(const u32x4*)(G + o), g, T());
-        unpack(*(const u32x4*)(X + o), x, T());
+        unpack(vg, g, T());
+        unpack(vx, x, T());
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
             const float* pp = p + 5 * (c0 + j);
@@ -375,17 +380,26 @@ __device__ __forceinline__ void bn_bwd_run(const rnvp_bn_bwd_args& a, double* ds
         }
         if (R) {
             float r[CH];
-            unpack(*(const u32x4*)(R + o), r, T());
+            unpack(vr, r, T());
 #pragma unroll
             for (int j = 0; j < CH; ++j) d[j] += r[j];
         }
         if (a.accumulate) {
             float r[CH];
-            unpack(*(const u32x4*)(DX + o), r, T());
+            unpack(vd, r, T());
 #pragma unroll
             for (int j = 0; j < CH; ++j) d[j] += r[j];
         }
         *(u32x4*)(DX + o) = pack(d, T());
+    };
+    if (q0 < nch) apply(q0 * CH, fg, fx, fr, fd);
+    for (long long q = q0 + qs; q < nch; q += qs) {
+        const long long o = q * CH;
+        if (!fixed) c0 = (int)(q % cpr) * CH;
+        const u32x4 vg = *(const u32x4*)(G + o), vx = *(const u32x4*)(X + o);
+        const u32x4 vr = R ? *(const u32x4*)(R + o) : vg;
+        const u32x4 vd = a.accumulate ? *(const u32x4*)(DX + o) : vg;
+        apply(o, vg, vx, vr, vd);
     }
 }
 

@@ -249,8 +249,9 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
     // to their use; left alone it reused one fragment register, i.e. waited
     // for every LDS read right before its MFMAs.  The 8-wave 3x3 tiles with
     // the larger register footprints keep the single-buffered loop (the second
-    // buffer would spill there).
-    constexpr bool DBUF = NW == 4 || KSZ == 1 || (BN == 32 ? NC <= 2 : NC == 1);
+    // buffer would spill there), and so does the 4-wave 64-channel tile at
+    // 1024 channels (its A double buffer spilled ~120 VGPRs into AGPRs).
+    constexpr bool DBUF = KSZ == 1 || (NW == 4 ? (BN == 32 || NC <= 4) : (BN == 32 ? NC <= 2 : NC == 1));
     auto aload = [&](int st, u32x4* dst) {
         const int tp = st / NC, ch = st - (st / NC) * NC;
         const int toff = ((tp / KSZ - PAD) * W + (tp % KSZ - PAD)) * pitch + wk * KS + ch * WK * KS;

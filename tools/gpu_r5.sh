@@ -48,6 +48,7 @@ case $JOB in
       TAILN=40 step mb_new.log timeout -k 10 300 python3 -u tools/conv_microbench.py $MB
       TAILN=40 step mb_base.log env RNVP_LIB_PATH=$R/${BASE:-tools/variants/lib_base.so} timeout -k 10 300 python3 -u tools/conv_microbench.py $MB
     fi
+    [ -n "$STAMPS" ] && TAILN=40 step stamps.log timeout -k 10 300 python3 -u tools/probe/deep_stamps.py
     STEPS=${STEPS:-30} bench _new
     step bench_base.log env RNVP_LIB_PATH=$R/${BASE:-tools/variants/lib_base.so} timeout -k 10 300 python3 -u bench.py --steps ${STEPS:-30} --warmup 5 --no-cpu-baseline --no-secondary
     STEPS=${STEPS:-30} bench _new2

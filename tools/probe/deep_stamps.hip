@@ -12,6 +12,10 @@ extern "C" int rnvp_stat_shards(long long M) {
     return r;
 }
 
+// the wide-scale fan-out groups live in conv_s1.hip (not part of this probe)
+int rnvp_s1_fanout_prepare(rnvp_net_step*, int, int*, int*, int*) { return RNVP_E_UNSUPPORTED; }
+int rnvp_s1_fanout_launch(const rnvp_group_kargs&, int, int, int, hipStream_t) { return RNVP_E_UNSUPPORTED; }
+
 extern "C" int probe_deep(const rnvp_conv_args* a, void* stream, int cfg, unsigned long long* stamps) {
     if (hipMemcpyToSymbolAsync(HIP_SYMBOL(g_deep_stamps), &stamps, sizeof(stamps), 0, hipMemcpyHostToDevice,
                                (hipStream_t)stream) != hipSuccess)
