@@ -1515,6 +1515,43 @@ constexpr int WN_TCO = 32, WN_TCI = 32, WN_TCI1 = 256;
 
 __host__ __device__ constexpr int wn_tci(int ks) { return ks == 1 ? WN_TCI1 : WN_TCI; }
 
+// The fragment-major copies (rnvp_wn_desc.wf_frag / wd_frag, read by the deep
+// 3x3 tiles through rnvp_conv_args.w_frag) of one [32 co] x [32 ci] x 3x3
+// tile: block (row / 16, k / 32) of 512 elements, lane L = row % 16 + 16 *
+// (k % 32 / 8) holding k % 8 = 0..7.  With cs_in, cs_out, co0 and ci0
+// multiples of 32 every block of the tile (per tap one 32-k block per 16
+// rows) lies wholly in this tile and is written whole: 16-byte stores, 1 KiB
+// per block.  val(c, ci, tap) is the tile's value of w[co0 + c][ci0 + ci][tap]
+// as the row-major image holds it (0 outside the conv's rows / channels).
+template <typename T, typename F>
+__device__ __forceinline__ void wn_frag_tile(const rnvp_wn_desc& d, int co0, int ci0, int nco, int ncc, F val) {
+    if constexpr (sizeof(T) != 2) return;   // the deep tiles read fragment-major images in bf16 only
+    if (d.ks != 3) return;
+    const int rbo = (nco + 15) >> 4, rbi = (ncc + 15) >> 4;   // row blocks this tile owns
+    if (d.wf_frag) {
+        for (int q = threadIdx.x; q < rbo * 9 * 64; q += blockDim.x) {
+            const int L = q & 63, bt = q >> 6, rb = bt / 9, tap = bt - rb * 9;
+            const int c = rb * 16 + (L & 15), kg = L >> 4;
+            float f[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] = (c < nco && kg * 8 + e < ncc) ? val(c, kg * 8 + e, tap) : 0.f;
+            T* dst = (T*)d.wf_frag + ((long long)((co0 >> 4) + rb) * (d.kp_f >> 5) + ((tap * d.cs_in + ci0) >> 5)) * 512 + L * 8;
+            *(RNVP_GLOBAL u32x4*)dst = pack(f, T());
+        }
+    }
+    if (d.wd_frag) {
+        for (int q = threadIdx.x; q < rbi * 9 * 64; q += blockDim.x) {
+            const int L = q & 63, bt = q >> 6, rb = bt / 9, tp = bt - rb * 9;
+            const int ci = rb * 16 + (L & 15), kg = L >> 4;
+            float f[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] = (ci < ncc && kg * 8 + e < nco) ? val(kg * 8 + e, ci, 8 - tp) : 0.f;
+            T* dst = (T*)d.wd_frag + ((long long)((ci0 >> 4) + rb) * (d.kp_d >> 5) + ((tp * d.cs_out + co0) >> 5)) * 512 + L * 8;
+            *(RNVP_GLOBAL u32x4*)dst = pack(f, T());
+        }
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_wn_pack(const rnvp_wn_desc* __restrict__ descs, int n_desc) {
     constexpr int TP = WN_TCI * 9 + 1;                      // LDS row pitch (floats), odd
@@ -1560,6 +1597,7 @@ __global__ __launch_bounds__(256) void k_wn_pack(const rnvp_wn_desc* __restrict_
             for (int e = 0; e < 4 && c4 + e < ncc; ++e) stv(dst + e, w[e]);
         }
     }
+    wn_frag_tile<T>(d, co0, ci0, nco, ncc, [&](int c, int ci, int tap) { return scl[c] * tile[c * TP + ci * kk + tap]; });
     if (!d.wd) return;
     // data-gradient image: 4 consecutive co per item
     const int mg = (nco + 3) / 4;
@@ -1623,6 +1661,7 @@ __global__ __launch_bounds__(256) void k_wn_wd(const rnvp_wn_desc* __restrict__ 
             if (c8 + e < ncc) tile[c * TP + (c8 + e) * kk + tap] = f[e];
     }
     __syncthreads();
+    wn_frag_tile<T>(d, co0, ci0, nco, ncc, [&](int c, int ci, int tap) { return tile[c * TP + ci * kk + tap]; });
     // 8 consecutive output channels per item: one 16-byte store (bf16)
     const int mg = (nco + 7) / 8;
     const float r_kmg = 1.0f / (float)(kk * mg), r_mg = 1.0f / (float)mg;
@@ -1811,6 +1850,7 @@ extern "C" int rnvp_conv2d(const rnvp_conv_args* a, void* stream) {
     if (a->variant < 0 || (a->variant > RNVP_VARIANT_DEEP && a->variant < RNVP_VARIANT_DEEP0) ||
         a->variant >= RNVP_VARIANT_DEEP0 + RNVP_DEEP_CFGS)
         return RNVP_E_INVALID;
+    if (a->w_frag && !al16(a->w_frag)) return RNVP_E_INVALID;
     if (a->dtype != RNVP_F32 && a->dtype != RNVP_BF16) return RNVP_E_INVALID;
     if (a->ks != 1 && a->ks != 3) return RNVP_E_UNSUPPORTED;
     if (a->B < 0 || a->H <= 0 || a->W <= 0 || a->n <= 0 || a->cin <= 0) return RNVP_E_INVALID;

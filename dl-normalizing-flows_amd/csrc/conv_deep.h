@@ -41,7 +41,12 @@ size_t deep_lds_bytes(int cs, int W, int ks) {
 // its resident workgroups loop over (vb % 8 is still the XCD when the
 // resident grid is a multiple of 8).  Callers separate consecutive tiles of
 // one workgroup with a barrier (the LDS is reused).
-template <typename T, int BN, int KSZ, bool PRO, int NW, int WK, int DK, int NC>
+// FM: the weights come from the fragment-major image (rnvp_conv_args.w_frag,
+// bf16): 16 output rows x 32 k per 1 KiB block, in MFMA lane order, so every
+// weight load of a wave is one contiguous KiB (eight whole 128-B lines)
+// instead of 64 B from each of 16 rows -- the row-major loads held the deep
+// 3x3 tiles to ~37 GB/s of weights per CU (TA busy ~55 cycles per load)
+template <typename T, int BN, int KSZ, bool PRO, int NW, int WK, int DK, int NC, bool FM = false>
 __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, int xa, int xb, int vb, int nvb,
                                           char* lds) {
     constexpr int NT = 64 * NW;
@@ -90,7 +95,7 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
     }
     const int m0 = mt * BM, n0 = nt * BN;
     const T* __restrict__ X = (const T*)a.x;
-    const T* __restrict__ Wt = (const T*)a.w;
+    const T* __restrict__ Wt = (const T*)(FM ? a.w_frag : a.w);
     const bool epi_bn = a.epi_relu_bn_bwd != 0;
     static_assert(BN <= NT, "bias / table loads: one channel per thread");
 
@@ -183,9 +188,16 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
     const T* wrow[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-        // rows >= N (clamped to row 0) only feed output columns that are never stored
-        const int row = n0 + j * 16 + li;
-        wrow[j] = Wt + (long long)(row < N ? row : 0) * a.kp + g * CH;
+        if constexpr (FM) {
+            static_assert(sizeof(T) == 2 && KS == 32, "fragment-major images are bf16");
+            // row blocks >= ceil(N / 16) (clamped to block 0) only feed columns never stored
+            const int nb = (n0 >> 4) + j, nbl = (N + 15) >> 4;
+            wrow[j] = Wt + (long long)(nb < nbl ? nb : 0) * (a.kp >> 5) * 512 + (li + 16 * g) * CH;
+        } else {
+            // rows >= N (clamped to row 0) only feed output columns that are never stored
+            const int row = n0 + j * 16 + li;
+            wrow[j] = Wt + (long long)(row < N ? row : 0) * a.kp + g * CH;
+        }
     }
     // wave wk's k-step s: tap s / NC, channel chunk (s % NC) * WK + wk of KS
     // (plain loads: buffer loads here measured slower -- the ring's waits)
@@ -194,7 +206,7 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
         const int tp = st / NC, ch = st - (st / NC) * NC;
         const int k = tp * cs + (ch * WK + wk) * KS;
 #pragma unroll
-        for (int j = 0; j < TN; ++j) rb[st % DK][j] = *(const u32x4*)(wrow[j] + k);
+        for (int j = 0; j < TN; ++j) rb[st % DK][j] = *(const u32x4*)(wrow[j] + (FM ? (k >> 5) * 512 : k));
     };
 #pragma unroll
     for (int u = 0; u < DK; ++u)

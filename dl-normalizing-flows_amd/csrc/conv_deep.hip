@@ -21,10 +21,10 @@
 
 namespace {
 
-template <typename T, int BN, int KSZ, bool PRO, int NW, int WK, int DK, int NC>
+template <typename T, int BN, int KSZ, bool PRO, int NW, int WK, int DK, int NC, bool FM = false>
 __global__ __launch_bounds__(64 * NW) void k_conv_deep(rnvp_conv_args a, int shards, int xa, int xb) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
-    deep_tile<T, BN, KSZ, PRO, NW, WK, DK, NC>(a, shards, xa, xb, blockIdx.x, gridDim.x, lds);
+    deep_tile<T, BN, KSZ, PRO, NW, WK, DK, NC, FM>(a, shards, xa, xb, blockIdx.x, gridDim.x, lds);
 }
 
 template <typename T, int BN, int NW, int WK, int DK, int NC, int KSZ>
@@ -38,6 +38,15 @@ int launch_deep_nc(const rnvp_conv_args* a, hipStream_t s) {
     const dim3 blk(64 * NW);
     int xa, xb;
     xcd_blocks(a, (int)gm, (int)gn, BN, sizeof(T), &xa, &xb);
+    // the fragment-major weight image where the caller provides one (bf16 3x3)
+    if constexpr (sizeof(T) == 2 && KSZ == 3 && NC <= 4) {
+        if (a->w_frag) {
+            if (a->pro_bn_relu) k_conv_deep<T, BN, KSZ, true, NW, WK, DK, NC, true><<<grid, blk, shm, s>>>(*a, sh, xa, xb);
+            else k_conv_deep<T, BN, KSZ, false, NW, WK, DK, NC, true><<<grid, blk, shm, s>>>(*a, sh, xa, xb);
+            RNVP_LAUNCH_CHECK();
+            return RNVP_OK;
+        }
+    }
     if (a->pro_bn_relu) k_conv_deep<T, BN, KSZ, true, NW, WK, DK, NC><<<grid, blk, shm, s>>>(*a, sh, xa, xb);
     else k_conv_deep<T, BN, KSZ, false, NW, WK, DK, NC><<<grid, blk, shm, s>>>(*a, sh, xa, xb);
     RNVP_LAUNCH_CHECK();

@@ -4,7 +4,24 @@
 
 #include "common.h"
 
-extern "C" int rnvp_version(void) { return 100; }
+extern "C" int rnvp_version(void) { return 105; }
+
+extern "C" int rnvp_struct_size(int which) {
+    switch (which) {
+        case 0: return (int)sizeof(rnvp_bn_src);
+        case 1: return (int)sizeof(rnvp_bn_running);
+        case 2: return (int)sizeof(rnvp_conv_args);
+        case 3: return (int)sizeof(rnvp_wgrad_conv);
+        case 4: return (int)sizeof(rnvp_wgrad_group);
+        case 5: return (int)sizeof(rnvp_bn_bwd_args);
+        case 6: return (int)sizeof(rnvp_wn_desc);
+        case 7: return (int)sizeof(rnvp_adam_args);
+        case 8: return (int)sizeof(rnvp_coupling_args);
+        case 9: return (int)sizeof(rnvp_net_step);
+        case 10: return (int)sizeof(rnvp_range);
+    }
+    return -1;
+}
 
 extern "C" const char* rnvp_status_string(int s) {
     if (s == RNVP_OK) return "ok";

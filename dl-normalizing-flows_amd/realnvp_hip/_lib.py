@@ -38,7 +38,7 @@ class ConvArgs(C.Structure):
                 ("pro_bn_relu", i32), ("pro", BNSrc),
                 ("out_sums", vp),
                 ("epi_relu_bn_bwd", i32), ("epi_x", vp), ("epi", BNSrc), ("epi_sums", vp),
-                ("ws", vp), ("ws_elems", i64), ("variant", i32)]
+                ("ws", vp), ("ws_elems", i64), ("variant", i32), ("w_frag", vp)]
 
 
 class BNBwdArgs(C.Structure):
@@ -62,7 +62,8 @@ class WNDesc(C.Structure):
                 ("dw", vp), ("dv_off", i64), ("dg_off", i64),
                 ("cout", i32), ("cin", i32), ("ks", i32), ("cs_in", i32), ("kp_f", i32),
                 ("cs_out", i32), ("kp_d", i32), ("row0", i32), ("tile0", i32),
-                ("nz", i32), ("dbp", vp), ("db_off", i64), ("zero_after", i32), ("blk0", i32)]
+                ("nz", i32), ("dbp", vp), ("db_off", i64), ("zero_after", i32), ("blk0", i32),
+                ("wf_frag", vp), ("wd_frag", vp)]
 
 
 class Range(C.Structure):
@@ -119,6 +120,7 @@ class TensorRef(C.Structure):
 
 _SIGS = {
     "rnvp_version": (i32, []),
+    "rnvp_struct_size": (i32, [i32]),
     "rnvp_status_string": (C.c_char_p, [i32]),
     "rnvp_marker": (i32, [i32, vp]),
     "rnvp_checkerboard_mask": (i32, [vp, i32, i32, vp]),
@@ -177,10 +179,18 @@ class _Lib:
             fn = getattr(self.dll, name)
             fn.restype = res
             fn.argtypes = args
-            raw = name in ("rnvp_version", "rnvp_stat_shards", "rnvp_wgrad_slabs", "rnvp_wgrad_replicas",
+            raw = name in ("rnvp_version", "rnvp_struct_size", "rnvp_stat_shards", "rnvp_wgrad_slabs", "rnvp_wgrad_replicas",
                            "rnvp_weight_norm_tiles", "rnvp_weight_norm_opt_blocks",
                            "rnvp_net_group_prepare") or res is not i32
             setattr(self, name[len("rnvp_"):], fn if raw else self._wrap(name, fn))
+        # the struct mirrors must match the library's layouts (rnvp_struct_size): a
+        # table read at another stride would address arbitrary device memory
+        mirrors = (BNSrc, BNRunning, ConvArgs, WgradConv, WgradGroup, BNBwdArgs, WNDesc, AdamArgs, CouplingArgs,
+                   NetStep, Range)
+        for i, m in enumerate(mirrors):
+            if self.dll.rnvp_struct_size(i) != C.sizeof(m):
+                raise RuntimeError("%s: struct %s is %d bytes in the library, %d in the binding (stale build?)"
+                                   % (path, m.__name__, self.dll.rnvp_struct_size(i), C.sizeof(m)))
 
     def _wrap(self, name, fn):
         dll = self.dll

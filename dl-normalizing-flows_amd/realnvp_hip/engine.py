@@ -262,6 +262,13 @@ class CouplingEngine:
             ar.add("wf:" + name, spec.cout * kp_f * esz)
             ar.add("wd:" + name, spec.cin * kp_d * esz)
             ar.add("norm:" + name, spec.cout * 4)
+            # bf16 3x3: fragment-major copies for the deep-scale tiles (rnvp_conv_args.w_frag),
+            # written beside the row-major images by the weight-norm pack / transpose kernels
+            if dtype == "bf16" and spec.ks == 3:
+                if cs_in % 32 == 0:
+                    ar.add("wff:" + name, round_up(spec.cout, 16) * kp_f * esz)
+                if cs_out % 32 == 0:
+                    ar.add("wdf:" + name, round_up(spec.cin, 16) * kp_d * esz)
         ar.alloc(dev, zero=True)   # zero padding of the packed images, once
         descs = []
         row0 = tile0 = blk0 = 0
@@ -272,6 +279,8 @@ class CouplingEngine:
             d.v = T[vn].data_ptr()
             d.g = T[gn].data_ptr() if gn else None
             d.wf, d.wd, d.norm = ar.ptr("wf:" + name), ar.ptr("wd:" + name), ar.ptr("norm:" + name)
+            d.wf_frag = ar.ptr("wff:" + name) if ar.has("wff:" + name) else None
+            d.wd_frag = ar.ptr("wdf:" + name) if ar.has("wdf:" + name) else None
             d.dw = None
             d.dv_off = self.layout[vn][0]
             d.dg_off = self.layout[gn][0] if (gn and spec.scale) else -1
@@ -513,6 +522,7 @@ class CouplingEngine:
             a.dtype, a.B, a.H, a.W, a.ks = dt, B, H, W, spec.ks
             a.x, a.cs_in, a.cin = ar.ptr(op.x), cs_in, spec.cin
             a.w, a.kp = war.ptr("wf:" + op.conv), kp_f
+            a.w_frag = war.ptr("wff:" + op.conv) if war.has("wff:" + op.conv) else None
             a.y, a.cs_out, a.n = ar.ptr(op.y), cs_out, spec.cout
             _, _, bn_ = self._conv_names(spec)
             a.bias = T[bn_].data_ptr() if bn_ else None
@@ -658,6 +668,7 @@ class CouplingEngine:
                 c.dtype, c.B, c.H, c.W, c.ks = dt, B, H, W, spec.ks
                 c.x, c.cs_in, c.cin = sar.ptr(st.gy), cs_out, spec.cout
                 c.w, c.kp = war.ptr("wd:" + op.conv), kp_d
+                c.w_frag = war.ptr("wdf:" + op.conv) if war.has("wdf:" + op.conv) else None
                 c.y = sar.ptr(st.tmp if st.tmp else st.gx)
                 c.cs_out, c.n = cs_in, spec.cin
                 c.residual = sar.ptr(st.residual) if st.residual else None

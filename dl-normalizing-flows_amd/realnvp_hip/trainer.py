@@ -322,7 +322,9 @@ class FlowTrainer:
         esz = 2 if self.dtype == "bf16" else 4
         n_w = sum(d.cout * d.cin * d.ks * d.ks for d in model_descs)
         nrep = sum(d.cout * d.cin * d.ks * d.ks * max(d.nz, 1) for d in slab_descs) if slab_descs else 0
-        self._param_bytes = (4 * (nrep if slab_descs else n_w) + 32 * n_w + esz * n_w, 2 * esz * n_w)
+        # the transposes also write the fragment-major copies (engine.weights: bf16 3x3 convs)
+        n_frag = sum(d.cout * d.cin * d.ks * d.ks * (int(bool(d.wf_frag)) + int(bool(d.wd_frag))) for d in model_descs)
+        self._param_bytes = (4 * (nrep if slab_descs else n_w) + 32 * n_w + esz * n_w, 2 * esz * n_w + esz * n_frag)
         self._slab_table = None
         if slab_descs:
             self._slab_table = (upload(bytes((WNDesc * len(slab_descs))(*slab_descs)), self.dev), len(slab_descs),

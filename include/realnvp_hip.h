@@ -33,6 +33,13 @@ enum { RNVP_OK = 0, RNVP_E_INVALID = -1, RNVP_E_UNSUPPORTED = -2 };
 
 /* ---- version / capabilities ------------------------------------------- */
 int rnvp_version(void);
+/* sizeof the library's argument structs, in this order: rnvp_bn_src,
+ * rnvp_bn_running, rnvp_conv_args, rnvp_wgrad_conv, rnvp_wgrad_group,
+ * rnvp_bn_bwd_args, rnvp_wn_desc, rnvp_adam_args, rnvp_coupling_args,
+ * rnvp_net_step, rnvp_range (-1 past the end).  A binding compares them with
+ * its own mirrors at load time: a library built from another header revision
+ * is refused instead of reading descriptor tables at the wrong stride. */
+int rnvp_struct_size(int which);
 const char* rnvp_status_string(int status);
 /* empty one-lane dispatch: delimits engine launches in PMC traces (profiling only) */
 int rnvp_marker(int tag, void* stream);
@@ -142,6 +149,12 @@ typedef struct rnvp_conv_args {
     int epi_relu_bn_bwd; const void* epi_x; rnvp_bn_src epi; double* epi_sums;
     float* ws; long long ws_elems;      /* split-K workspace (optional) */
     int variant;
+    /* optional (NULL: none): the same weights as w in the fragment-major image
+     * -- block (n / 16, k / 32) of 512 bf16 at ((n / 16) * kp / 32 + k / 32) * 512,
+     * element (n % 16 + 16 * (k % 32 / 8)) * 8 + k % 8 inside it (n padded to
+     * 16 rows with zeros).  The bf16 3x3 deep-scale kernels read it instead of
+     * w: each weight load of a wave is one contiguous KiB in MFMA lane order. */
+    const void* w_frag;
 } rnvp_conv_args;
 int rnvp_conv2d(const rnvp_conv_args* a, void* stream);
 
@@ -209,6 +222,10 @@ typedef struct rnvp_wn_desc {
     long long db_off;                  /* bias gradient offset (elements) */
     int zero_after;                    /* re-zero dw / dbp after use (atomic accumulation) */
     int blk0;                          /* first row block (prefix sum of rnvp_weight_norm_opt_blocks) */
+    /* optional fragment-major copies of wf / wd (rnvp_conv_args.w_frag; 3x3,
+     * cs_in resp. cs_out a multiple of 32, rows padded to 16), written beside
+     * the row-major images by rnvp_weight_norm_fwd / _transpose, or NULL */
+    void* wf_frag; void* wd_frag;
 } rnvp_wn_desc;
 /* fwd, for any number of convs (a whole model): one launch computes every
  * row norm, one writes both packed images on [32 co] x [32 ci] tiles

@@ -33,7 +33,7 @@ def bf16_round(t):
 
 
 def run_case(B, H, W, cin, cout, ks, dtype, pro=False, residual=False, acc=False, stats=False, dgrad=False,
-             bias=True, variant=0, seed=0, rows=None):
+             bias=True, variant=0, seed=0, rows=None, fm=False):
     """rows: compute the float64 reference only at these output pixels
     (config 4's M = 2^22 shapes, whose full float64 conv is too slow on the
     host); the statistics are then checked against the float64 sums of the
@@ -70,6 +70,14 @@ def run_case(B, H, W, cin, cout, ks, dtype, pro=False, residual=False, acc=False
             base = (ky * ks + kx) * csi
             wp[:, base:base + cin] = w[:, ky, kx, :].to(tdt)
     dx, dw = nhwc(x, csi), wp.to(DEV)
+    dwf = None
+    if fm:   # the fragment-major image (w_frag): 16 x 32 blocks in MFMA lane order; w = zeros, so a
+        # kernel reading w instead of w_frag fails the float64 comparison
+        npad = (cout + 15) // 16 * 16
+        wpad = torch.zeros(npad, kp, dtype=tdt, device=DEV)
+        wpad[:cout] = dw
+        dwf = wpad.view(npad // 16, 16, kp // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
+        dw = torch.zeros_like(dw)
     dy = nhwc(yold, cso) if acc else torch.zeros(M, cso, dtype=tdt, device=DEV)
     dres, dex = nhwc(res, cso), nhwc(ex, cso)      # 1-row placeholders when unused
     db = bvec.float().to(DEV)
@@ -97,6 +105,7 @@ def run_case(B, H, W, cin, cout, ks, dtype, pro=False, residual=False, acc=False
     a.B, a.H, a.W, a.ks = B, H, W, ks
     a.x, a.cs_in, a.cin = dx.data_ptr(), csi, cin
     a.w, a.kp = dw.data_ptr(), kp
+    a.w_frag = dwf.data_ptr() if dwf is not None else None
     a.y, a.cs_out, a.n = dy.data_ptr(), cso, cout
     a.bias = db.data_ptr() if bias else None
     a.residual = dres.data_ptr() if residual else None
@@ -349,3 +358,26 @@ def test_deep_family_vs_float64(case, cfg, dtype):
     if s1 is not None:
         assert rel(sums[0], s1) < 10 * tol, rel(sums[0], s1)
         assert rel(sums[1], s2) < 10 * tol, rel(sums[1], s2)
+
+
+# fragment-major weight images (rnvp_conv_args.w_frag, bf16 3x3 deep tiles):
+# the same MFMAs in the same order from another weight layout -- bitwise equal
+# outputs to the row-major image, every configuration (w itself is zeros in
+# the w_frag run: a kernel that read it would miss the float64 reference)
+@pytest.mark.parametrize("cfg", [0, 1, 4, 5])
+@pytest.mark.parametrize("case", [c for c in DEEP_FAMILY if c[6] == 3], ids=[c[0] for c in DEEP_FAMILY if c[6] == 3])
+def test_deep_frag_major_weights(case, cfg):
+    name, B, H, W, cin, cout, ks, fl = case
+    if cin // ((4 if cfg < 2 else 8) * 32) > 4:
+        pytest.skip("no fragment-major kernel beyond 4 channel chunks per wave (the row-major image is used)")
+    try:
+        a = run_case(B, H, W, cin, cout, ks, "bf16", variant=VARIANT_DEEP0 + cfg, **fl)
+    except RuntimeError as e:
+        if "unsupported" in str(e):
+            pytest.skip("configuration %d does not apply" % cfg)
+        raise
+    b = run_case(B, H, W, cin, cout, ks, "bf16", variant=VARIANT_DEEP0 + cfg, fm=True, **fl)
+    assert torch.equal(a[0], b[0])
+    if a[2] is not None:
+        assert torch.allclose(a[2], b[2], rtol=1e-12, atol=1e-9)
+    assert rel(b[0], b[1]) < 4e-3

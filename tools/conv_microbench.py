@@ -48,8 +48,18 @@ def bench(fn, iters=20, reps=5):
     return ts[len(ts) // 2] * 1e3   # us
 
 
+def frag_major(w):
+    """[n][kp] -> the fragment-major image (rnvp_conv_args.w_frag): 16-row x 32-k
+    blocks in MFMA lane order (lane = n % 16 + 16 * (k % 32 // 8))."""
+    n, kp = w.shape
+    npad = (n + 15) // 16 * 16
+    wp = torch.zeros(npad, kp, dtype=w.dtype, device=w.device)
+    wp[:n] = w
+    return wp.view(npad // 16, 16, kp // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
+
+
 def conv_case(B, H, W, cin, cout, ks, pro=False, stats=False, residual=False, acc=False, dgrad_epi=False,
-              dtype="bf16", wgrad=False, variant=0):
+              dtype="bf16", wgrad=False, variant=0, fm=False):
     dev = "cuda"
     tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
     esz = 2 if dtype == "bf16" else 4
@@ -91,6 +101,9 @@ def conv_case(B, H, W, cin, cout, ks, pro=False, stats=False, residual=False, ac
         a.B, a.H, a.W, a.ks = B, H, W, ks
         a.x, a.cs_in, a.cin = x.data_ptr(), csi, cin
         a.w, a.kp = w.data_ptr(), kp
+        if fm:
+            wfm = frag_major(w)
+            a.w_frag = wfm.data_ptr()
         a.y, a.cs_out, a.n = y.data_ptr(), cso, cout
         a.residual = r.data_ptr() if residual else None
         a.accumulate = int(acc)
@@ -160,6 +173,7 @@ CASES = [
 def main():
     torch.manual_seed(0)
     variants = [0, 1] if "--v01" in sys.argv else [0]
+    fms = [False, True] if "--fm" in sys.argv else [False]
     if "--deep" in sys.argv:   # the deep-scale family's configurations (RNVP_VARIANT_DEEP0 + c)
         variants = [0] + [16 + c for c in range(6)]
     only = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--case=")]
@@ -168,13 +182,14 @@ def main():
         if only and not any(o in name for o in only):
             continue
         for v in variants:
-            if fl.get("wgrad") and v:
-                continue
-            try:
-                us, gbs, tfs = conv_case(B, H, W, ci, co, ks, variant=v, **fl)
-            except RuntimeError:
-                continue   # configuration does not apply to this shape
-            print("%-32s %3d %9.1f %9.1f %9.1f" % (name, v, us, gbs, tfs), flush=True)
+            for fm in fms:
+                if (fl.get("wgrad") and (v or fm)) or (fm and ks != 3):
+                    continue
+                try:
+                    us, gbs, tfs = conv_case(B, H, W, ci, co, ks, variant=v, fm=fm, **fl)
+                except RuntimeError:
+                    continue   # configuration does not apply to this shape
+                print("%-32s %3d%s %9.1f %9.1f %9.1f" % (name, v, "f" if fm else " ", us, gbs, tfs), flush=True)
 
 
 if __name__ == "__main__":

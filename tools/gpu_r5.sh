@@ -44,14 +44,14 @@ case $JOB in
   ab)
     # library A/B: optional tests, the conv microbench cases ${MB} and the step, HEAD build vs $BASE
     [ -n "$TFILES" ] && TAILN=8 step pytest.log timeout -k 10 900 $PYT $TFILES ${TK:+-k "$TK"}
-    if [ -n "$MB" ]; then
-      TAILN=40 step mb_new.log timeout -k 10 300 python3 -u tools/conv_microbench.py $MB
-      TAILN=40 step mb_base.log env RNVP_LIB_PATH=$R/${BASE:-tools/variants/lib_base.so} timeout -k 10 300 python3 -u tools/conv_microbench.py $MB
-    fi
+    # BASE: a library built from the SAME header revision (the binding refuses
+    # another one: rnvp_struct_size); without it only the HEAD build runs
+    [ -n "$MB" ] && TAILN=40 step mb_new.log timeout -k 10 300 python3 -u tools/conv_microbench.py $MB
+    [ -n "$MB" ] && [ -n "$BASE" ] && TAILN=40 step mb_base.log env RNVP_LIB_PATH=$R/$BASE timeout -k 10 300 python3 -u tools/conv_microbench.py $MB
     [ -n "$STAMPS" ] && TAILN=40 step stamps.log timeout -k 10 300 python3 -u tools/probe/deep_stamps.py
     STEPS=${STEPS:-30} bench _new
-    step bench_base.log env RNVP_LIB_PATH=$R/${BASE:-tools/variants/lib_base.so} timeout -k 10 300 python3 -u bench.py --steps ${STEPS:-30} --warmup 5 --no-cpu-baseline --no-secondary
-    STEPS=${STEPS:-30} bench _new2
+    [ -n "$BASE" ] && step bench_base.log env RNVP_LIB_PATH=$R/$BASE timeout -k 10 300 python3 -u bench.py --steps ${STEPS:-30} --warmup 5 --no-cpu-baseline --no-secondary
+    [ -n "$BASE" ] && STEPS=${STEPS:-30} bench _new2
     [ -n "$TRACE" ] && trace
     ;;
   *) echo "unknown job $JOB"; exit 2;;
