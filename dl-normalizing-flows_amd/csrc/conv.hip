@@ -1516,36 +1516,38 @@ constexpr int WN_TCO = 32, WN_TCI = 32, WN_TCI1 = 256;
 __host__ __device__ constexpr int wn_tci(int ks) { return ks == 1 ? WN_TCI1 : WN_TCI; }
 
 // The fragment-major copies (rnvp_wn_desc.wf_frag / wd_frag, read by the deep
-// 3x3 tiles through rnvp_conv_args.w_frag) of one [32 co] x [32 ci] x 3x3
-// tile: block (row / 16, k / 32) of 512 elements, lane L = row % 16 + 16 *
-// (k % 32 / 8) holding k % 8 = 0..7.  With cs_in, cs_out, co0 and ci0
-// multiples of 32 every block of the tile (per tap one 32-k block per 16
-// rows) lies wholly in this tile and is written whole: 16-byte stores, 1 KiB
-// per block.  val(c, ci, tap) is the tile's value of w[co0 + c][ci0 + ci][tap]
-// as the row-major image holds it (0 outside the conv's rows / channels).
+// tiles through rnvp_conv_args.w_frag) of one k_wn_pack / k_wn_wd tile
+// ([32 co] x [32 ci] x 3x3, or [32 co] x [256 ci] for 1x1): block (row / 16,
+// k / 32) of 512 elements, lane L = row % 16 + 16 * (k % 32 / 8) holding
+// k % 8 = 0..7.  With cs_in, cs_out, co0 and ci0 multiples of 32 every block
+// the tile touches lies wholly in it (per tap: 16 rows x 32 ci, resp. 16 ci x
+// 32 co) and is written whole: 16-byte stores, 1 KiB per block.
+// val(c, ci, tap) is the tile's value of w[co0 + c][ci0 + ci][tap] as the
+// row-major image holds it (0 outside the conv's rows / channels).
 template <typename T, typename F>
 __device__ __forceinline__ void wn_frag_tile(const rnvp_wn_desc& d, int co0, int ci0, int nco, int ncc, F val) {
     if constexpr (sizeof(T) != 2) return;   // the deep tiles read fragment-major images in bf16 only
-    if (d.ks != 3) return;
-    const int rbo = (nco + 15) >> 4, rbi = (ncc + 15) >> 4;   // row blocks this tile owns
+    const int kk = d.ks * d.ks;
+    const int rbo = (nco + 15) >> 4, rbi = (ncc + 15) >> 4, nkb = (ncc + 31) >> 5;
     if (d.wf_frag) {
-        for (int q = threadIdx.x; q < rbo * 9 * 64; q += blockDim.x) {
-            const int L = q & 63, bt = q >> 6, rb = bt / 9, tap = bt - rb * 9;
-            const int c = rb * 16 + (L & 15), kg = L >> 4;
+        for (int q = threadIdx.x; q < rbo * kk * nkb * 64; q += blockDim.x) {
+            const int L = q & 63, r = q >> 6, kb = r % nkb, r2 = r / nkb, tap = r2 % kk, rb = r2 / kk;
+            const int c = rb * 16 + (L & 15), ci = kb * 32 + (L >> 4) * 8;
             float f[8];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) f[e] = (c < nco && kg * 8 + e < ncc) ? val(c, kg * 8 + e, tap) : 0.f;
-            T* dst = (T*)d.wf_frag + ((long long)((co0 >> 4) + rb) * (d.kp_f >> 5) + ((tap * d.cs_in + ci0) >> 5)) * 512 + L * 8;
+            for (int e = 0; e < 8; ++e) f[e] = (c < nco && ci + e < ncc) ? val(c, ci + e, tap) : 0.f;
+            T* dst = (T*)d.wf_frag +
+                     ((long long)((co0 >> 4) + rb) * (d.kp_f >> 5) + ((tap * d.cs_in + ci0) >> 5) + kb) * 512 + L * 8;
             *(RNVP_GLOBAL u32x4*)dst = pack(f, T());
         }
     }
     if (d.wd_frag) {
-        for (int q = threadIdx.x; q < rbi * 9 * 64; q += blockDim.x) {
-            const int L = q & 63, bt = q >> 6, rb = bt / 9, tp = bt - rb * 9;
-            const int ci = rb * 16 + (L & 15), kg = L >> 4;
+        for (int q = threadIdx.x; q < rbi * kk * 64; q += blockDim.x) {
+            const int L = q & 63, r = q >> 6, tp = r % kk, rb = r / kk;
+            const int ci = rb * 16 + (L & 15), co = (L >> 4) * 8;
             float f[8];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) f[e] = (ci < ncc && kg * 8 + e < nco) ? val(kg * 8 + e, ci, 8 - tp) : 0.f;
+            for (int e = 0; e < 8; ++e) f[e] = (ci < ncc && co + e < nco) ? val(co + e, ci, kk - 1 - tp) : 0.f;
             T* dst = (T*)d.wd_frag + ((long long)((ci0 >> 4) + rb) * (d.kp_d >> 5) + ((tp * d.cs_out + co0) >> 5)) * 512 + L * 8;
             *(RNVP_GLOBAL u32x4*)dst = pack(f, T());
         }

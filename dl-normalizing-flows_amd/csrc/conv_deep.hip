@@ -38,8 +38,8 @@ int launch_deep_nc(const rnvp_conv_args* a, hipStream_t s) {
     const dim3 blk(64 * NW);
     int xa, xb;
     xcd_blocks(a, (int)gm, (int)gn, BN, sizeof(T), &xa, &xb);
-    // the fragment-major weight image where the caller provides one (bf16 3x3)
-    if constexpr (sizeof(T) == 2 && KSZ == 3 && NC <= 4) {
+    // the fragment-major weight image where the caller provides one (bf16)
+    if constexpr (sizeof(T) == 2 && NC <= 4) {
         if (a->w_frag) {
             if (a->pro_bn_relu) k_conv_deep<T, BN, KSZ, true, NW, WK, DK, NC, true><<<grid, blk, shm, s>>>(*a, sh, xa, xb);
             else k_conv_deep<T, BN, KSZ, false, NW, WK, DK, NC, true><<<grid, blk, shm, s>>>(*a, sh, xa, xb);
@@ -109,7 +109,7 @@ int launch_cfg(const rnvp_conv_args* a, hipStream_t s, int cfg) {
 // grouped independent 1x1 convs: one launch, the convs' tiles concatenated
 // (block b -> the conv whose tile range holds b; every conv keeps its own
 // XCD-aware tile order).  Both prologue forms are compiled in.
-template <typename T, int BN, int NW, int WK, int DK, int NC>
+template <typename T, int BN, int NW, int WK, int DK, int NC, bool FM = false>
 __global__ __launch_bounds__(64 * NW) void k_net_group(const rnvp_group_kargs g) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     int b = blockIdx.x, c = 0;
@@ -118,15 +118,26 @@ __global__ __launch_bounds__(64 * NW) void k_net_group(const rnvp_group_kargs g)
         ++c;
     }
     if (g.conv[c].pro_bn_relu)
-        deep_tile<T, BN, 1, true, NW, WK, DK, NC>(g.conv[c], g.shards[c], g.xa[c], g.xb[c], b, g.tiles[c], lds);
+        deep_tile<T, BN, 1, true, NW, WK, DK, NC, FM>(g.conv[c], g.shards[c], g.xa[c], g.xb[c], b, g.tiles[c], lds);
     else
-        deep_tile<T, BN, 1, false, NW, WK, DK, NC>(g.conv[c], g.shards[c], g.xa[c], g.xb[c], b, g.tiles[c], lds);
+        deep_tile<T, BN, 1, false, NW, WK, DK, NC, FM>(g.conv[c], g.shards[c], g.xa[c], g.xb[c], b, g.tiles[c], lds);
 }
 
 using GroupKernel = void (*)(const rnvp_group_kargs);
 
 template <typename T, int BN, int NW, int WK, int DK>
-GroupKernel group_kernel_nc(int nc) {
+GroupKernel group_kernel_nc(int nc, bool fm) {
+    if constexpr (sizeof(T) == 2) {
+        if (fm) {   // every member carries a fragment-major weight image
+            switch (nc) {
+                case 1: return k_net_group<T, BN, NW, WK, DK, 1, true>;
+                case 2: return k_net_group<T, BN, NW, WK, DK, 2, true>;
+                case 4: return k_net_group<T, BN, NW, WK, DK, 4, true>;
+            }
+            return nullptr;
+        }
+    }
+    if (fm) return nullptr;
     switch (nc) {
         case 1: return k_net_group<T, BN, NW, WK, DK, 1>;
         case 2: return k_net_group<T, BN, NW, WK, DK, 2>;
@@ -139,20 +150,22 @@ GroupKernel group_kernel_nc(int nc) {
 
 // the configuration table of launch_cfg (cfg 0 / 1 / 4 / 5)
 template <typename T>
-GroupKernel group_kernel_t(int cfg, int nc) {
+GroupKernel group_kernel_t(int cfg, int nc, bool fm) {
     switch (cfg) {
-        case 0: return group_kernel_nc<T, 32, 4, 4, 8>(nc);
-        case 1: return group_kernel_nc<T, 64, 4, 4, 6>(nc);
-        case 4: return group_kernel_nc<T, 32, 8, 8, 8>(nc);
-        case 5: return group_kernel_nc<T, 64, 8, 8, 6>(nc);
+        case 0: return group_kernel_nc<T, 32, 4, 4, 8>(nc, fm);
+        case 1: return group_kernel_nc<T, 64, 4, 4, 6>(nc, fm);
+        case 4: return group_kernel_nc<T, 32, 8, 8, 8>(nc, fm);
+        case 5: return group_kernel_nc<T, 64, 8, 8, 6>(nc, fm);
     }
     return nullptr;
 }
 
-// klass = cfg | nc << 4
+// klass = cfg | nc << 4 | fm << 11 (fm: the members' fragment-major weight images)
+constexpr int GROUP_FM = 1 << 11;
 GroupKernel group_kernel(int dtype, int klass) {
-    const int cfg = klass & 15, nc = klass >> 4;
-    return dtype == RNVP_F32 ? group_kernel_t<float>(cfg, nc) : group_kernel_t<bf16_t>(cfg, nc);
+    const int cfg = klass & 15, nc = (klass >> 4) & 127;
+    const bool fm = (klass & GROUP_FM) != 0;
+    return dtype == RNVP_F32 ? group_kernel_t<float>(cfg, nc, fm) : group_kernel_t<bf16_t>(cfg, nc, fm);
 }
 
 struct GroupCfg { int bn, nw, wk; };
@@ -226,7 +239,9 @@ extern "C" int rnvp_net_group_prepare(rnvp_net_step* steps, int n, int* klass, i
         tiles += st.tiles;
     }
     if (tiles <= 0 || tiles >= (1ll << 31)) return RNVP_E_INVALID;
-    *klass = cfg | (nc << 4);
+    bool fm = a0.dtype == RNVP_BF16 && nc <= 4;
+    for (int i = 0; i < n; ++i) fm = fm && steps[i].conv.w_frag != nullptr && (((uintptr_t)steps[i].conv.w_frag) & 15) == 0;
+    *klass = cfg | (nc << 4) | (fm ? GROUP_FM : 0);
     *grid = (int)tiles;
     *lds_bytes = (int)lds;
     return group_kernel(a0.dtype, *klass) ? RNVP_OK : RNVP_E_UNSUPPORTED;

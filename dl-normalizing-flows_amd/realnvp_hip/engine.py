@@ -263,7 +263,10 @@ class CouplingEngine:
             ar.add("wd:" + name, spec.cin * kp_d * esz)
             ar.add("norm:" + name, spec.cout * 4)
             # bf16 3x3: fragment-major copies for the deep-scale tiles (rnvp_conv_args.w_frag),
-            # written beside the row-major images by the weight-norm pack / transpose kernels
+            # written beside the row-major images by the weight-norm pack / transpose kernels.
+            # (The 1x1 tiles and groups read them too, but their weight slices are small:
+            # copies for them measured a wash -- 0.1 ms of tile time against 0.05 ms more
+            # transpose traffic, gpurun_out/r5_fm1x1.)
             if dtype == "bf16" and spec.ks == 3:
                 if cs_in % 32 == 0:
                     ar.add("wff:" + name, round_up(spec.cout, 16) * kp_f * esz)

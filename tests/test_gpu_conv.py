@@ -360,15 +360,15 @@ def test_deep_family_vs_float64(case, cfg, dtype):
         assert rel(sums[1], s2) < 10 * tol, rel(sums[1], s2)
 
 
-# fragment-major weight images (rnvp_conv_args.w_frag, bf16 3x3 deep tiles):
-# the same MFMAs in the same order from another weight layout -- bitwise equal
+# fragment-major weight images (rnvp_conv_args.w_frag, bf16 deep tiles): the
+# same MFMAs in the same order from another weight layout -- bitwise equal
 # outputs to the row-major image, every configuration (w itself is zeros in
 # the w_frag run: a kernel that read it would miss the float64 reference)
-@pytest.mark.parametrize("cfg", [0, 1, 4, 5])
-@pytest.mark.parametrize("case", [c for c in DEEP_FAMILY if c[6] == 3], ids=[c[0] for c in DEEP_FAMILY if c[6] == 3])
+@pytest.mark.parametrize("cfg", range(DEEP_CFGS))
+@pytest.mark.parametrize("case", DEEP_FAMILY, ids=[c[0] for c in DEEP_FAMILY])
 def test_deep_frag_major_weights(case, cfg):
     name, B, H, W, cin, cout, ks, fl = case
-    if cin // ((4 if cfg < 2 else 8) * 32) > 4:
+    if (cin + 7) // 8 * 8 // ((4, 4, 1, 2, 8, 8)[cfg] * 32) > 4:
         pytest.skip("no fragment-major kernel beyond 4 channel chunks per wave (the row-major image is used)")
     try:
         a = run_case(B, H, W, cin, cout, ks, "bf16", variant=VARIANT_DEEP0 + cfg, **fl)

@@ -244,3 +244,69 @@ def test_group_c_abi_two_skip_convs():
     act = torch.relu((x - mean.float()) / torch.sqrt(var.float() + 1e-5) * gam + bet)
     assert rel(y1g, x @ w1.t()) < 1e-5
     assert rel(y2g, act @ w2.t()) < 1e-5
+
+
+def _frag_major(w):
+    """[n][kp] -> the fragment-major image of rnvp_conv_args.w_frag"""
+    n, kp = w.shape
+    npad = (n + 15) // 16 * 16
+    wp = torch.zeros(npad, kp, dtype=w.dtype, device=w.device)
+    wp[:n] = w
+    return wp.view(npad // 16, 16, kp // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
+
+
+def test_group_frag_major_members():
+    """bf16 grouped 1x1 convs whose members carry fragment-major weight images
+    (rnvp_conv_args.w_frag; their row-major w zeroed): bitwise the row-major
+    single launches"""
+    from realnvp_hip import _lib
+    from realnvp_hip._lib import BNSrc, ConvArgs, NetStep
+    from realnvp_hip.engine import stat_shards
+    L = _lib.lib()
+    B, H, W, Cc = 64, 4, 4, 512
+    M = B * H * W
+    torch.manual_seed(5)
+    x = torch.randn(M, Cc, device=DEV).to(torch.bfloat16)
+    ws = [(torch.randn(Cc, Cc, device=DEV) * 0.05).to(torch.bfloat16) for _ in range(2)]
+    wfs = [_frag_major(w) for w in ws]
+    zero = torch.zeros(Cc, Cc, device=DEV, dtype=torch.bfloat16)
+    sh = stat_shards(M)
+    bsum = torch.zeros(sh, 2, Cc, device=DEV, dtype=torch.float64)
+    bsum[0, 0] = x.double().sum(0)
+    bsum[0, 1] = (x.double() ** 2).sum(0)
+    gam = torch.rand(Cc, device=DEV) + 0.5
+    bet = torch.randn(Cc, device=DEV) * 0.1
+    s = torch.cuda.current_stream().cuda_stream
+
+    def run(grouped):
+        ys = [torch.zeros(M, Cc, device=DEV, dtype=torch.bfloat16) for _ in range(2)]
+        args = []
+        for i in range(2):
+            a = ConvArgs()
+            a.dtype, a.B, a.H, a.W, a.ks = 1, B, H, W, 1
+            a.x, a.cs_in, a.cin, a.kp = x.data_ptr(), Cc, Cc, Cc
+            a.w = zero.data_ptr() if grouped else ws[i].data_ptr()
+            a.w_frag = wfs[i].data_ptr() if grouped else None
+            a.y, a.cs_out, a.n = ys[i].data_ptr(), Cc, Cc
+            if i == 1:
+                a.pro_bn_relu = 1
+                a.pro = BNSrc(bsum.data_ptr(), float(M), None, None, gam.data_ptr(), bet.data_ptr(), 1e-5, sh)
+            args.append(a)
+        if grouped:
+            steps = (NetStep * 2)()
+            for st, a in zip(steps, args):
+                st.kind, st.conv, st.dgamma_off, st.dbeta_off = 0, a, -1, -1
+            k, g, lb = C.c_int(), C.c_int(), C.c_int()
+            assert L.net_group_prepare(steps, 2, C.byref(k), C.byref(g), C.byref(lb)) == 0
+            assert k.value & (1 << 11), "the fragment-major group kernel"
+            L.net_group(C.addressof(steps), 2, 1, k.value, g.value, lb.value, s)
+        else:
+            for a in args:
+                L.conv2d(C.byref(a), s)
+        torch.cuda.synchronize()
+        return ys
+
+    single, grouped = run(False), run(True)
+    for a, b in zip(single, grouped):
+        assert torch.equal(a, b)
+    assert rel(grouped[0].float(), x.float() @ ws[0].float().t()) < 1e-2
