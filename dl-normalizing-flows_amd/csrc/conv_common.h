@@ -413,7 +413,7 @@ __device__ __forceinline__ void bn_bwd_body(const rnvp_bn_bwd_args& a, double* d
 
 // deep-scale conv family (conv_deep.hip): number of configurations and the
 // launcher of configuration cfg (RNVP_E_UNSUPPORTED when it does not apply)
-constexpr int RNVP_DEEP_CFGS = 6;
+constexpr int RNVP_DEEP_CFGS = 7;
 int rnvp_deep_launch(const rnvp_conv_args* a, hipStream_t s, int cfg);
 int rnvp_deep_auto_cfg(const rnvp_conv_args* a);
 

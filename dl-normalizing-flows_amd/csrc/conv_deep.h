@@ -23,9 +23,9 @@ constexpr int DEEP_MAX_CS = 1024;    // prologue BN table capacity (channels)
 template <typename T>
 __host__ __device__ constexpr int deep_pitch(int cs) { return lds_mfma_pitch(cs, Mf<T>::CH); }
 
-template <typename T, int BN, int NW, int WK>
+template <typename T, int BN, int NW, int WK, int BM = DEEP_BM>
 size_t deep_lds_bytes(int cs, int W, int ks) {
-    constexpr int BM = DEEP_BM, TM = BM / 16, WM = NW / WK;
+    constexpr int TM = BM / 16, WM = NW / WK;
     constexpr int G = WK > 1 ? TM : WM;
     const int hal = (ks / 2) * (W + 1), R = BM + 2 * hal;
     const size_t head = 4 * (5 * (size_t)BN) + 8 * (2 * (size_t)G * BN) + 4 * 2 * (size_t)cs;
@@ -46,11 +46,12 @@ size_t deep_lds_bytes(int cs, int W, int ks) {
 // weight load of a wave is one contiguous KiB (eight whole 128-B lines)
 // instead of 64 B from each of 16 rows -- the row-major loads held the deep
 // 3x3 tiles to ~37 GB/s of weights per CU (TA busy ~55 cycles per load)
-template <typename T, int BN, int KSZ, bool PRO, int NW, int WK, int DK, int NC, bool FM = false>
+// BM: pixels per tile (64; 128 for the 3x3 tiles of cfg 6, which read each
+// weight slice for twice the pixels: half the weight stream per launch)
+template <typename T, int BN, int KSZ, bool PRO, int NW, int WK, int DK, int NC, bool FM = false, int BM = DEEP_BM>
 __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, int xa, int xb, int vb, int nvb,
                                           char* lds) {
     constexpr int NT = 64 * NW;
-    constexpr int BM = DEEP_BM;
     constexpr int CH = Mf<T>::CH, KS = 4 * CH;
     constexpr int TM = BM / 16, TN = BN / 16;
     constexpr int WM = NW / WK;
@@ -61,6 +62,10 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
     constexpr int G = WK > 1 ? TM : WM;          // stat partial groups per column
     constexpr int FR = WK > 1 ? (TM * TN) / NW : 1;
     static_assert(WK == 1 || FR * NW == TM * TN, "final tiles");
+    // TALL: more 16-pixel row groups than waves (BM = 128 with 4 waves): wave
+    // wid takes row groups wid, wid + NW, ... with all TN column tiles of each
+    constexpr bool TALL = WK > 1 && TM > NW;
+    static_assert(!TALL || TM % NW == 0, "row groups per wave");
     // the operand's channel stride is NC * WK * KS exactly (launcher): the BN
     // table needs ceil(cs / NT) channels per thread, not DEEP_MAX_CS's
     constexpr int CPT = (NC * WK * KS + NT - 1) / NT;
@@ -161,7 +166,10 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
     // epilogue elements of this thread: (pixel m, tile column col) of element e
     constexpr int NE = WK > 1 ? FR : TMW * TN;
     auto elem = [&](int e, int& m, int& col) {
-        if constexpr (WK > 1) {
+        if constexpr (TALL) {
+            m = m0 + (wid + NW * (e / TN)) * 16 + li;
+            col = (e % TN) * 16 + 4 * g;
+        } else if constexpr (WK > 1) {
             m = m0 + (wid % TM) * 16 + li;
             col = ((wid / TM) * FR + e) * 16 + 4 * g;
         } else {
@@ -302,13 +310,14 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
     DEEP_STAMP(3);
     // ---- epilogue ----
     const bool want_sums = a.out_sums || (epi_bn && a.epi_sums);
-    constexpr int NS = WK > 1 ? FR : TN;          // stat slots (distinct columns) per thread
+    constexpr int NS = (WK > 1 && !TALL) ? FR : TN;   // stat slots (distinct columns) per thread
     double s1[NS][4], s2[NS][4];
 #pragma unroll
     for (int f = 0; f < NS; ++f)
 #pragma unroll
         for (int r = 0; r < 4; ++r) s1[f][r] = s2[f][r] = 0.0;
-    const int grp = WK > 1 ? wid % TM : wm;
+    const int grp = TALL ? wid : (WK > 1 ? wid % TM : wm);
+    constexpr int GU = TALL ? NW : G;             // stat partial groups in use
     if constexpr (WK > 1) {
         // sum the WK partial tiles through LDS (aliases the activation tile)
         float* red = (float*)act;
@@ -326,10 +335,12 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
             elem(f, m, col);
             const int n = n0 + col;
             if (m >= M || n >= cso) continue;
-            floatx4 v = *(const floatx4*)&red[(fi * 16 + li) * RP + col];
+            const int ri = TALL ? wid + NW * (f / TN) : fi;   // the element's row group
+            const int sl = TALL ? f % TN : f;                    // its stat slot
+            floatx4 v = *(const floatx4*)&red[(ri * 16 + li) * RP + col];
 #pragma unroll
-            for (int w = 1; w < WK; ++w) v += *(const floatx4*)&red[(w * BM + fi * 16 + li) * RP + col];
-            epi4p<T>(a, (long long)m * cso + n, v, btab + col, epi_bn, etab + col, BN, s1[f], s2[f], N - n, pre[f]);
+            for (int w = 1; w < WK; ++w) v += *(const floatx4*)&red[(w * BM + ri * 16 + li) * RP + col];
+            epi4p<T>(a, (long long)m * cso + n, v, btab + col, epi_bn, etab + col, BN, s1[sl], s2[sl], N - n, pre[f]);
         }
     } else {
 #pragma unroll
@@ -350,7 +361,7 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
             for (int r = 0; r < 4; ++r) {
                 const double u1 = row_sum16(s1[f][r]), u2 = row_sum16(s2[f][r]);
                 if (li == 0) {
-                    const int cb = (WK > 1 ? ((wid / TM) * FR + f) : f) * 16 + 4 * g;
+                    const int cb = ((WK > 1 && !TALL) ? ((wid / TM) * FR + f) : f) * 16 + 4 * g;
                     sred[(grp * BN + cb + r) * 2] = u1;
                     sred[(grp * BN + cb + r) * 2 + 1] = u2;
                 }
@@ -362,7 +373,7 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
             if (n >= N) continue;
             double t1 = 0.0, t2 = 0.0;
 #pragma unroll
-            for (int q = 0; q < G; ++q) {
+            for (int q = 0; q < GU; ++q) {
                 t1 += sred[(q * BN + col) * 2];
                 t2 += sred[(q * BN + col) * 2 + 1];
             }
@@ -379,12 +390,12 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
 // pixel x channel tiles (xa | gm, xb | gn, xa * xb = grid / 8) whose unique
 // bytes (xa activation tiles + xb weight slices) are smallest: that is what
 // one XCD's L2 has to bring in.
-inline void xcd_blocks(const rnvp_conv_args* a, int gm, int gn, int bn, int esz, int* xa, int* xb) {
+inline void xcd_blocks(const rnvp_conv_args* a, int gm, int gn, int bn, int esz, int* xa, int* xb, int bm = DEEP_BM) {
     *xa = -1;
     *xb = 1;
     const long long per = (long long)gm * gn / 8;
     const int hal = (a->ks / 2) * (a->W + 1);
-    const double act = (double)(DEEP_BM + 2 * hal) * a->cs_in * esz;
+    const double act = (double)(bm + 2 * hal) * a->cs_in * esz;
     const double wsl = (double)bn * a->ks * a->ks * a->cs_in * esz;
     double best = 1e300;
     for (int x = 1; x <= gm; ++x) {

@@ -21,34 +21,34 @@
 
 namespace {
 
-template <typename T, int BN, int KSZ, bool PRO, int NW, int WK, int DK, int NC, bool FM = false>
+template <typename T, int BN, int KSZ, bool PRO, int NW, int WK, int DK, int NC, bool FM = false, int BM = DEEP_BM>
 __global__ __launch_bounds__(64 * NW) void k_conv_deep(rnvp_conv_args a, int shards, int xa, int xb) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
-    deep_tile<T, BN, KSZ, PRO, NW, WK, DK, NC, FM>(a, shards, xa, xb, blockIdx.x, gridDim.x, lds);
+    deep_tile<T, BN, KSZ, PRO, NW, WK, DK, NC, FM, BM>(a, shards, xa, xb, blockIdx.x, gridDim.x, lds);
 }
 
-template <typename T, int BN, int NW, int WK, int DK, int NC, int KSZ>
+template <typename T, int BN, int NW, int WK, int DK, int NC, int KSZ, int BM = DEEP_BM>
 int launch_deep_nc(const rnvp_conv_args* a, hipStream_t s) {
     const long long M = (long long)a->B * a->H * a->W;
-    const size_t shm = deep_lds_bytes<T, BN, NW, WK>(a->cs_in, a->W, a->ks);
+    const size_t shm = deep_lds_bytes<T, BN, NW, WK, BM>(a->cs_in, a->W, a->ks);
     if (shm > 160 * 1024) return RNVP_E_UNSUPPORTED;
-    const long long gm = (M + DEEP_BM - 1) / DEEP_BM, gn = (a->n + BN - 1) / BN;
+    const long long gm = (M + BM - 1) / BM, gn = (a->n + BN - 1) / BN;
     const unsigned grid = (unsigned)(gm * gn);
     const int sh = rnvp_stat_shards(M);
     const dim3 blk(64 * NW);
     int xa, xb;
-    xcd_blocks(a, (int)gm, (int)gn, BN, sizeof(T), &xa, &xb);
+    xcd_blocks(a, (int)gm, (int)gn, BN, sizeof(T), &xa, &xb, BM);
     // the fragment-major weight image where the caller provides one (bf16)
     if constexpr (sizeof(T) == 2 && NC <= 4) {
         if (a->w_frag) {
-            if (a->pro_bn_relu) k_conv_deep<T, BN, KSZ, true, NW, WK, DK, NC, true><<<grid, blk, shm, s>>>(*a, sh, xa, xb);
-            else k_conv_deep<T, BN, KSZ, false, NW, WK, DK, NC, true><<<grid, blk, shm, s>>>(*a, sh, xa, xb);
+            if (a->pro_bn_relu) k_conv_deep<T, BN, KSZ, true, NW, WK, DK, NC, true, BM><<<grid, blk, shm, s>>>(*a, sh, xa, xb);
+            else k_conv_deep<T, BN, KSZ, false, NW, WK, DK, NC, true, BM><<<grid, blk, shm, s>>>(*a, sh, xa, xb);
             RNVP_LAUNCH_CHECK();
             return RNVP_OK;
         }
     }
-    if (a->pro_bn_relu) k_conv_deep<T, BN, KSZ, true, NW, WK, DK, NC><<<grid, blk, shm, s>>>(*a, sh, xa, xb);
-    else k_conv_deep<T, BN, KSZ, false, NW, WK, DK, NC><<<grid, blk, shm, s>>>(*a, sh, xa, xb);
+    if (a->pro_bn_relu) k_conv_deep<T, BN, KSZ, true, NW, WK, DK, NC, false, BM><<<grid, blk, shm, s>>>(*a, sh, xa, xb);
+    else k_conv_deep<T, BN, KSZ, false, NW, WK, DK, NC, false, BM><<<grid, blk, shm, s>>>(*a, sh, xa, xb);
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
 }
@@ -85,6 +85,27 @@ int launch_deep(const rnvp_conv_args* a, hipStream_t s) {
     return RNVP_E_UNSUPPORTED;
 }
 
+// 128-pixel 3x3 tiles (bf16, <= 4 channel chunks per wave): each weight
+// slice serves twice the pixels of the 64-pixel tiles
+template <typename T, int BN, int NW, int WK, int DK>
+int launch_deep_tall(const rnvp_conv_args* a, hipStream_t s) {
+    constexpr int KS = 4 * Mf<T>::CH;
+    if constexpr (sizeof(T) != 2) {
+        return RNVP_E_UNSUPPORTED;
+    } else {
+        const long long M = (long long)a->B * a->H * a->W;
+        if (a->ks != 3 || M > 65536 || a->n < BN / 2 || a->cs_in % (WK * KS)) return RNVP_E_UNSUPPORTED;
+        if (a->pro_bn_relu && a->pro.sums && a->pro.shards > 2) return RNVP_E_UNSUPPORTED;
+        if (a->epi_relu_bn_bwd && a->epi.sums && a->epi.shards > 2) return RNVP_E_UNSUPPORTED;
+        switch (a->cs_in / (WK * KS)) {
+            case 1: return launch_deep_nc<T, BN, NW, WK, DK, 1, 3, 128>(a, s);
+            case 2: return launch_deep_nc<T, BN, NW, WK, DK, 2, 3, 128>(a, s);
+            case 4: return launch_deep_nc<T, BN, NW, WK, DK, 4, 3, 128>(a, s);
+        }
+        return RNVP_E_UNSUPPORTED;
+    }
+}
+
 //                       BN  NW  WK  DK
 // cfg 0                 32   4   4   8   whole 64x32 tile per wave, K / 4 (deep K)
 // cfg 1                 64   4   4   6   whole 64x64 tile per wave, K / 4
@@ -92,6 +113,7 @@ int launch_deep(const rnvp_conv_args* a, hipStream_t s) {
 // cfg 3                 32   4   2   8   32-pixel halves x K / 2
 // cfg 4                 32   8   8   8   cfg 0 with 8 waves (two per SIMD: one's memory waits under the other's MFMAs)
 // cfg 5                 64   8   8   6   cfg 1 with 8 waves
+// cfg 6                 32   4   4   8   cfg 0 on 128-pixel tiles (bf16 3x3)
 template <typename T>
 int launch_cfg(const rnvp_conv_args* a, hipStream_t s, int cfg) {
     switch (cfg) {
@@ -101,6 +123,7 @@ int launch_cfg(const rnvp_conv_args* a, hipStream_t s, int cfg) {
         case 3: return a->ks == 1 ? launch_deep<T, 32, 4, 2, 8>(a, s) : RNVP_E_UNSUPPORTED;
         case 4: return launch_deep<T, 32, 8, 8, 8>(a, s);
         case 5: return launch_deep<T, 64, 8, 8, 6>(a, s);
+        case 6: return launch_deep_tall<T, 32, 4, 4, 8>(a, s);
     }
     return RNVP_E_INVALID;
 }
@@ -297,6 +320,10 @@ int rnvp_deep_auto_cfg(const rnvp_conv_args* a) {
     const int kc = a->dtype == RNVP_F32 ? 16 : 32;   // channels per k-step
     if (M <= 1024) return a->cs_in % (8 * kc) == 0 ? 4 : 0;
     if (dgrad) return 0;
+    // 128-pixel tiles for the bf16 3x3 forward convs at 128 channels (scale 3:
+    // 21.8 vs 22.6-23.1 us with fragment-major weights; data gradients and the
+    // wider channels measured slower, gpurun_out/r5_tall)
+    if (a->ks == 3 && a->dtype == RNVP_BF16 && M > 4096 && a->cs_in == 128) return 6;
     // (32-channel tiles for the forward convs as well measured slower in the
     // step, profiles/r4_step_ab.txt)
     return a->cs_in % (8 * kc) == 0 ? 5 : 1;

@@ -338,7 +338,7 @@ DEEP_FAMILY = DEEP + [
     ("s4_3x3_ragged_m", 3, 7, 9, 256, 200, 3, dict(pro=True, stats=True)),                # M % 64 != 0, N % 64 != 0
     ("s2_1x1_64", 8, 32, 32, 64, 64, 1, dict(pro=True, residual=True, stats=True)),
 ]
-DEEP_CFGS = 6
+DEEP_CFGS = 7
 VARIANT_DEEP0 = 16
 
 
@@ -368,7 +368,7 @@ def test_deep_family_vs_float64(case, cfg, dtype):
 @pytest.mark.parametrize("case", DEEP_FAMILY, ids=[c[0] for c in DEEP_FAMILY])
 def test_deep_frag_major_weights(case, cfg):
     name, B, H, W, cin, cout, ks, fl = case
-    if (cin + 7) // 8 * 8 // ((4, 4, 1, 2, 8, 8)[cfg] * 32) > 4:
+    if (cin + 7) // 8 * 8 // ((4, 4, 1, 2, 8, 8, 4)[cfg] * 32) > 4:
         pytest.skip("no fragment-major kernel beyond 4 channel chunks per wave (the row-major image is used)")
     try:
         a = run_case(B, H, W, cin, cout, ks, "bf16", variant=VARIANT_DEEP0 + cfg, **fl)

@@ -175,7 +175,7 @@ def main():
     variants = [0, 1] if "--v01" in sys.argv else [0]
     fms = [False, True] if "--fm" in sys.argv else [False]
     if "--deep" in sys.argv:   # the deep-scale family's configurations (RNVP_VARIANT_DEEP0 + c)
-        variants = [0] + [16 + c for c in range(6)]
+        variants = [0] + [16 + c for c in range(7)]
     only = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--case=")]
     print("%-32s %3s %9s %9s %9s" % ("case", "var", "us", "GB/s", "TFLOP/s"))
     for name, B, H, W, ci, co, ks, fl in CASES:
