@@ -550,11 +550,12 @@ def main():
             out["dp"] = dp
     del tr, model
     torch.cuda.empty_cache()
-    if rank == 0 and world == 1:
-        if not args.no_secondary:
-            out["secondary"] = secondary(args, dev)
-        if not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0 and world == 1 and not args.no_secondary:
+        out["secondary"] = secondary(args, dev)
+    # the CPU baseline on rank 0 at every world size, after the timed region
+    # (the other ranks wait at the closing barrier; --cpu-steps bounds it)
+    if rank == 0 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if pg is not None:

@@ -14,6 +14,9 @@
 // Product D[n][m] = W[n][k] X[m][k]^T: a lane owns 4 consecutive output
 // channels of one pixel (8-byte epilogue vectors).
 #include "common.h"
+#include <map>
+#include <mutex>
+
 #include "conv_common.h"
 
 #include <type_traits>
@@ -549,18 +552,25 @@ int rnvp_s1_fanout_prepare(rnvp_net_step* steps, int n, int* klass, int* grid, i
 int rnvp_s1_fanout_launch(const rnvp_group_kargs& g, int klass, int grid, int lds_bytes, hipStream_t s) {
     const int nt = (klass >> 4) & 15, nks = klass & 15;
     const FanKernel k = fan_kernel(nt, nks);
-    // resident workgroups per CU of this kernel at this LDS size (cached per
-    // kernel and LDS size; the members' weights make the LDS size vary)
-    static int cache_lds[3][2] = {{-1, -1}, {-1, -1}, {-1, -1}}, cache_n[3][2];
-    const int ti = nt == 1 ? 0 : (nt == 2 ? 1 : 2), ki = nks == 1 ? 0 : 1;
-    if (cache_lds[ti][ki] != lds_bytes) {
-        int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, lds_bytes) != hipSuccess || per_cu < 1)
-            per_cu = 1;
-        cache_n[ti][ki] = per_cu;
-        cache_lds[ti][ki] = lds_bytes;
+    // resident workgroups per CU of this kernel at this LDS size: one runtime
+    // query per (kernel, LDS size) -- the members' weights make the LDS size
+    // vary -- cached behind a lock (launches may come from several threads;
+    // the query is not a stream operation, so a capture in progress is fine)
+    static std::mutex mu;
+    static std::map<long long, int> occ;
+    const long long key = ((long long)klass << 32) | (unsigned)lds_bytes;
+    int per_cu;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = occ.find(key);
+        if (it == occ.end()) {
+            int q = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&q, k, 256, lds_bytes) != hipSuccess || q < 1) q = 1;
+            it = occ.emplace(key, q).first;
+        }
+        per_cu = it->second;
     }
-    const long long cap = 256LL * cache_n[ti][ki];
+    const long long cap = 256LL * per_cu;
     hipLaunchKernelGGL(k, dim3((unsigned)(grid < cap ? grid : cap)), dim3(256), lds_bytes, s, g);
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;

@@ -9,151 +9,9 @@
 // Flow tensors are NCHW fp32, net tensors NHWC; the reductions and the
 // NHWC-touching passes run on pixel tiles (see "pixel tiles" below), the
 // purely elementwise NCHW passes grid-stride.
-#include <math.h>
-
-#include "common.h"
+#include "coupling_common.h"
 
 namespace {
-
-struct Geo {
-    int kind, B, C, H, W, HW, Cb, cfg, on_base, off_base;
-};
-
-__device__ __forceinline__ Geo geo(const rnvp_coupling_args& a) {
-    Geo g;
-    g.kind = a.kind; g.B = a.B; g.C = a.C; g.H = a.H; g.W = a.W; g.HW = a.H * a.W;
-    g.cfg = a.mask_config ? 1 : 0;
-    if (a.kind == 0) {
-        g.Cb = a.C; g.on_base = 0; g.off_base = 0;
-    } else {
-        g.Cb = a.C / 2;
-        // mask_config truthy: (on, off) = (top, bottom) halves (modules_realnvp.py:333-336)
-        g.on_base = g.cfg ? 0 : g.Cb;
-        g.off_base = g.cfg ? g.Cb : 0;
-    }
-    return g;
-}
-
-// checkerboard mask at pixel p (= h*W + w): 1 = kept ("masked in") position
-__device__ __forceinline__ int ckbd_m(const Geo& g, int p) { return (g.cfg + p / g.W + p % g.W) & 1; }
-
-// number of transformed (mask == 0) positions per (sample, channel)
-__device__ __forceinline__ double n_transformed(const Geo& g) {
-    if (g.kind == 1) return (double)g.HW;
-    const long long total = (long long)g.H * g.W;
-    // positions with (i + j) even
-    const long long even = ((g.H & 1) && (g.W & 1)) ? (total + 1) / 2 : total / 2;
-    // mask == 0  <=>  (cfg + i + j) even
-    return (double)(g.cfg ? total - even : even);
-}
-
-template <typename T>
-__device__ __forceinline__ const T* cptr(const void* p) { return (const T*)p; }
-
-// ---------------------------------------------------------------------------
-// pixel tiles
-// ---------------------------------------------------------------------------
-// A workgroup owns TP consecutive pixels of one image (all channels): NCHW
-// flow-tensor planes are read/written as coalesced TP-runs per channel, the
-// NHWC net tensors (h0, st and their gradients) as one contiguous
-// [TP][cs] region staged through LDS, per-channel reductions are wave
-// segment sums (seg = min(TP, 64) lanes share a channel) folded into LDS and
-// then one global atomic per channel per workgroup.
-struct Tile {
-    int b, p0, tp;
-    long long m0;
-};
-
-__device__ __forceinline__ Tile tile_of(const Geo& g, int TP) {
-    const int tpi = (g.HW + TP - 1) / TP;
-    Tile t;
-    t.b = blockIdx.x / tpi;
-    t.p0 = (blockIdx.x - t.b * tpi) * TP;
-    t.tp = min(TP, g.HW - t.p0);
-    t.m0 = (long long)t.b * g.HW + t.p0;
-    return t;
-}
-
-// Elements of a block's first CP_K passes (e0 = 256 k) whose global operands
-// are loaded at kernel entry, before the BN tables / LDS tiles: their memory
-// round trip overlaps the table's (one exposed latency instead of two or
-// three per launch; at the deep scales every thread has <= 2 elements)
-constexpr int CP_K = 4;
-
-// sum over groups of `seg` lanes (power of 2 <= 64; 1 = no reduction)
-__device__ __forceinline__ float seg_sum(float v, int seg) {
-    for (int o = 1; o < seg; o <<= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-__device__ __forceinline__ double seg_sum(double v, int seg) {
-    for (int o = 1; o < seg; o <<= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-// per-channel sums of doubles over a lane segment: seg >= 16 (the wide
-// scales) -> DPP row sums on the VALU, every 16-lane row's lane 0 then adds
-// its row (rows never straddle a segment); shorter segments -> ds_bpermute
-// shuffles.  The shuffles were the coupling passes' bottleneck at the wide
-// scales (6 steps x 2 bpermutes per double and quantity).  seg_mask: a lane
-// with (lane & seg_mask(seg)) == 0 holds a sum to add.
-__device__ __forceinline__ double seg_red(double v, int seg) { return seg >= 16 ? row_sum16(v) : seg_sum(v, seg); }
-__device__ __forceinline__ int seg_mask(int seg) { return seg >= 16 ? 15 : seg - 1; }
-
-template <typename T>
-__device__ __forceinline__ void tile_copy_in(const void* src, long long m0, int tp, int cs, T* lds) {
-    const int n16 = tp * cs * (int)sizeof(T) / 16;
-    const u32x4* s = (const u32x4*)((const T*)src + m0 * cs);
-    u32x4* d = (u32x4*)lds;
-    for (int i = threadIdx.x; i < n16; i += blockDim.x) d[i] = s[i];
-}
-
-template <typename T>
-__device__ __forceinline__ void tile_copy_out(const T* lds, long long m0, int tp, int cs, void* dst) {
-    const int n16 = tp * cs * (int)sizeof(T) / 16;
-    const u32x4* s = (const u32x4*)lds;
-    u32x4* d = (u32x4*)((T*)dst + m0 * cs);
-    for (int i = threadIdx.x; i < n16; i += blockDim.x) d[i] = s[i];
-}
-
-__device__ __forceinline__ void lds_zero(double* p, int n) {
-    for (int i = threadIdx.x; i < n; i += blockDim.x) p[i] = 0.0;
-}
-
-// coupling reductions: [RNVP_COUPLING_SHARDS][k*Cb] fp64, this block's shard
-__device__ __forceinline__ double* cshard(double* sums, int width) {
-    return sums + (long long)(blockIdx.x % RNVP_COUPLING_SHARDS) * width;
-}
-// sum over the shards of entry i of a [shards][width] reduction.  Fully
-// unrolled: all RNVP_COUPLING_SHARDS loads are independent and go out
-// together (one memory round trip, not one per unroll group), then are
-// added in shard order.
-__device__ __forceinline__ double csum(const double* sums, int width, int i) {
-    double v[RNVP_COUPLING_SHARDS];
-#pragma unroll
-    for (int h = 0; h < RNVP_COUPLING_SHARDS; ++h) v[h] = sums[(long long)h * width + i];
-    double t = 0.0;
-#pragma unroll
-    for (int h = 0; h < RNVP_COUPLING_SHARDS; ++h) t += v[h];
-    return t;
-}
-
-// per-channel in_bn table of the in part: scale, shift, mean, rstd [Cb each]
-__device__ __forceinline__ void in_bn_table(const rnvp_coupling_args& a, const Geo& g, float* t) {
-    for (int cb = threadIdx.x; cb < g.Cb; cb += blockDim.x) {
-        rnvp_bn_src s;
-        s.shards = RNVP_COUPLING_SHARDS;
-        s.sums = a.training ? a.in_sums : nullptr;
-        s.count = (double)g.B * g.HW;
-        s.mean = a.in_rmean; s.var = a.in_rvar;
-        s.gamma = a.in_gamma; s.beta = a.in_beta; s.eps = a.eps;
-        float sc, sf, mean, rstd;
-        bn_affine(s, g.Cb, cb, sc, sf, &mean, &rstd);
-        t[cb] = sc;
-        t[g.Cb + cb] = sf;
-        t[2 * g.Cb + cb] = mean;
-        t[3 * g.Cb + cb] = rstd;
-    }
-}
 
 // ---------------------------------------------------------------------------
 // in part, forward
@@ -275,10 +133,9 @@ __global__ __launch_bounds__(256) void k_out1(rnvp_coupling_args a, int TP, int 
     const Geo g = geo(a);
     const Tile t = tile_of(g, TP);
     const int lane = threadIdx.x & 63;
-    double* red = dsm;                          // [4*Cb] (+ pad to 16 B): out_bn sums | next_sums
+    double* red = dsm;                          // [2*Cb] (+ pad to 16 B): out_bn sums
     __shared__ float redl[16];
-    T* st = (T*)(dsm + 4 * ((g.Cb + 1) / 2 * 2));   // [tp][cs_st]
-    const bool nxt = a.next_sums != nullptr && g.kind == 0;
+    T* st = (T*)(dsm + 2 * ((g.Cb + 1) / 2 * 2));   // [tp][cs_st]
     const int total = g.C * t.tp;
     auto xidx = [&](int e) {
         const int c = e / t.tp, pl = e - c * t.tp;
@@ -290,7 +147,7 @@ __global__ __launch_bounds__(256) void k_out1(rnvp_coupling_args a, int TP, int 
         const int e = k * 256 + threadIdx.x;
         { const float v = a.x[xidx(e < total ? e : 0)]; xp[k] = e < total ? v : 0.f; }   // unconditional (clamped) load: no branch, no wait
     }
-    lds_zero(red, 4 * g.Cb);
+    lds_zero(red, 2 * g.Cb);
     tile_copy_in<T>(a.st, t.m0, t.tp, a.cs_st, st);
     __syncthreads();
     const float sc = a.scale[0], ss = a.scale_shift[0];
@@ -317,13 +174,6 @@ __global__ __launch_bounds__(256) void k_out1(rnvp_coupling_args a, int TP, int 
             atomicAdd(&red[cb], s1);
             atomicAdd(&red[g.Cb + cb], s2);
         }
-        if (nxt) {   // uniform: the transformed positions' share, for the next coupling's in_bn
-            const double t1 = seg_red(tr ? (double)u : 0.0, seg), t2 = seg_red(tr ? (double)u * u : 0.0, seg);
-            if (ok && (lane & seg_mask(seg)) == 0) {
-                atomicAdd(&red[2 * g.Cb + cb], t1);
-                atomicAdd(&red[3 * g.Cb + cb], t2);
-            }
-        }
     };
     // e0 is block-uniform (seg_sum shuffles need every lane)
 #pragma unroll
@@ -339,178 +189,6 @@ __global__ __launch_bounds__(256) void k_out1(rnvp_coupling_args a, int TP, int 
         double* dst = cshard(a.out_sums, 2 * g.Cb);
         for (int c = threadIdx.x; c < 2 * g.Cb; c += blockDim.x) atomicAdd(&dst[c], red[c]);
     }
-    if (nxt) {
-        double* dst = cshard(a.next_sums, 2 * g.Cb);
-        for (int c = threadIdx.x; c < 2 * g.Cb; c += blockDim.x) atomicAdd(&dst[c], red[2 * g.Cb + c]);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// chained couplings, forward: z of coupling a AND the in part of coupling nx
-// (nx->x == a->z, same kind and shape, opposite mask) in one pass
-// ---------------------------------------------------------------------------
-// a's out_bn batch statistics of channel cb (fp64) and the closed-form in_bn
-// sums of nx over the positions nx's in_bn reads (= a's transformed ones,
-// where z = (u - mean_f) * rstd_f with the fp32 mean / rstd k_out2 applies)
-__device__ __forceinline__ void chain_in_sums(const rnvp_coupling_args& a, const Geo& g, int cb, float& mean_f,
-                                              float& rstd_f, float& hlv, double& D1, double& D2) {
-    const double cnt = (double)g.B * g.HW;
-    const double o1 = csum(a.out_sums, 2 * g.Cb, cb), o2 = csum(a.out_sums, 2 * g.Cb, g.Cb + cb);
-    const double mean = o1 / cnt;
-    double var = o2 / cnt - mean * mean;
-    if (var < 0) var = 0;
-    mean_f = (float)mean;
-    rstd_f = (float)(1.0 / sqrt(var + (double)a.eps));
-    hlv = (float)(0.5 * log(var + (double)a.eps));
-    double S1, S2, n;
-    if (g.kind == 0) {   // the transformed squares only
-        S1 = csum(a.next_sums, 2 * g.Cb, cb);
-        S2 = csum(a.next_sums, 2 * g.Cb, g.Cb + cb);
-        n = (double)g.B * n_transformed(g);
-    } else {             // the whole transformed half
-        S1 = o1;
-        S2 = o2;
-        n = cnt;
-    }
-    const double m = (double)mean_f, r = (double)rstd_f;
-    D1 = r * (S1 - n * m);
-    D2 = r * r * (S2 - 2.0 * m * S1 + n * m * m);
-    if (D2 < 0) D2 = 0;
-}
-
-template <typename T>
-__global__ __launch_bounds__(256) void k_out2_in(rnvp_coupling_args a, rnvp_coupling_args nx, int TP, int main_grid) {
-    extern __shared__ double dsm[];
-    if ((int)blockIdx.x >= main_grid) {
-        // extra workgroups: one s/t-net BatchNorm running-stat update each (as k_out2)
-        const rnvp_bn_running r = a.net_running[blockIdx.x - main_grid];
-        double* tmp = dsm;   // [2*C]
-        block_shard_sums(r.sums, r.C, r.shards, 0, r.C, tmp, tmp + r.C);
-        const float mom = a.momentum;
-        for (int c = threadIdx.x; c < r.C; c += blockDim.x) {
-            double mean = tmp[c] / r.count;
-            double var = tmp[r.C + c] / r.count - mean * mean;
-            if (var < 0) var = 0;
-            double unb = r.count > 1 ? var * r.count / (r.count - 1) : var;
-            r.rmean[c] = (1.f - mom) * r.rmean[c] + mom * (float)mean;
-            r.rvar[c] = (1.f - mom) * r.rvar[c] + mom * (float)unb;
-        }
-        if (threadIdx.x == 0 && r.nbt) r.nbt[0] += 1;
-        return;
-    }
-    const Geo g = geo(a), gn = geo(nx);
-    const Tile t = tile_of(g, TP);
-    const int Cb = g.Cb, Cr = (Cb + 3) / 4 * 4;
-    float* ot = (float*)dsm;                     // a's out_bn: mean | rstd | half log var [Cr each]
-    float* it = ot + 3 * Cr;                     // nx's in_bn: scale | shift [Cr each]
-    T* h = (T*)(it + 2 * Cr);                    // nx's h0 tile [tp][cs_h0] (16-B aligned: 20*Cr B)
-    const int cs = nx.cs_h0;
-    const double cnt = (double)g.B * g.HW;
-    const int total = g.C * t.tp;
-    auto uidx = [&](int e) {
-        const int c = e / t.tp, pl = e - c * t.tp;
-        return ((long long)t.b * g.C + c) * g.HW + t.p0 + pl;
-    };
-    float up[CP_K];
-#pragma unroll
-    for (int k = 0; k < CP_K; ++k) {
-        const int e = k * 256 + threadIdx.x;
-        { const float v = a.u[uidx(e < total ? e : 0)]; up[k] = e < total ? v : 0.f; }
-    }
-    for (int cb = threadIdx.x; cb < Cb; cb += blockDim.x) {
-        float mf, rf, hl;
-        double D1, D2;
-        chain_in_sums(a, g, cb, mf, rf, hl, D1, D2);
-        ot[cb] = mf;
-        ot[Cr + cb] = rf;
-        ot[2 * Cr + cb] = hl;
-        // nx's in_bn from the closed-form sums, as bn_affine forms it
-        const double mean = D1 / cnt;
-        double var = D2 / cnt - mean * mean;
-        if (var < 0) var = 0;
-        const float rstd = (float)(1.0 / sqrt(var + (double)nx.eps));
-        const float gam = nx.in_gamma ? nx.in_gamma[cb] : 1.f, bet = nx.in_beta ? nx.in_beta[cb] : 0.f;
-        it[cb] = gam * rstd;
-        it[Cr + cb] = bet - (float)mean * gam * rstd;
-        if (blockIdx.x == 0) {
-            // a's out_bn running stats (as k_out2); nx's in_bn sums (shard 0) and running stats (as k_in_apply)
-            const double o1 = csum(a.out_sums, 2 * Cb, cb), o2 = csum(a.out_sums, 2 * Cb, Cb + cb);
-            const double om = o1 / cnt;
-            double ov = o2 / cnt - om * om;
-            if (ov < 0) ov = 0;
-            const double unb = cnt > 1 ? ov * cnt / (cnt - 1) : ov;
-            if (a.out_rmean) {
-                a.out_rmean[cb] = (1.f - a.momentum) * a.out_rmean[cb] + a.momentum * (float)om;
-                a.out_rvar[cb] = (1.f - a.momentum) * a.out_rvar[cb] + a.momentum * (float)unb;
-            }
-            nx.in_sums[cb] = D1;
-            nx.in_sums[Cb + cb] = D2;
-            if (nx.in_rmean) {
-                const double iu = cnt > 1 ? var * cnt / (cnt - 1) : var;
-                nx.in_rmean[cb] = (1.f - nx.momentum) * nx.in_rmean[cb] + nx.momentum * (float)mean;
-                nx.in_rvar[cb] = (1.f - nx.momentum) * nx.in_rvar[cb] + nx.momentum * (float)iu;
-            }
-        }
-    }
-    // nx's padding / mask channels of the h0 tile
-    for (int e = threadIdx.x; e < t.tp * cs; e += blockDim.x) {
-        const int pl = e / cs, ch = e - pl * cs;
-        if (ch >= 2 * Cb) {
-            float out = 0.f;
-            if (gn.kind == 0 && ch == 2 * Cb) out = (float)ckbd_m(gn, t.p0 + pl);
-            stv(&h[pl * cs + ch], out);
-        }
-    }
-    __syncthreads();
-    if (blockIdx.x == 0) {
-        if (threadIdx.x == 0) {
-            if (a.out_nbt) a.out_nbt[0] += 1;
-            if (nx.in_nbt) nx.in_nbt[0] += 1;
-        }
-        // per-sample constant of a: -sum_c 0.5*log(var_c+eps) * (#transformed positions per channel)
-        float k = 0.f;
-        for (int cb = 0; cb < Cb; ++cb) k += ot[2 * Cr + cb];
-        k = -k * (float)n_transformed(g);
-        for (int b = threadIdx.x; b < g.B; b += blockDim.x) a.ldj_sample[b] += k;
-    }
-    auto body = [&](int e, float u) {
-        const int c = e / t.tp, pl = e - c * t.tp, p = t.p0 + pl;
-        const long long idx = ((long long)t.b * g.C + c) * g.HW + p;
-        bool tr;
-        int cb;
-        if (g.kind == 0) {
-            tr = !ckbd_m(g, p);
-            cb = c;
-        } else {
-            tr = c >= g.on_base && c < g.on_base + Cb;
-            cb = c - g.on_base;
-        }
-        const float zv = tr ? (u - ot[cb]) * ot[Cr + cb] : u;
-        a.z[idx] = zv;
-        // nx's in part: masked input (checkerboard: every channel at nx's kept
-        // squares; channelwise: nx's conditioning half = a's transformed half)
-        int cn;
-        float xm;
-        if (gn.kind == 0) {
-            cn = c;
-            xm = ckbd_m(gn, p) ? zv : 0.f;
-        } else {
-            if (c < gn.off_base || c >= gn.off_base + Cb) return;
-            cn = c - gn.off_base;
-            xm = zv;
-        }
-        const float xa = xm * it[cn] + it[Cr + cn];
-        stv(&h[pl * cs + cn], fmaxf(xa, 0.f));
-        stv(&h[pl * cs + Cb + cn], fmaxf(-xa, 0.f));
-    };
-#pragma unroll
-    for (int k = 0; k < CP_K; ++k) {
-        const int e = k * 256 + threadIdx.x;
-        if (e < total) body(e, up[k]);
-    }
-    for (int e = CP_K * 256 + threadIdx.x; e < total; e += 256) body(e, a.u[uidx(e)]);
-    __syncthreads();
-    tile_copy_out<T>(h, t.m0, t.tp, cs, nx.h0);
 }
 
 // z = out_bn(u) on transformed positions; ldj var term; running stats.
@@ -850,6 +528,26 @@ __global__ __launch_bounds__(256) void k_out_bwd_apply(rnvp_coupling_args a, int
 // ---------------------------------------------------------------------------
 // in part, backward (through CReLU and in_bn)
 // ---------------------------------------------------------------------------
+// fold the out part's sharded scale / scale_shift partials into g_scale /
+// g_scale_shift (+=) and leave them zero (wave 0 of block 0; every partial
+// was written by an earlier launch)
+__device__ __forceinline__ void fold_gscale(const rnvp_coupling_args& a) {
+    const int l = threadIdx.x;
+    double v0 = 0.0, v1 = 0.0;
+    if (l < RNVP_COUPLING_SHARDS) {
+        v0 = a.gscale_part[2 * l];
+        v1 = a.gscale_part[2 * l + 1];
+        a.gscale_part[2 * l] = 0.0;
+        a.gscale_part[2 * l + 1] = 0.0;
+    }
+    v0 = wave_sum(v0);
+    v1 = wave_sum(v1);
+    if (l == 0) {
+        *a.g_scale += (float)v0;
+        *a.g_scale_shift += (float)v1;
+    }
+}
+
 // gxa = d/dxa of [relu(xa), relu(-xa)] . [g1, g2]; gh: LDS tile [tp][cs_gh0]
 template <typename T>
 __device__ __forceinline__ void in_bwd_vals(const rnvp_coupling_args& a, const Geo& g, const Tile& t, const T* gh,
@@ -869,8 +567,9 @@ __global__ __launch_bounds__(256) void k_in_bwd_red(rnvp_coupling_args a, int TP
     const Geo g = geo(a);
     const Tile t = tile_of(g, TP);
     const int lane = threadIdx.x & 63;
-    double* red = dsm;                                   // [2*Cb]
-    float* tab = (float*)(dsm + 2 * g.Cb);               // [4*Cb]
+    const bool ext = a.in_bwd_ext != nullptr;
+    double* red = dsm;                                   // [2*Cb] (+ [2*Cb] ext)
+    float* tab = (float*)(dsm + (ext ? 4 : 2) * g.Cb);   // [4*Cb]
     T* gh = (T*)(tab + 4 * ((g.Cb + 3) / 4 * 4));        // [tp][cs_gh0]
     const int total = g.Cb * t.tp;
     auto xidx = [&](int e) {
@@ -884,9 +583,10 @@ __global__ __launch_bounds__(256) void k_in_bwd_red(rnvp_coupling_args a, int TP
         const int e = k * 256 + threadIdx.x;
         { const float v = a.x[xidx(e < total ? e : 0)]; xp[k] = e < total ? v : 0.f; }   // unconditional (clamped) load: no branch, no wait
     }
-    lds_zero(red, 2 * g.Cb);
+    lds_zero(red, (ext ? 4 : 2) * g.Cb);
     in_bn_table(a, g, tab);
     tile_copy_in<T>(a.gh0, t.m0, t.tp, a.cs_gh0, gh);
+    if (blockIdx.x == 0 && a.gscale_part && threadIdx.x < 64) fold_gscale(a);
     __syncthreads();
     auto body = [&](int e0, float xv) {
         const int e = e0 + threadIdx.x;
@@ -899,6 +599,14 @@ __global__ __launch_bounds__(256) void k_in_bwd_red(rnvp_coupling_args a, int TP
             atomicAdd(&red[cb], s1);
             atomicAdd(&red[g.Cb + cb], s2);
         }
+        if (ext) {   // over the positions in_bn normalises (coupling links' closed forms)
+            const bool kept = ok && (g.kind != 0 || ckbd_m(g, t.p0 + pl));
+            const double e1 = seg_red(kept ? (double)gxa : 0.0, seg), e2 = seg_red(kept ? (double)gxa * xv : 0.0, seg);
+            if (ok && (lane & seg_mask(seg)) == 0) {
+                atomicAdd(&red[2 * g.Cb + cb], e1);
+                atomicAdd(&red[3 * g.Cb + cb], e2);
+            }
+        }
     };
 #pragma unroll
     for (int k = 0; k < CP_K; ++k)
@@ -910,38 +618,33 @@ __global__ __launch_bounds__(256) void k_in_bwd_red(rnvp_coupling_args a, int TP
     __syncthreads();
     double* dst = cshard(a.in_bwd_sums, 2 * g.Cb);
     for (int c = threadIdx.x; c < 2 * g.Cb; c += blockDim.x) atomicAdd(&dst[c], red[c]);
+    if (ext) {
+        double* dx = cshard(a.in_bwd_ext, 2 * g.Cb);
+        for (int c = threadIdx.x; c < 2 * g.Cb; c += blockDim.x) atomicAdd(&dx[c], red[2 * g.Cb + c]);
+    }
 }
 
-template <typename T, bool CHAIN>
-__global__ __launch_bounds__(256) void k_in_bwd_apply(rnvp_coupling_args a, rnvp_coupling_args pv, int TP, int seg) {
+template <typename T>
+__global__ __launch_bounds__(256) void k_in_bwd_apply(rnvp_coupling_args a, int TP, int seg) {
     extern __shared__ double dsm[];
     const Geo g = geo(a);
     const Tile t = tile_of(g, TP);
-    const int lane = threadIdx.x & 63;
-    float* tab = (float*)dsm;                            // sc | sf | mean | rstd | coef | k1 | k2 | pm | pr [Cb each]
-    const int tabn = 12 * ((g.Cb + 3) / 4 * 4);
-    double* pred = (double*)(tab + tabn);                // CHAIN: prev's A | B | G [Cb each]
-    T* gh = (T*)(pred + (CHAIN ? 3 * ((g.Cb + 1) / 2 * 2) : 0));
+    float* tab = (float*)dsm;                            // sc | sf | mean | rstd | coef | k1 | k2 [Cb each]
+    const int tabn = 8 * ((g.Cb + 3) / 4 * 4);
+    T* gh = (T*)(tab + tabn);
     const int total = g.Cb * t.tp;
     auto xidx = [&](int e) {
         const int cb = e / t.tp, p = t.p0 + (e - cb * t.tp);
         const int c = (g.kind == 0) ? cb : g.off_base + cb;
         return ((long long)t.b * g.C + c) * g.HW + p;
     };
-    float xp[CP_K], gxp[CP_K], pup[CP_K];
+    float xp[CP_K], gxp[CP_K];
 #pragma unroll
     for (int k = 0; k < CP_K; ++k) {
         const int e = k * 256 + threadIdx.x;
         const long long idx = xidx(e < total ? e : 0);   // unconditional (clamped) loads
         xp[k] = a.x[idx];
         gxp[k] = a.gx[idx];
-        pup[k] = CHAIN ? pv.u[idx] : 0.f;
-    }
-    if (CHAIN) {
-        lds_zero(pred, 3 * g.Cb);
-        const Geo gp = geo(pv);
-        for (int cb = threadIdx.x; cb < g.Cb; cb += blockDim.x)
-            out_bn_stats(pv, gp, cb, tab[7 * g.Cb + cb], tab[8 * g.Cb + cb]);
     }
     in_bn_table(a, g, tab);
     const double cnt = (double)g.B * g.HW;
@@ -957,74 +660,27 @@ __global__ __launch_bounds__(256) void k_in_bwd_apply(rnvp_coupling_args a, rnvp
             if (a.g_in_gamma) a.g_in_gamma[cb] = (float)s2;
         }
     }
-    if (blockIdx.x == 0 && a.gscale_part && threadIdx.x < 64) {
-        // fold the out part's sharded scale / scale_shift partials (wave 0)
-        const int l = threadIdx.x;
-        double v0 = 0.0, v1 = 0.0;
-        if (l < RNVP_COUPLING_SHARDS) {
-            v0 = a.gscale_part[2 * l];
-            v1 = a.gscale_part[2 * l + 1];
-            a.gscale_part[2 * l] = 0.0;
-            a.gscale_part[2 * l + 1] = 0.0;
-        }
-        v0 = wave_sum(v0);
-        v1 = wave_sum(v1);
-        if (l == 0) {
-            *a.g_scale += (float)v0;
-            *a.g_scale_shift += (float)v1;
-        }
-    }
+    if (blockIdx.x == 0 && a.gscale_part && threadIdx.x < 64) fold_gscale(a);   // (no-op after k_in_bwd_red)
     tile_copy_in<T>(a.gh0, t.m0, t.tp, a.cs_gh0, gh);
     __syncthreads();
-    auto body = [&](int e0, float xv, float gxv, float puv) {
-        const int e = e0 + threadIdx.x;
-        const bool ok = e < total;
-        const int cb = ok ? e / t.tp : 0, pl = ok ? e - cb * t.tp : 0, p = t.p0 + pl;
+    auto body = [&](int e, float xv, float gxv) {
+        const int cb = e / t.tp, pl = e - cb * t.tp, p = t.p0 + pl;
         const int c = (g.kind == 0) ? cb : g.off_base + cb;
         const long long idx = ((long long)t.b * g.C + c) * g.HW + p;
-        float gfin = 0.f;
-        bool ptr = false;   // a transformed position of prev (= kept square / conditioning half of a)
-        if (ok) {
-            float gxa, xh;
-            in_bwd_vals<T>(a, g, t, gh, tab, cb, pl, xv, gxa, xh);
-            float gxm = tab[4 * g.Cb + cb] * (gxa - tab[5 * g.Cb + cb] - xh * tab[6 * g.Cb + cb]);
-            const bool kept = g.kind != 0 || ckbd_m(g, p);
-            if (!kept) gxm = 0.f;   // xm = x * mask
-            gfin = gxv + gxm;
-            a.gx[idx] = gfin;
-            ptr = kept;
-        }
-        if (CHAIN) {
-            // prev's k_out_bwd_red over its transformed positions, from the
-            // final gradient of z_prev = x_a (every lane takes part in seg_sum)
-            float vA = 0.f, vB = 0.f, vG = 0.f;
-            if (ptr) {
-                vA = gfin;
-                vB = gfin * (puv - tab[7 * g.Cb + cb]) * tab[8 * g.Cb + cb];
-                vG = pv.gl_sample ? pv.gl_sample[t.b] : 0.f;
-            }
-            const double dA = seg_red((double)vA, seg), dB = seg_red((double)vB, seg), dG = seg_red((double)vG, seg);
-            if (ok && (lane & seg_mask(seg)) == 0) {
-                atomicAdd(&pred[cb], dA);
-                atomicAdd(&pred[g.Cb + cb], dB);
-                atomicAdd(&pred[2 * g.Cb + cb], dG);
-            }
-        }
+        float gxa, xh;
+        in_bwd_vals<T>(a, g, t, gh, tab, cb, pl, xv, gxa, xh);
+        float gxm = tab[4 * g.Cb + cb] * (gxa - tab[5 * g.Cb + cb] - xh * tab[6 * g.Cb + cb]);
+        if (g.kind == 0 && !ckbd_m(g, p)) gxm = 0.f;   // xm = x * mask
+        a.gx[idx] = gxv + gxm;
     };
-    // e0 block-uniform (the CHAIN seg_sum shuffles need every lane)
 #pragma unroll
-    for (int k = 0; k < CP_K; ++k)
-        if (k * 256 < total) body(k * 256, xp[k], gxp[k], pup[k]);
-    for (int e0 = CP_K * 256; e0 < total; e0 += 256) {
-        const int e = e0 + threadIdx.x;
-        const long long idx = xidx(e < total ? e : 0);
-        const float xv = a.x[idx], gxv = a.gx[idx], puv = CHAIN ? pv.u[idx] : 0.f;
-        body(e0, e < total ? xv : 0.f, e < total ? gxv : 0.f, puv);
+    for (int k = 0; k < CP_K; ++k) {
+        const int e = k * 256 + threadIdx.x;
+        if (e < total) body(e, xp[k], gxp[k]);
     }
-    if (CHAIN) {
-        __syncthreads();
-        double* dst = cshard(pv.bwd_sums, 3 * g.Cb);
-        for (int c = threadIdx.x; c < 3 * g.Cb; c += blockDim.x) atomicAdd(&dst[c], pred[c]);
+    for (int e = CP_K * 256 + threadIdx.x; e < total; e += 256) {
+        const long long idx = xidx(e);
+        body(e, a.x[idx], a.gx[idx]);
     }
 }
 
@@ -1062,8 +718,6 @@ inline TileCfg tile_cfg(const rnvp_coupling_args* a) {
     c.grid = a->B * ((HW + c.TP - 1) / c.TP);
     return c;
 }
-inline int r4(int x) { return (x + 3) / 4 * 4; }
-
 }  // namespace
 
 extern "C" int rnvp_coupling_in_fwd(const rnvp_coupling_args* a, void* stream) {
@@ -1087,6 +741,23 @@ extern "C" int rnvp_coupling_in_fwd(const rnvp_coupling_args* a, void* stream) {
     return RNVP_OK;
 }
 
+extern "C" int rnvp_coupling_in_apply(const rnvp_coupling_args* a, void* stream) {
+    int st = check(a);
+    if (st) return st;
+    if (!a->h0 || (a->training && !a->in_sums) || (!a->training && (!a->in_rmean || !a->in_rvar))) return RNVP_E_INVALID;
+    const int Cb = cb_of(a);
+    if (a->cs_h0 < (a->kind == 0 ? 2 * Cb + 1 : 2 * Cb)) return RNVP_E_INVALID;
+    if (a->B == 0) return RNVP_OK;
+    const TileCfg tc = tile_cfg(a);
+    const int esz = a->dtype == RNVP_F32 ? 4 : 2;
+    const size_t shm = 16 * r4(Cb) + (size_t)tc.TP * a->cs_h0 * esz;
+    hipStream_t s = (hipStream_t)stream;
+    if (a->dtype == RNVP_F32) k_in_apply<float><<<tc.grid, 256, shm, s>>>(*a, tc.TP, tc.seg);
+    else k_in_apply<bf16_t><<<tc.grid, 256, shm, s>>>(*a, tc.TP, tc.seg);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
 extern "C" int rnvp_coupling_out_fwd(const rnvp_coupling_args* a, void* stream) {
     int st = check(a);
     if (st) return st;
@@ -1099,7 +770,7 @@ extern "C" int rnvp_coupling_out_fwd(const rnvp_coupling_args* a, void* stream) 
     hipStream_t s = (hipStream_t)stream;
     const TileCfg tc = tile_cfg(a);
     const int esz = a->dtype == RNVP_F32 ? 4 : 2;
-    const size_t shm1 = 32 * ((Cb + 1) / 2 * 2) + (size_t)tc.TP * a->cs_st * esz;
+    const size_t shm1 = 16 * ((Cb + 1) / 2 * 2) + (size_t)tc.TP * a->cs_st * esz;
     if (a->dtype == RNVP_F32) k_out1<float><<<tc.grid, 256, shm1, s>>>(*a, tc.TP, tc.seg);
     else k_out1<bf16_t><<<tc.grid, 256, shm1, s>>>(*a, tc.TP, tc.seg);
     RNVP_LAUNCH_CHECK();
@@ -1143,7 +814,7 @@ extern "C" int rnvp_coupling_out_bwd(const rnvp_coupling_args* a, void* stream) 
     hipStream_t s = (hipStream_t)stream;
     const TileCfg tc = tile_cfg(a);
     const int esz = a->dtype == RNVP_F32 ? 4 : 2;
-    if (stats && !a->bwd_sums_ready) {
+    if (stats) {
         k_out_bwd_red<<<tc.grid, 256, 24 * Cb + 8 * Cb, s>>>(*a, tc.TP, tc.seg);
         RNVP_LAUNCH_CHECK();
     }
@@ -1157,7 +828,9 @@ extern "C" int rnvp_coupling_out_bwd(const rnvp_coupling_args* a, void* stream) 
 extern "C" int rnvp_coupling_in_bwd(const rnvp_coupling_args* a, void* stream) {
     int st = check(a);
     if (st) return st;
-    if (!a->gh0 || !a->gx) return RNVP_E_INVALID;
+    // gx NULL: the reduction pass only (coupling links: the in_bn backward apply
+    // is folded into the previous coupling's rnvp_coupling_link_bwd)
+    if (!a->gh0 || (!a->gx && !(a->in_bwd_ext && a->training))) return RNVP_E_INVALID;
     if (a->training && (!a->in_sums || !a->in_bwd_sums)) return RNVP_E_INVALID;
     if (!a->training && (!a->in_rmean || !a->in_rvar)) return RNVP_E_INVALID;
     const int Cb = cb_of(a);
@@ -1169,75 +842,15 @@ extern "C" int rnvp_coupling_in_bwd(const rnvp_coupling_args* a, void* stream) {
     const size_t gsh = (size_t)tc.TP * a->cs_gh0 * esz;
     if (a->training || a->g_in_gamma || a->g_in_beta) {
         if (!a->in_bwd_sums) return RNVP_E_INVALID;
-        const size_t shm = 16 * Cb + 16 * r4(Cb) + gsh;
+        const size_t shm = (a->in_bwd_ext ? 32 : 16) * Cb + 16 * r4(Cb) + gsh;
         if (a->dtype == RNVP_F32) k_in_bwd_red<float><<<tc.grid, 256, shm, s>>>(*a, tc.TP, tc.seg);
         else k_in_bwd_red<bf16_t><<<tc.grid, 256, shm, s>>>(*a, tc.TP, tc.seg);
         RNVP_LAUNCH_CHECK();
     }
-    const size_t shm = 48 * r4(Cb) + gsh;
-    if (a->dtype == RNVP_F32) k_in_bwd_apply<float, false><<<tc.grid, 256, shm, s>>>(*a, *a, tc.TP, tc.seg);
-    else k_in_bwd_apply<bf16_t, false><<<tc.grid, 256, shm, s>>>(*a, *a, tc.TP, tc.seg);
-    RNVP_LAUNCH_CHECK();
-    return RNVP_OK;
-}
-
-namespace {
-// a and b chain: b consumes a's output (same kind / shape, the opposite mask)
-int chain_check(const rnvp_coupling_args* a, const rnvp_coupling_args* b) {
-    if (check(a) || check(b)) return RNVP_E_INVALID;
-    if (a->kind != b->kind || a->B != b->B || a->C != b->C || a->H != b->H || a->W != b->W || a->dtype != b->dtype)
-        return RNVP_E_INVALID;
-    if ((a->mask_config ? 1 : 0) == (b->mask_config ? 1 : 0)) return RNVP_E_INVALID;
-    if (!a->training || !b->training || !a->coupling_bn) return RNVP_E_INVALID;
-    return RNVP_OK;
-}
-}  // namespace
-
-extern "C" int rnvp_coupling_out_in_fwd(const rnvp_coupling_args* a, const rnvp_coupling_args* nx, void* stream) {
-    if (!a || !nx || chain_check(a, nx)) return RNVP_E_INVALID;
-    if (!a->st || !a->u || !a->z || !a->ldj_sample || !a->scale || !a->scale_shift || !a->out_sums || a->ldj_full)
-        return RNVP_E_INVALID;
-    if (a->kind == 0 && !a->next_sums) return RNVP_E_INVALID;
-    if (!nx->h0 || !nx->in_sums || nx->x != a->z) return RNVP_E_INVALID;
-    const int Cb = cb_of(a);
-    if (a->cs_st < 2 * Cb || nx->cs_h0 < (nx->kind == 0 ? 2 * Cb + 1 : 2 * Cb)) return RNVP_E_INVALID;
-    if (a->B == 0) return RNVP_OK;
-    hipStream_t s = (hipStream_t)stream;
-    const TileCfg tc = tile_cfg(a);
-    const int esz = a->dtype == RNVP_F32 ? 4 : 2;
-    const size_t shm1 = 32 * ((Cb + 1) / 2 * 2) + (size_t)tc.TP * a->cs_st * esz;
-    if (a->dtype == RNVP_F32) k_out1<float><<<tc.grid, 256, shm1, s>>>(*a, tc.TP, tc.seg);
-    else k_out1<bf16_t><<<tc.grid, 256, shm1, s>>>(*a, tc.TP, tc.seg);
-    RNVP_LAUNCH_CHECK();
-    const TileCfg tn = tile_cfg(nx);
-    const int nrun = a->net_running ? a->n_net_running : 0;
-    if (nrun < 0 || (nrun > 0 && a->net_running_cmax <= 0)) return RNVP_E_INVALID;
-    size_t shm = 20 * (size_t)r4(Cb) + (size_t)tn.TP * nx->cs_h0 * esz;
-    if (nrun > 0 && 16 * (size_t)a->net_running_cmax > shm) shm = 16 * (size_t)a->net_running_cmax;
-    if (a->dtype == RNVP_F32) k_out2_in<float><<<tn.grid + nrun, 256, shm, s>>>(*a, *nx, tn.TP, tn.grid);
-    else k_out2_in<bf16_t><<<tn.grid + nrun, 256, shm, s>>>(*a, *nx, tn.TP, tn.grid);
-    RNVP_LAUNCH_CHECK();
-    return RNVP_OK;
-}
-
-extern "C" int rnvp_coupling_in_bwd_chain(const rnvp_coupling_args* a, const rnvp_coupling_args* pv, void* stream) {
-    if (!a || !pv || chain_check(pv, a)) return RNVP_E_INVALID;
-    if (!a->gh0 || !a->gx || !a->in_sums || !a->in_bwd_sums) return RNVP_E_INVALID;
-    if (!pv->u || !pv->out_sums || !pv->bwd_sums || pv->gl_full) return RNVP_E_INVALID;
-    const int Cb = cb_of(a);
-    if (a->cs_gh0 < 2 * Cb) return RNVP_E_INVALID;
-    if (a->B == 0) return RNVP_OK;
-    hipStream_t s = (hipStream_t)stream;
-    const TileCfg tc = tile_cfg(a);
-    const int esz = a->dtype == RNVP_F32 ? 4 : 2;
-    const size_t gsh = (size_t)tc.TP * a->cs_gh0 * esz;
-    const size_t shm0 = 16 * Cb + 16 * r4(Cb) + gsh;
-    if (a->dtype == RNVP_F32) k_in_bwd_red<float><<<tc.grid, 256, shm0, s>>>(*a, tc.TP, tc.seg);
-    else k_in_bwd_red<bf16_t><<<tc.grid, 256, shm0, s>>>(*a, tc.TP, tc.seg);
-    RNVP_LAUNCH_CHECK();
-    const size_t shm = 48 * r4(Cb) + 24 * ((Cb + 1) / 2 * 2) + gsh;
-    if (a->dtype == RNVP_F32) k_in_bwd_apply<float, true><<<tc.grid, 256, shm, s>>>(*a, *pv, tc.TP, tc.seg);
-    else k_in_bwd_apply<bf16_t, true><<<tc.grid, 256, shm, s>>>(*a, *pv, tc.TP, tc.seg);
+    if (!a->gx) return RNVP_OK;
+    const size_t shm = 32 * r4(Cb) + gsh;
+    if (a->dtype == RNVP_F32) k_in_bwd_apply<float><<<tc.grid, 256, shm, s>>>(*a, tc.TP, tc.seg);
+    else k_in_bwd_apply<bf16_t><<<tc.grid, 256, shm, s>>>(*a, tc.TP, tc.seg);
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
 }

@@ -2,9 +2,9 @@
 // BN running stats, fused Adam.  All HBM-bound elementwise / reduction work.
 #include <math.h>
 
-#include "common.h"
+#include "coupling_common.h"
 
-extern "C" int rnvp_version(void) { return 105; }
+extern "C" int rnvp_version(void) { return 106; }
 
 extern "C" int rnvp_struct_size(int which) {
     switch (which) {
@@ -19,6 +19,7 @@ extern "C" int rnvp_struct_size(int which) {
         case 8: return (int)sizeof(rnvp_coupling_args);
         case 9: return (int)sizeof(rnvp_net_step);
         case 10: return (int)sizeof(rnvp_range);
+        case 11: return (int)sizeof(rnvp_link_args);
     }
     return -1;
 }
@@ -214,6 +215,93 @@ extern "C" int rnvp_logit_fwd(const float* x, const float* noise, uint64_t seed,
     return RNVP_OK;
 }
 
+// The training step's input pass: the logit transform over pixel tiles of
+// every sample (all CUs busy: k_logit_fwd has one workgroup per sample), the
+// per-sample log-det added with one atomic per workgroup, and the first
+// coupling's in_bn batch sums (k_in_stats) of the values just computed.
+__global__ __launch_bounds__(256) void k_flow_in(const float* __restrict__ x, uint64_t seed, const long long* epoch,
+                                                 uint64_t epoch_stride, float cst, float* __restrict__ y,
+                                                 float* __restrict__ logdet, rnvp_coupling_args a, int first, int C,
+                                                 int HW, int TP, int seg) {
+    // the noise stream of rnvp_logit_fwd: Philox counter = NCHW index + epoch * B*C*H*W
+    const uint64_t offset = epoch ? (uint64_t)epoch[0] * epoch_stride : 0;
+    extern __shared__ double red[];   // [2*Cb]
+    __shared__ double redl[16];
+    const int tpi = (HW + TP - 1) / TP;
+    const int b = blockIdx.x / tpi, p0 = (blockIdx.x - b * tpi) * TP, tp = min(TP, HW - p0);
+    const int lane = threadIdx.x & 63;
+    Geo g;
+    int Cb = 0;
+    if (first) {
+        g = geo(a);
+        Cb = g.Cb;
+        lds_zero(red, 2 * Cb);
+        __syncthreads();
+    }
+    const float sp_pre = softplusf(-(float)(log((double)cst) - log(1.0 - (double)cst)));
+    const int total = C * tp;
+    double acc = 0.0;
+    for (int e0 = 0; e0 < total; e0 += 256) {   // block-uniform: the segment sums need every lane
+        const int e = e0 + threadIdx.x;
+        const bool ok = e < total;
+        const int c = ok ? e / tp : 0, p = p0 + (ok ? e - c * tp : 0);
+        const long long idx = ((long long)b * C + c) * HW + p;
+        float l = 0.f;
+        if (ok) {
+            const float u = philox_uniform(seed, offset + (uint64_t)idx);
+            float v = (x[idx] * 255.f + u) / 256.f;
+            v = ((v * 2.f - 1.f) * cst + 1.f) / 2.f;
+            l = logf(v) - logf(1.f - v);
+            y[idx] = l;
+            acc += (double)(softplusf(l) + softplusf(-l) - sp_pre);
+        }
+        if (first) {
+            int cb = c;
+            float xm = l;
+            if (g.kind == 0) {
+                if (!ckbd_m(g, p)) xm = 0.f;
+            } else {
+                cb = c - g.off_base;
+                if (cb < 0 || cb >= Cb) xm = 0.f;
+            }
+            const double s1 = seg_red((double)xm, seg), s2 = seg_red((double)xm * xm, seg);
+            if (ok && cb >= 0 && cb < Cb && (lane & seg_mask(seg)) == 0) {
+                atomicAdd(&red[cb], s1);
+                atomicAdd(&red[Cb + cb], s2);
+            }
+        }
+    }
+    acc = block_sum(acc, redl);   // (barriers also publish red)
+    if (threadIdx.x == 0) atomicAdd(&logdet[b], (float)acc);
+    if (first) {
+        double* dst = cshard(a.in_sums, 2 * Cb);
+        for (int c = threadIdx.x; c < 2 * Cb; c += blockDim.x) atomicAdd(&dst[c], red[c]);
+    }
+}
+
+extern "C" int rnvp_flow_in_fwd(const float* x, uint64_t seed, const long long* epoch, float constraint, float* y,
+                                float* logdet, const rnvp_coupling_args* first, int B, int C, int H, int W,
+                                void* stream) {
+    if (!x || !y || !logdet || B < 0 || C <= 0 || H <= 0 || W <= 0) return RNVP_E_INVALID;
+    if (first && (first->x != y || !first->training || !first->in_sums || first->B != B || first->C != C ||
+                  first->H != H || first->W != W || (first->kind == 1 && (C & 1))))
+        return RNVP_E_INVALID;
+    if (B == 0) return RNVP_OK;
+    const int HW = H * W;
+    int TP = HW < 256 ? HW : 256;
+    while (TP > 16 && TP % 2 == 0 && (long long)B * ((HW + TP - 1) / TP) < 1024) TP /= 2;
+    int seg = 1;
+    while (seg < 64 && TP % (2 * seg) == 0 && HW % (2 * seg) == 0) seg *= 2;
+    const int grid = B * ((HW + TP - 1) / TP);
+    const int Cb = first ? (first->kind == 0 ? C : C / 2) : 0;
+    rnvp_coupling_args none{};
+    k_flow_in<<<grid, 256, 16 * (size_t)Cb, (hipStream_t)stream>>>(x, seed, epoch, (uint64_t)B * C * HW, constraint,
+                                                                   y, logdet, first ? *first : none, first ? 1 : 0, C,
+                                                                   HW, TP, seg);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
 __global__ void k_logit_inv(const float* __restrict__ x, float* __restrict__ y, float cst, long long n) {
     for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
         float v = 1.f / (expf(-x[e]) + 1.f);
@@ -348,6 +436,33 @@ extern "C" int rnvp_prior_logprob_bwd(const float* z, const float* gout, float* 
     long long total = (long long)B * n;
     if (total == 0) return RNVP_OK;
     k_prior_bwd<<<rnvp_grid(total, 256), 256, 0, (hipStream_t)stream>>>(z, gout, gz, n, total);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+// end of the training step's forward (flow_realnvp.py:336-338, train.py:192-196):
+// lp = prior + ldj per sample, the step's mean log-likelihood into the device
+// accumulator, and the per-step accumulators left zero for the next step
+__global__ void k_lp_finish(double* prior, float* ldj, float* logdet, int zero_logdet, float* lp, double* ll_acc,
+                            int B) {
+    __shared__ double red[16];
+    double acc = 0.0;
+    for (int b = threadIdx.x; b < B; b += blockDim.x) {
+        const float l = (float)(prior[b] + (double)ldj[b]);
+        lp[b] = l;
+        acc += (double)(l + logdet[b]);
+        prior[b] = 0.0;
+        ldj[b] = 0.f;
+        if (zero_logdet) logdet[b] = 0.f;
+    }
+    acc = block_sum(acc, red);
+    if (threadIdx.x == 0) ll_acc[0] += acc / (double)B;
+}
+
+extern "C" int rnvp_flow_lp_finish(double* prior, float* ldj, float* logdet, int zero_logdet, float* lp,
+                                   double* ll_acc, int B, void* stream) {
+    if (!prior || !ldj || !logdet || !lp || !ll_acc || B <= 0) return RNVP_E_INVALID;
+    k_lp_finish<<<1, 256, 0, (hipStream_t)stream>>>(prior, ldj, logdet, zero_logdet, lp, ll_acc, B);
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
 }

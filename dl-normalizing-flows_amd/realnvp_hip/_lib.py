@@ -8,8 +8,12 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# RNVP_LIB_PATH: a probe build of the same library (tools/, timing experiments)
+# RNVP_LIB_PATH: a probe build of the same library (tools/, timing experiments);
+# announced on stderr, and refused at load when its structs differ (rnvp_struct_size)
 LIB_PATH = os.environ.get("RNVP_LIB_PATH") or os.path.join(_HERE, "librealnvp_hip.so")
+if os.environ.get("RNVP_LIB_PATH"):
+    import sys as _sys
+    print("realnvp_hip: RNVP_LIB_PATH=%s replaces the in-tree library" % LIB_PATH, file=_sys.stderr)
 
 RNVP_F32, RNVP_BF16 = 0, 1
 
@@ -111,7 +115,15 @@ class CouplingArgs(C.Structure):
                 ("gh0", vp), ("cs_gh0", i32),
                 ("in_bwd_sums", vp), ("g_in_gamma", vp), ("g_in_beta", vp),
                 ("net_running", vp), ("n_net_running", i32), ("net_running_cmax", i32),
-                ("gscale_part", vp), ("next_sums", vp), ("bwd_sums_ready", i32)]
+                ("gscale_part", vp),
+                ("nclass", i32), ("cls_sums", vp), ("prior_sums", vp), ("outp_sums", vp), ("in_bwd_ext", vp)]
+
+
+RNVP_LINK_SAME, RNVP_LINK_SQUEEZE, RNVP_LINK_UNFACTOR, RNVP_LINK_FINAL = 0, 1, 2, 3
+
+
+class LinkArgs(C.Structure):
+    _fields_ = [("type", i32), ("g_lp", vp), ("prior", vp), ("off", vp), ("z", vp)]
 
 
 class TensorRef(C.Structure):
@@ -155,8 +167,13 @@ _SIGS = {
     "rnvp_coupling_reverse": (i32, [C.POINTER(CouplingArgs), vp]),
     "rnvp_coupling_out_bwd": (i32, [C.POINTER(CouplingArgs), vp]),
     "rnvp_coupling_in_bwd": (i32, [C.POINTER(CouplingArgs), vp]),
-    "rnvp_coupling_out_in_fwd": (i32, [C.POINTER(CouplingArgs), C.POINTER(CouplingArgs), vp]),
-    "rnvp_coupling_in_bwd_chain": (i32, [C.POINTER(CouplingArgs), C.POINTER(CouplingArgs), vp]),
+    "rnvp_link_nclass": (i32, [i32, i32]),
+    "rnvp_coupling_out_u": (i32, [C.POINTER(CouplingArgs), vp]),
+    "rnvp_coupling_link_fwd": (i32, [C.POINTER(CouplingArgs), C.POINTER(CouplingArgs), C.POINTER(LinkArgs), vp]),
+    "rnvp_coupling_link_bwd": (i32, [C.POINTER(CouplingArgs), C.POINTER(CouplingArgs), C.POINTER(LinkArgs), vp]),
+    "rnvp_coupling_in_apply": (i32, [C.POINTER(CouplingArgs), vp]),
+    "rnvp_flow_in_fwd": (i32, [vp, C.c_uint64, vp, f32, vp, vp, C.POINTER(CouplingArgs), i32, i32, i32, i32, vp]),
+    "rnvp_flow_lp_finish": (i32, [vp, vp, vp, i32, vp, vp, i32, vp]),
     "rnvp_sumsq_multi": (i32, [vp, i32, vp, vp]),
     "rnvp_sumsq_bwd_multi": (i32, [vp, i32, vp, f32, vp]),
     "rnvp_adam_step": (i32, [vp, vp, vp, vp, i64, vp, f32, f32, f32, f32, f32, vp, f32, vp]),
@@ -180,13 +197,14 @@ class _Lib:
             fn.restype = res
             fn.argtypes = args
             raw = name in ("rnvp_version", "rnvp_struct_size", "rnvp_stat_shards", "rnvp_wgrad_slabs", "rnvp_wgrad_replicas",
+                           "rnvp_link_nclass",
                            "rnvp_weight_norm_tiles", "rnvp_weight_norm_opt_blocks",
                            "rnvp_net_group_prepare") or res is not i32
             setattr(self, name[len("rnvp_"):], fn if raw else self._wrap(name, fn))
         # the struct mirrors must match the library's layouts (rnvp_struct_size): a
         # table read at another stride would address arbitrary device memory
         mirrors = (BNSrc, BNRunning, ConvArgs, WgradConv, WgradGroup, BNBwdArgs, WNDesc, AdamArgs, CouplingArgs,
-                   NetStep, Range)
+                   NetStep, Range, LinkArgs)
         for i, m in enumerate(mirrors):
             if self.dll.rnvp_struct_size(i) != C.sizeof(m):
                 raise RuntimeError("%s: struct %s is %d bytes in the library, %d in the binding (stale build?)"

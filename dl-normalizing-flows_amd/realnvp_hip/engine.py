@@ -294,6 +294,8 @@ class CouplingEngine:
             _, _, bname = self._conv_names(spec)
             d.db_off = self.layout[bname][0] if bname else -1
             d.blk0 = blk0
+            # the fused pass's row blocks assume the packed row stride round_up(cin, 8)
+            assert cs_in == round_up(spec.cin, 8), (name, cs_in, spec.cin)
             nb = int(_lib.lib().weight_norm_opt_blocks(spec.cout, spec.cin, spec.ks))
             blk0 = blk0 + nb if (nb > 0 and blk0 >= 0) else -1
             row0 += spec.cout
@@ -325,7 +327,9 @@ class CouplingEngine:
         ar.add("u", B * self.C * H * W * 4)
         ar.add("in_sums", COUPLING_SHARDS * 2 * self.Cb * 8)
         ar.add("out_sums", COUPLING_SHARDS * 2 * self.Cb * 8)
-        ar.add("next_sums", COUPLING_SHARDS * 2 * self.Cb * 8)   # chained couplings (rnvp_coupling_out_in_fwd)
+        # coupling links (rnvp_coupling_out_u / _link_fwd): u's sums per pixel class, the prior's sums
+        ar.add("cls_sums", COUPLING_SHARDS * 4 * 2 * self.C * 8)
+        ar.add("prior_sums", COUPLING_SHARDS * 4 * 2 * self.C * 8)
         sh = stat_shards(M)
         for bn, spec in self.P.bns.items():
             ar.add("s:" + bn, sh * 2 * spec.c * 8)
@@ -399,6 +403,9 @@ class CouplingEngine:
         # zeroed every backward: the reductions (kept contiguous)
         wsz = self.weights(dtype)
         ar.add("bwd_sums", COUPLING_SHARDS * 3 * self.Cb * 8)
+        # coupling links (rnvp_coupling_link_bwd): direct input-gradient sums, in_bn kept-position sums
+        ar.add("outp_sums", COUPLING_SHARDS * 2 * 2 * self.C * 8)
+        ar.add("in_bwd_ext", COUPLING_SHARDS * 2 * self.Cb * 8)
         ar.add("in_bwd_sums", COUPLING_SHARDS * 2 * self.Cb * 8)
         ar.add("gscale_part", COUPLING_SHARDS * 2 * 8)   # left zero by coupling_in_bwd
         first, last = "bwd_sums", "in_bwd_sums"
@@ -545,23 +552,19 @@ class CouplingEngine:
 
     # ---------------------------------------------------------------- forward
     def chains_into(self, nxt):
-        """True when coupling `nxt` can consume this coupling's output through
-        the chained kernels (rnvp_coupling_out_in_fwd / _in_bwd_chain): same
-        kind, the opposite mask, out_bn with batch statistics."""
+        """True when coupling `nxt` directly consumes this coupling's output
+        as the next coupling of the same combo (a RNVP_LINK_SAME link): same
+        kind and shape, the opposite mask, out_bn with batch statistics."""
         return (nxt.kind == self.kind and nxt.C == self.C and nxt.cfg != self.cfg and
                 bool(self.hp.coupling_bn))
 
     def forward(self, x, training, dtype, full_ldj, saved=None, prepare=True, ldj_sample=None, z_out=None,
-                zero_sums=True, chain_next=None, in_done=False):
+                zero_sums=True):
         """x: [B,C,H,W] fp32 device tensor.  Returns (z, ldj, saved) where ldj
         is the elementwise log_diag_J [B,C,H,W] (full_ldj) or this coupling's
         per-sample sum [B] (accumulated into ldj_sample when given).
         zero_sums=False: the batch-statistic sums of `saved` are already zero
-        (the previous step's backward left them so: backward(zero_at_end=True)).
-        chain_next = (engine, saved arena) of the coupling that consumes z
-        (chains_into): its in part (h0, in_bn sums and running stats) is
-        produced by this coupling's out launch; that coupling's forward then
-        runs with in_done=True."""
+        (the previous step's backward left them so: backward(zero_at_end=True))."""
         L = _lib.lib()
         B, Cc, H, W = x.shape
         assert Cc == self.C, "channel mismatch"
@@ -575,11 +578,6 @@ class CouplingEngine:
         if ldj_sample is None:
             ldj_sample = torch.zeros(B, device=dev, dtype=torch.float32)
         ldj_full = torch.empty_like(x) if full_ldj else None
-        if in_done and zero_sums:
-            # the previous coupling's chained out launch already wrote this
-            # coupling's in_sums (closed form, shard 0); zeroing them here
-            # would silently corrupt the in_bn backward
-            raise ValueError("forward(in_done=True) requires zero_sums=False")
         if training and zero_sums:
             s0, e0 = ar.range_bytes("in_sums", list(ar.slots)[-1])
             ar.buf[s0:e0].zero_()
@@ -588,10 +586,9 @@ class CouplingEngine:
         a.h0 = ar.ptr("h0")
         n_el, esz = x.numel(), DTYPES[dtype][1]
         cs_h0, cs_st = chan_stride(self.P.buf_ch["h0"]), chan_stride(self.P.buf_ch["st"])
-        if not in_done:
-            # algorithmic bytes: x read by the stats and the apply pass, h0 written
-            _launch("coupling", (8 if training else 4) * n_el + esz * B * H * W * cs_h0, 0.0, L.coupling_in_fwd,
-                    C.byref(a), s)
+        # algorithmic bytes: x read by the stats and the apply pass, h0 written
+        _launch("coupling", (8 if training else 4) * n_el + esz * B * H * W * cs_h0, 0.0, L.coupling_in_fwd,
+                C.byref(a), s)
         self._net_forward(T, sv, ws, training, s)
         if training and "bn_table" in sv:
             # the net BNs' running-stat updates ride on the out launch
@@ -602,17 +599,7 @@ class CouplingEngine:
         a.out_sums = ar.ptr("out_sums")
         a.ldj_sample = ldj_sample.data_ptr()
         a.ldj_full = ldj_full.data_ptr() if full_ldj else None
-        if chain_next is not None:
-            neng, nsv = chain_next
-            nx = neng._coupling_args(neng._tensors(), z, B, H, W, dtype, training)
-            nx.in_sums = nsv["arena"].ptr("in_sums")
-            nx.h0 = nsv["arena"].ptr("h0")
-            a.next_sums = ar.ptr("next_sums")
-            # x, u (w + r), z; st read; the next coupling's h0 written
-            _launch("coupling", 16 * n_el + esz * B * H * W * (cs_st + cs_h0), 0.0, L.coupling_out_in_fwd,
-                    C.byref(a), C.byref(nx), s)
-        else:
-            _launch("coupling", 16 * n_el + esz * B * H * W * cs_st, 0.0, L.coupling_out_fwd, C.byref(a), s)
+        _launch("coupling", 16 * n_el + esz * B * H * W * cs_st, 0.0, L.coupling_out_fwd, C.byref(a), s)
         sv["x"] = x
         return z, (ldj_full if full_ldj else ldj_sample), sv
 
@@ -646,6 +633,104 @@ class CouplingEngine:
         a.ldj_full = ldj.data_ptr() if want_ldj else None
         L.coupling_reverse(C.byref(a), s)
         return out, ldj
+
+
+    def _net_backward(self, sv, sc, ws, T, training, gp, s):
+        """The net's data-gradient chain: conv data gradients and BatchNorm
+        backward applies (single or grouped launches) from d st to d h0."""
+        L = _lib.lib()
+        x = sv["x"]
+        dt = DTYPES[sv["dtype"]][0]
+        # the net's data-gradient chain and grouped weight gradients: argument
+        # structs cached per (saved arena, scratch, weight set); only the
+        # BatchNorm-affine gradient pointers follow this call's grad block
+        key = (ws["key"], id(sc), bool(training))
+        plan = sv.get("bwd_plan")
+        if plan is None or plan[0] != key:
+            plan = (key, self._bwd_args(T, sv, sc, ws, training))
+            sv["bwd_plan"] = plan
+        items, groups, wg_bytes, wg_flops = plan[1]
+        if len(plan) < 3:
+            steps, rw = [], []
+            bsteps = [st for st in self.steps if st.kind != "wgrad"]
+            for (kind, c, nb, fl, bn), bst in zip(items, bsteps):
+                st = NetStep()
+                st.dgamma_off = st.dbeta_off = -1
+                op = bst.op
+                dst = bst.tmp if (kind == "dgrad" and bst.tmp) else bst.gx
+                reads = ({bst.residual} if bst.residual else set()) | ({dst} if bst.accumulate else set())
+                if kind == "dgrad":
+                    st.kind = RNVP_STEP_CONV
+                    st.conv = c
+                    reads |= {bst.gy} | ({op.x} if op.pro_bn else set())
+                    writes = {dst} | ({"e:" + op.pro_bn} if op.pro_bn else set())
+                else:
+                    st.kind = RNVP_STEP_BN_BWD
+                    st.bn = c
+                    st.dgamma_off = self.layout[bn + "weight"][0]
+                    st.dbeta_off = self.layout[bn + "bias"][0]
+                    reads |= {bst.tmp, op.x, "e:" + bn}
+                    writes = {dst}
+                steps.append(st)
+                rw.append((reads, writes))
+            plan = plan + (plan_launches(steps, x.device, rw),)
+            sv["bwd_plan"] = plan
+        for g in plan[2]:
+            if g[0] == "single":
+                kind, c, nb, fl, bn = items[g[1]]
+                if kind == "dgrad":
+                    _launch("conv_dgrad", nb, fl, L.conv2d, C.byref(c), s)
+                else:
+                    c.dgamma, c.dbeta = gp(bn + "weight"), gp(bn + "bias")
+                    _launch("bn_bwd", nb, 0.0, L.bn_bwd_apply, C.byref(c), s)
+            else:
+                _, i0, i1, klass, grid, lds, tab = g
+                nb = sum(items[i][2] for i in range(i0, i1))
+                fl = sum(items[i][3] for i in range(i0, i1))
+                _launch("conv_dgrad", nb, fl, L.net_group, C.addressof(tab), i1 - i0, dt, klass, grid, lds, s)
+
+    def _weight_grads(self, sv, sc, ws, zero_at_end, opt, after, gbase):
+        """The closure issuing the net's grouped weight gradients (+ the
+        weight-norm backward or the fused parameter pass, see backward)."""
+        L = _lib.lib()
+        ar, sar = sv["arena"], sc["arena"]
+        z0, z1 = sc["zero"]
+        dt = DTYPES[sv["dtype"]][0]
+        items, groups, wg_bytes, wg_flops = sv["bwd_plan"][1]
+
+        # the weight gradients (grouped wgrad + weight-norm backward)
+        # only feed the optimizer: on a side stream they overlap the backward
+        # of the couplings before this one.  They read this coupling's saved
+        # activations and gradient scratch, which nothing later in the step
+        # rewrites; `after` runs behind them on the same stream (per-coupling
+        # optimizer update).
+        def weight_grads():
+            ss = stream_ptr()
+            for grp in groups:
+                _launch("conv_wgrad", wg_bytes / len(groups), wg_flops / len(groups), L.conv2d_wgrad_grouped,
+                        C.byref(grp), ss)
+            # the backward reductions live in the scratch shared by every
+            # caller of this shape (trainer and drop-in autograd alike): it is
+            # ALWAYS left zero, so whichever path runs next finds it clean
+            # (the drop-in also zeroes it on entry).  The forward's batch sums
+            # belong to the saved arena: left zero only for the trainer's
+            # persistent arenas (zero_at_end).
+            if zero_at_end:
+                f0, f1 = ar.range_bytes("in_sums", list(ar.slots)[-1])
+                zr = (ar.base + f0, f1 - f0, sar.base + z0, z1 - z0)
+            else:
+                zr = (None, 0, sar.base + z0, z1 - z0)
+            if isinstance(opt, str):
+                pass    # "defer": the caller's model-wide parameter pass reads the slabs
+            elif opt is not None:
+                L.weight_norm_bwd_adam(sc["wn_table"].data_ptr(), sc["n_wn"], sc["wn_blocks"], 1, dt, C.byref(opt),
+                                       *zr, ss)
+            else:
+                L.weight_norm_bwd(sc["wn_table"].data_ptr(), sc["n_wn"], sc["wn_rows"], gbase, *zr, ss)
+            if after is not None:
+                after()
+
+        return weight_grads
 
     # --------------------------------------------------------------- backward
     def _bwd_args(self, T, sv, sc, ws, training):
@@ -720,14 +805,9 @@ class CouplingEngine:
         return items, groups, wg_bytes, wg_flops
 
     def backward(self, sv, gz, gl_full, gl_sample, grad_block, gx=None, side=None, after=None, zero_at_end=False,
-                 defer=None, chain_prev=None, sums_ready=False, opt=None):
+                 defer=None, opt=None):
         """Returns dL/dx; parameter gradients are written into grad_block
         (flat fp32, zeroed by the caller; scale/shift grads accumulate).
-
-        chain_prev = (engine, saved arena) of the coupling whose output this
-        one consumed (its chains_into): this coupling's in backward also
-        reduces that coupling's out_bn backward sums (rnvp_coupling_in_bwd_chain),
-        and that coupling's backward then runs with sums_ready=True.
 
         The data-gradient chain (dgrad -> BN apply per conv) runs first; the
         weight gradients of all the net's convs only need their (complete,
@@ -753,13 +833,11 @@ class CouplingEngine:
         L = _lib.lib()
         x = sv["x"]
         B, H, W, dtype, training = sv["B"], sv["H"], sv["W"], sv["dtype"], sv["training"]
-        M = B * H * W
-        dt = DTYPES[dtype][0]
         s = stream_ptr()
         T = self._tensors()
         ws = self.weights(dtype)
         sc = self.scratch_checked(B, H, W, dtype, x.device)
-        ar, sar, war = sv["arena"], sc["arena"], ws["arena"]
+        ar, sar = sv["arena"], sc["arena"]
         z0, z1 = sc["zero"]
         if not zero_at_end:
             sar.buf[z0:z1].zero_()
@@ -783,113 +861,27 @@ class CouplingEngine:
         a.bwd_sums = sar.ptr("bwd_sums")
         a.g_scale, a.g_scale_shift = gp("scale"), gp("scale_shift")
         a.gscale_part = sar.ptr("gscale_part")
-        a.bwd_sums_ready = int(bool(sums_ready))
         n_el, esz = x.numel(), DTYPES[dtype][1]
         cs_st = chan_stride(self.P.buf_ch["st"])
         # (reduction: gz, u) + apply: gz, u, x read, gx written; st read, gst written
-        _launch("coupling", (0 if sums_ready else 8 * n_el) + 16 * n_el + esz * B * H * W * 2 * cs_st, 0.0,
-                L.coupling_out_bwd, C.byref(a), s)
+        _launch("coupling", 24 * n_el + esz * B * H * W * 2 * cs_st, 0.0, L.coupling_out_bwd, C.byref(a), s)
 
-        # the net's data-gradient chain and grouped weight gradients: argument
-        # structs cached per (saved arena, scratch, weight set); only the
-        # BatchNorm-affine gradient pointers follow this call's grad block
-        key = (ws["key"], id(sc), bool(training))
-        plan = sv.get("bwd_plan")
-        if plan is None or plan[0] != key:
-            plan = (key, self._bwd_args(T, sv, sc, ws, training))
-            sv["bwd_plan"] = plan
-        items, groups, wg_bytes, wg_flops = plan[1]
-        if len(plan) < 3:
-            steps, rw = [], []
-            bsteps = [st for st in self.steps if st.kind != "wgrad"]
-            for (kind, c, nb, fl, bn), bst in zip(items, bsteps):
-                st = NetStep()
-                st.dgamma_off = st.dbeta_off = -1
-                op = bst.op
-                dst = bst.tmp if (kind == "dgrad" and bst.tmp) else bst.gx
-                reads = ({bst.residual} if bst.residual else set()) | ({dst} if bst.accumulate else set())
-                if kind == "dgrad":
-                    st.kind = RNVP_STEP_CONV
-                    st.conv = c
-                    reads |= {bst.gy} | ({op.x} if op.pro_bn else set())
-                    writes = {dst} | ({"e:" + op.pro_bn} if op.pro_bn else set())
-                else:
-                    st.kind = RNVP_STEP_BN_BWD
-                    st.bn = c
-                    st.dgamma_off = self.layout[bn + "weight"][0]
-                    st.dbeta_off = self.layout[bn + "bias"][0]
-                    reads |= {bst.tmp, op.x, "e:" + bn}
-                    writes = {dst}
-                steps.append(st)
-                rw.append((reads, writes))
-            plan = plan + (plan_launches(steps, x.device, rw),)
-            sv["bwd_plan"] = plan
-        for g in plan[2]:
-            if g[0] == "single":
-                kind, c, nb, fl, bn = items[g[1]]
-                if kind == "dgrad":
-                    _launch("conv_dgrad", nb, fl, L.conv2d, C.byref(c), s)
-                else:
-                    c.dgamma, c.dbeta = gp(bn + "weight"), gp(bn + "bias")
-                    _launch("bn_bwd", nb, 0.0, L.bn_bwd_apply, C.byref(c), s)
-            else:
-                _, i0, i1, klass, grid, lds, tab = g
-                nb = sum(items[i][2] for i in range(i0, i1))
-                fl = sum(items[i][3] for i in range(i0, i1))
-                _launch("conv_dgrad", nb, fl, L.net_group, C.addressof(tab), i1 - i0, dt, klass, grid, lds, s)
+        self._net_backward(sv, sc, ws, T, training, gp, s)
         # in_bn backward closes the critical path (dL/dx of the coupling) ...
         a.gh0, a.cs_gh0 = sar.ptr("g:h0"), chan_stride(self.P.buf_ch["h0"])
         a.in_bwd_sums = sar.ptr("in_bwd_sums")
         a.g_in_gamma, a.g_in_beta = gp("in_bn.weight"), gp("in_bn.bias")
-        if chain_prev is not None:
-            peng, psv = chain_prev
-            pv = peng._coupling_args(peng._tensors(), psv["x"], B, H, W, dtype, training)
-            pv.u, pv.out_sums = psv["arena"].ptr("u"), psv["arena"].ptr("out_sums")
-            # the previous coupling's backward resolves its scratch the same
-            # way (scratch_checked), so these sums land where it reads them
-            pv.bwd_sums = peng.scratch_checked(B, H, W, dtype, x.device)["arena"].ptr("bwd_sums")
-            pv.gl_sample = gl_sample.data_ptr() if gl_sample is not None else None
-            # reduction: x, gh0; apply: x, gx (r + w), gh0, and the previous coupling's u
-            _launch("coupling", 20 * n_el + 2 * esz * B * H * W * a.cs_gh0, 0.0, L.coupling_in_bwd_chain,
-                    C.byref(a), C.byref(pv), s)
-        else:
-            _launch("coupling", 16 * n_el + 2 * esz * B * H * W * a.cs_gh0, 0.0, L.coupling_in_bwd, C.byref(a), s)
+        _launch("coupling", 16 * n_el + 2 * esz * B * H * W * a.cs_gh0, 0.0, L.coupling_in_bwd, C.byref(a), s)
 
-        # ... while the weight gradients (grouped wgrad + weight-norm backward)
-        # only feed the optimizer: on a side stream they overlap the backward
-        # of the couplings before this one.  They read this coupling's saved
-        # activations and gradient scratch, which nothing later in the step
-        # rewrites; `after` runs behind them on the same stream (per-coupling
-        # optimizer update).
-        def weight_grads():
-            ss = stream_ptr()
-            for grp in groups:
-                _launch("conv_wgrad", wg_bytes / len(groups), wg_flops / len(groups), L.conv2d_wgrad_grouped,
-                        C.byref(grp), ss)
-            # the backward reductions live in the scratch shared by every
-            # caller of this shape (trainer and drop-in autograd alike): it is
-            # ALWAYS left zero, so whichever path runs next finds it clean
-            # (the drop-in also zeroes it on entry).  The forward's batch sums
-            # belong to the saved arena: left zero only for the trainer's
-            # persistent arenas (zero_at_end).
-            if zero_at_end:
-                f0, f1 = ar.range_bytes("in_sums", list(ar.slots)[-1])
-                zr = (ar.base + f0, f1 - f0, sar.base + z0, z1 - z0)
-            else:
-                zr = (None, 0, sar.base + z0, z1 - z0)
-            if isinstance(opt, str):
-                pass    # "defer": the caller's model-wide parameter pass reads the slabs
-            elif opt is not None:
-                L.weight_norm_bwd_adam(sc["wn_table"].data_ptr(), sc["n_wn"], sc["wn_blocks"], 1, dt, C.byref(opt),
-                                       *zr, ss)
-            else:
-                L.weight_norm_bwd(sc["wn_table"].data_ptr(), sc["n_wn"], sc["wn_rows"], gbase, *zr, ss)
-            if after is not None:
-                after()
+        # ... while the weight gradients only feed the optimizer
+        self._issue_weight_grads(self._weight_grads(sv, sc, ws, zero_at_end, opt, after, gbase), defer, side)
+        return gx
 
+    @staticmethod
+    def _issue_weight_grads(weight_grads, defer, side):
         if defer is not None:
-            # the caller issues the weight gradients later (e.g. several
-            # couplings' at once on a side stream: fewer fork edges)
+            # the caller issues the weight gradients later (e.g. after the
+            # previous coupling's link backward has read this one's sums)
             defer.append(weight_grads)
         elif side is None:
             weight_grads()
@@ -899,4 +891,107 @@ class CouplingEngine:
             side.wait_event(ev)
             with torch.cuda.stream(side):
                 weight_grads()
-        return gx
+
+    # ------------------------------------------------------------ coupling links
+    def link_args(self, sv, x, grad_block=None, gx=None):
+        """CouplingArgs of this coupling for the link kernels (rnvp_coupling_out_u,
+        rnvp_coupling_link_fwd / _bwd) over the saved arena sv (the trainer's,
+        persistent) and this shape's scratch: forward sums, backward sums and,
+        with grad_block / gx, the gradient outputs."""
+        B, H, W, dtype = sv["B"], sv["H"], sv["W"], sv["dtype"]
+        T = self._tensors()
+        ar = sv["arena"]
+        sar = self.scratch_checked(B, H, W, dtype, x.device)["arena"]
+        a = self._coupling_args(T, x, B, H, W, dtype, True)
+        a.in_sums, a.h0, a.st = ar.ptr("in_sums"), ar.ptr("h0"), ar.ptr("st")
+        a.cls_sums, a.prior_sums = ar.ptr("cls_sums"), ar.ptr("prior_sums")
+        a.gst, a.cs_gst = sar.ptr("g:st"), chan_stride(self.P.buf_ch["st"])
+        a.gh0, a.cs_gh0 = sar.ptr("g:h0"), chan_stride(self.P.buf_ch["h0"])
+        a.in_bwd_sums, a.in_bwd_ext = sar.ptr("in_bwd_sums"), sar.ptr("in_bwd_ext")
+        a.outp_sums, a.gscale_part = sar.ptr("outp_sums"), sar.ptr("gscale_part")
+        if grad_block is not None:
+            gb = grad_block.data_ptr()
+            gp = lambda n: gb + 4 * self.layout[n][0]  # noqa: E731
+            a.g_scale, a.g_scale_shift = gp("scale"), gp("scale_shift")
+            a.g_in_gamma, a.g_in_beta = gp("in_bn.weight"), gp("in_bn.bias")
+        if gx is not None:
+            a.gx = gx.data_ptr()
+        return a
+
+    def forward_link(self, x, sv, ldj_sample, link):
+        """Training forward of this coupling inside the trainer's flow program:
+        the s/t net (its input h0 and in_bn statistics were produced by the
+        previous link, or rnvp_flow_in_fwd + rnvp_coupling_in_apply for the
+        first coupling), then u's class sums and the link to the consumer
+        (rnvp_coupling_link_fwd: z at the consumer's permuted address, its in_bn
+        statistics / h0, the prior).  link: dict(type, args=LinkArgs, nxt=(engine,
+        saved arena, input tensor) or None)."""
+        L = _lib.lib()
+        s = stream_ptr()
+        dtype = sv["dtype"]
+        ws = self.weights(dtype)
+        T = self._tensors()
+        B, H, W = sv["B"], sv["H"], sv["W"]
+        self._net_forward(T, sv, ws, True, s)
+        a = self.link_args(sv, x)
+        a.nclass = link["nclass"]
+        a.ldj_sample = ldj_sample.data_ptr()
+        a.gl_sample = link["args"].g_lp
+        if "bn_table" in sv:   # the net BNs' running-stat updates ride on the link launch
+            a.net_running, a.n_net_running, a.net_running_cmax = sv["bn_table"].data_ptr(), sv["bn_n"], sv["bn_cmax"]
+        n_el, esz = x.numel(), DTYPES[dtype][1]
+        cs_st = chan_stride(self.P.buf_ch["st"])
+        # x and st read (u's class sums)
+        _launch("coupling", 4 * n_el + esz * B * H * W * cs_st, 0.0, L.coupling_out_u, C.byref(a), s)
+        nb = 8 * n_el + esz * B * H * W * cs_st        # x, st read; z written
+        if link["nxt"] is not None:
+            neng, nsv, nx = link["nxt"]
+            n = neng.link_args(nsv, nx)
+            nb += esz * nsv["B"] * nsv["H"] * nsv["W"] * chan_stride(neng.P.buf_ch["h0"])   # n's h0 written
+            _launch("coupling", nb, 0.0, L.coupling_link_fwd, C.byref(a), C.byref(n), C.byref(link["args"]), s)
+        else:
+            _launch("coupling", nb, 0.0, L.coupling_link_fwd, C.byref(a), None, C.byref(link["args"]), s)
+        sv["x"] = x
+
+    def backward_link(self, sv, link, grad_block, gx, gl_sample, first, defer, opt=None, after=None):
+        """Training backward of this coupling inside the trainer's flow program
+        (after the consumer's): the link backward (dL/dz from the consumer's
+        direct gradient + its in_bn backward, or the prior; then this coupling's
+        out part, rnvp_coupling_link_bwd), the net's data-gradient chain and the
+        in part's reduction pass (+ its apply pass for the first coupling:
+        dL/dx of the flow input).  gx receives this coupling's direct input
+        gradient (the full dL/dx for the first).  The weight-gradient closure
+        goes to `defer`: the caller runs it once the previous link's backward
+        has read this coupling's sums (the weight-norm backward zeroes them)."""
+        L = _lib.lib()
+        x = sv["x"]
+        B, H, W, dtype = sv["B"], sv["H"], sv["W"], sv["dtype"]
+        s = stream_ptr()
+        T = self._tensors()
+        ws = self.weights(dtype)
+        sc = self.scratch_checked(B, H, W, dtype, x.device)
+        gbase = grad_block.data_ptr()
+
+        def gp(name):
+            return gbase + 4 * self.layout[name][0]
+
+        a = self.link_args(sv, x, grad_block, gx)
+        a.nclass = link["nclass"]
+        a.gl_sample = gl_sample.data_ptr()
+        n_el, esz = x.numel(), DTYPES[dtype][1]
+        cs_st = chan_stride(self.P.buf_ch["st"])
+        nb = 12 * n_el + 2 * esz * B * H * W * cs_st   # x, consumer's gx read, gx written; st read, gst written
+        if link["nxt"] is not None:
+            neng, nsv, nx, ngx, nblock = link["nxt"]
+            n = neng.link_args(nsv, nx, nblock, ngx)
+            nb += esz * nsv["B"] * nsv["H"] * nsv["W"] * chan_stride(neng.P.buf_ch["h0"])   # consumer's gh0 read
+            _launch("coupling", nb, 0.0, L.coupling_link_bwd, C.byref(a), C.byref(n), C.byref(link["args"]), s)
+        else:
+            _launch("coupling", nb, 0.0, L.coupling_link_bwd, C.byref(a), None, C.byref(link["args"]), s)
+        self._net_backward(sv, sc, ws, T, True, gp, s)
+        if not first:
+            a.gx = None     # the reduction pass only; the apply is part of the previous link's backward
+        cs_h0 = chan_stride(self.P.buf_ch["h0"])
+        _launch("coupling", (8 if first else 4) * n_el + (2 if first else 1) * esz * B * H * W * cs_h0, 0.0,
+                L.coupling_in_bwd, C.byref(a), s)
+        self._issue_weight_grads(self._weight_grads(sv, sc, ws, True, opt, after, gbase), defer, None)

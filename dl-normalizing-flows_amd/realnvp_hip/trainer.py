@@ -21,19 +21,15 @@ MI355X-specific structure:
   * optimizer state converts to / from torch.optim.Adam.state_dict() format
     (train.py:139-154, 249-250 checkpoints).
 """
+import ctypes as C
 import gc
 import math
-import os
 
 import numpy as np
 import torch
 
 from . import _lib
-from .engine import stream_ptr
-
-# chained consecutive couplings (rnvp_coupling_out_in_fwd / _in_bwd_chain):
-# RNVP_CHAIN_COUPLING=0 launches every coupling's in and out parts on their own
-CHAIN_COUPLING = int(os.environ.get("RNVP_CHAIN_COUPLING", "1"))
+from .engine import _launch, stream_ptr
 
 
 def wn_table(engines, dtype, dev):
@@ -102,7 +98,7 @@ def bucket_plan(model, bucket_elems, n_total):
 class FlowTrainer:
     def __init__(self, model, batch_size, lr=5e-4, weight_decay=5e-5, betas=(0.9, 0.999), eps=1e-8,
                  scale_reg=5e-5, dtype="bf16", seed=0, process_group=None, bucket_mb=25, overlap=False,
-                 comm="overlap", reduce_dtype="fp32", param_pass="fused"):
+                 comm="overlap", reduce_dtype="fp32", param_pass=None, chain=True):
         self.model = model
         self.dev = next(model.parameters()).device
         if self.dev.type != "cuda":
@@ -119,7 +115,7 @@ class FlowTrainer:
         model.set_precision(dtype)
         model.train()
         self._build_arenas()
-        self._build_plan()
+        self._build_plan(chain)
         self.graph = None
         self.graph_opt = None
         self.graph_input = None
@@ -141,15 +137,11 @@ class FlowTrainer:
         # critical path (the forward/data-gradient chain)
         self.overlap = overlap
         self.side = torch.cuda.Stream(device=self.dev) if overlap else None
-        # side_group > 0 (single process, overlap): the weight gradients of
-        # side_group consecutive couplings are forked onto the side stream
-        # together -- one fork edge per group instead of one per coupling
-        # (each cross-stream edge of a replayed HIP graph costs a barrier
-        # packet between hardware queues)
-        self.side_group = int(os.environ.get("RNVP_SIDE_GROUP", "0")) if (overlap and process_group is None) else 0
-        if param_pass not in ("fused", "separate"):
-            raise ValueError("param_pass must be 'fused' or 'separate'")
-        self._build_param_pass(param_pass)
+        if param_pass not in (None, "fused", "separate"):
+            raise ValueError("param_pass must be None (fused when possible), 'fused' or 'separate'")
+        self._build_param_pass("separate" if param_pass == "separate" else "fused")
+        if param_pass == "fused" and not self.fused:
+            raise ValueError("param_pass='fused' is not possible for this model: %s" % self.param_pass_reason)
         self._build_adam_ranges()
         self._build_buckets()
         self._cap_pg = self._capture_group()
@@ -182,15 +174,16 @@ class FlowTrainer:
         self.n_trainable = int((mask > 0).sum())
 
     # ------------------------------------------------------------------- plan
-    def _build_plan(self):
+    def _build_plan(self, chain=True):
         m = self.model
         B, C, S = self.B, m.channels, m.image_size
         dev = self.dev
         f32 = dict(device=dev, dtype=torch.float32)
         self.pix = torch.zeros(B, C, S, S, **f32)
         self.xl = torch.empty(B, C, S, S, **f32)
-        self.logdet = torch.empty(B, **f32)
+        self.logdet = torch.zeros(B, **f32)
         self.ldj = torch.zeros(B, **f32)
+        self.prior = torch.zeros(B, dtype=torch.float64, device=dev)
         self.lp = torch.empty(B, **f32)
         self.g_lp = torch.full((B,), -1.0 / B, **f32)
         self.ll_acc = torch.zeros(1, dtype=torch.float64, device=dev)
@@ -222,19 +215,61 @@ class FlowTrainer:
             self.stages.append(("restore", cur, off, full))
             cur = full
         self.z = cur
-        # chained couplings: chain[i] = the coupling stage that consumes stage
-        # i's output directly (engine.chains_into), else None
-        self.chain = {}
-        for i, st in enumerate(self.stages):
-            if st[0] != "coupling":
-                continue
-            nx = self.stages[i + 1] if i + 1 < len(self.stages) else None
-            ok = (CHAIN_COUPLING and nx is not None and nx[0] == "coupling" and nx[3] is st[4] and
-                  st[2].chains_into(nx[2]))
-            self.chain[i] = nx if ok else None
         # backward buffers: a gradient buffer per forward tensor
         self.gbuf = {}
+        self._build_links(chain)
         self._build_wn_table()
+
+    def _build_links(self, chain):
+        """The flow program as coupling links (rnvp_coupling_link_fwd / _bwd,
+        include/realnvp_hip.h): what sits between coupling k and the next one
+        in the stage list -- nothing (the next coupling of the same combo),
+        a squeeze, undo_squeeze + factor_out (the next scale), or the end of
+        the flow (restores only).  The permutations then live in the links'
+        addressing and the next coupling's in part in the previous coupling's
+        link launch.  chain=False (or a model whose couplings do not link,
+        e.g. without out_bn) keeps every coupling's in / out parts, the
+        permutation kernels and the prior as separate launches."""
+        from ._lib import LinkArgs, RNVP_LINK_FINAL, RNVP_LINK_SAME, RNVP_LINK_SQUEEZE, RNVP_LINK_UNFACTOR
+        self.cidx = [i for i, st in enumerate(self.stages) if st[0] == "coupling"]
+        self.links = None
+        if not chain:
+            return
+        types = []
+        for k, i in enumerate(self.cidx):
+            j = self.cidx[k + 1] if k + 1 < len(self.cidx) else len(self.stages)
+            between = [self.stages[m][0] for m in range(i + 1, j)]
+            a = self.stages[i][2]
+            if not a.hp.coupling_bn:
+                return
+            if k + 1 == len(self.cidx):
+                if any(b != "restore" for b in between):
+                    return
+                types.append(RNVP_LINK_FINAL)
+                continue
+            n = self.stages[j][2]
+            if between == [] and a.chains_into(n):
+                types.append(RNVP_LINK_SAME)
+            elif between == ["squeeze"] and a.kind == 0 and n.kind == 1:
+                types.append(RNVP_LINK_SQUEEZE)
+            elif between == ["undo", "factor_out"] and a.kind == 1 and n.kind == 0:
+                types.append(RNVP_LINK_UNFACTOR)
+            else:
+                return
+        self.links = types
+        self.link_fwd, self.link_bwd = [], []
+        for k, (i, lt) in enumerate(zip(self.cidx, types)):
+            _, mod, eng, x, z, sv, block = self.stages[i]
+            la = LinkArgs(lt, self.g_lp.data_ptr(), self.prior.data_ptr(), None, None)
+            nc = int(_lib.lib().link_nclass(lt, eng.kind))
+            if lt == RNVP_LINK_FINAL:
+                nf = nb = None
+            else:
+                _, _, neng, nx, _, nsv, nblock = self.stages[self.cidx[k + 1]]
+                nf = (neng, nsv, nx)
+                nb = (neng, nsv, nx, self._g(nx), nblock)
+            self.link_fwd.append(dict(nclass=nc, args=la, nxt=nf))
+            self.link_bwd.append(dict(nclass=nc, args=la, nxt=nb))
 
     def _build_wn_table(self):
         """Weight-norm descriptor tables over the model's convs: the packed
@@ -269,6 +304,7 @@ class FlowTrainer:
         mode 'separate' keeps weight_norm_fwd + weight_norm_bwd + adam_step."""
         self.fused = False
         self._packed_token = None
+        self.param_pass_mode, self.param_pass_reason = "separate", "requested"
         if mode != "fused":
             return
         from ._lib import Range, WNDesc
@@ -294,6 +330,8 @@ class FlowTrainer:
             off = (block.data_ptr() - base) // 4
             ws = eng.weights(self.dtype)
             if ws["blocks"] < 0:
+                self.param_pass_reason = "a conv row of %s does not fit the fused pass's LDS" % self._module_name(
+                    st[1])
                 return
             if self.pg is None:
                 # single process: every coupling's pass is deferred to ONE launch
@@ -306,6 +344,8 @@ class FlowTrainer:
                 kr = d.cin * d.ks * d.ks
                 a = off + d.dv_off
                 if not (mask[a:a + d.cout * kr] == 1).all():
+                    self.param_pass_reason = "a conv of %s has frozen or regularised weight_v" % self._module_name(
+                        st[1])
                     return
                 covered[a:a + d.cout * kr] = True
                 if d.g and d.dg_off >= 0:
@@ -336,6 +376,7 @@ class FlowTrainer:
         self._opt_all = self._adam_args(0)
         self._vparams = [p for _, p in self.model.named_parameters()]
         self.fused = True
+        self.param_pass_mode, self.param_pass_reason = "fused", None
 
     def _adam_args(self, off):
         from ._lib import AdamArgs
@@ -358,11 +399,21 @@ class FlowTrainer:
     def _token(self):
         return (self.param._version, sum(p._version for p in self._vparams))
 
+    def invalidate_packed(self):
+        """Declare the parameters changed outside the trainer: the next step
+        re-derives the packed weight images (fused parameter pass).  Writes
+        through the parameters themselves (p.mul_, load_state_dict, ...) are
+        seen on their own; writes through `p.data` (e.g. nn.init on
+        `.data`, the reference's utils.py:103-113 style) or through the
+        arena tensor's storage by other means are NOT -- call this after them."""
+        self._packed_token = None
+
     def _ensure_packed(self):
         """Fused pass: the packed weight images and norms are the previous
         step's output; re-derive them (eagerly) when the parameters were
         changed by anything else (first step, capture's restore,
-        load_state_dict, a caller writing the parameters)."""
+        load_state_dict, a caller writing the parameters: their version
+        counters move; writes through `.data` need invalidate_packed())."""
         if not self.fused:
             return
         tok = self._token()
@@ -379,7 +430,7 @@ class FlowTrainer:
         when its update runs.  Disabled (one update at the end) unless the
         backward visits couplings in descending arena offset."""
         self.adam_ranges = None
-        if self.pg is not None or not self.overlap or self.fused:
+        if self.pg is not None or not self.overlap or self.fused or self.links is not None:
             return
         blocks = [st[6] for st in self.stages if st[0] == "coupling"]
         base = self.grad.data_ptr()
@@ -469,18 +520,12 @@ class FlowTrainer:
         return g
 
     # ------------------------------------------------------------------- step
-    def _forward(self):
-        L = _lib.lib()
-        s = stream_ptr()
-        B = self.B
-        n = self.pix[0].numel()
-        if not self.external_input:
-            L.logit_fwd(self.pix.data_ptr(), None, self.seed, 0, self.step_t.data_ptr(), 0.9, self.xl.data_ptr(),
-                        self.logdet.data_ptr(), B, n, s)
-        self.ldj.zero_()
+    def _wn_prepare(self):
+        """the packed weight images of this step (separate parameter pass:
+        the weight-norm forward; fused: the previous step's, _ensure_packed)"""
         late_ready = None
         if self.fused:
-            pass    # the packed images are the previous step's (_ensure_packed)
+            pass
         elif len(self.wn_tables) > 1 and self.side is not None:
             ev = torch.cuda.Event()
             ev.record()
@@ -493,6 +538,20 @@ class FlowTrainer:
         else:
             for t in self.wn_tables:
                 self._wn_fwd(t)
+        return late_ready
+
+    def _forward(self):
+        if self.links is not None:
+            return self._forward_links()
+        L = _lib.lib()
+        s = stream_ptr()
+        B = self.B
+        n = self.pix[0].numel()
+        if not self.external_input:
+            L.logit_fwd(self.pix.data_ptr(), None, self.seed, 0, self.step_t.data_ptr(), 0.9, self.xl.data_ptr(),
+                        self.logdet.data_ptr(), B, n, s)
+        self.ldj.zero_()
+        late_ready = self._wn_prepare()
         ci = 0
         for i, st in enumerate(self.stages):
             if st[0] == "coupling":
@@ -500,10 +559,8 @@ class FlowTrainer:
                     torch.cuda.current_stream().wait_event(late_ready)
                 ci += 1
                 _, mod, eng, x, z, sv, _ = st
-                nxt = self.chain[i]
                 eng.forward(x, True, self.dtype, False, saved=sv, prepare=False, ldj_sample=self.ldj, z_out=z,
-                            zero_sums=False, in_done=self.chain.get(i - 1) is not None,
-                            chain_next=None if nxt is None else (nxt[2], nxt[5]))
+                            zero_sums=False)
             elif st[0] == "squeeze":
                 _, a, b = st
                 L.squeeze(a.data_ptr(), b.data_ptr(), *a.shape, s)
@@ -519,15 +576,65 @@ class FlowTrainer:
         L.prior_logprob(self.z.data_ptr(), self.ldj.data_ptr(), self.lp.data_ptr(), B, self.z[0].numel(), s)
         self.ll_acc += (self.lp + self.logdet).mean().double()
 
+    def _forward_links(self):
+        """The flow program over coupling links: the input pass (logit
+        transform + the first coupling's in_bn sums), the first coupling's in
+        part, then per coupling its net, u's class sums and the link, and the
+        per-sample log-likelihood.  No permutation kernel, no prior pass:
+        the prior of the factored-out halves and of the last scale is added
+        by the links."""
+        L = _lib.lib()
+        s = stream_ptr()
+        B = self.B
+        _, _, eng0, x0, _, sv0, _ = self.stages[self.cidx[0]]
+        a0 = eng0.link_args(sv0, x0)
+        n_el, esz = x0.numel(), 2 if self.dtype == "bf16" else 4
+        cs_h0 = a0.cs_h0
+        if not self.external_input:
+            _launch("logit", 8 * n_el, 0.0, L.flow_in_fwd, self.pix.data_ptr(), self.seed, self.step_t.data_ptr(),
+                    0.9, self.xl.data_ptr(), self.logdet.data_ptr(), C.byref(a0), B, *x0.shape[1:], s)
+            _launch("coupling", 4 * n_el + esz * x0[:, 0].numel() * cs_h0, 0.0, L.coupling_in_apply, C.byref(a0), s)
+        else:
+            _launch("coupling", 8 * n_el + esz * x0[:, 0].numel() * cs_h0, 0.0, L.coupling_in_fwd, C.byref(a0), s)
+        late_ready = self._wn_prepare()
+        for k, i in enumerate(self.cidx):
+            if k == self.wn_split and late_ready is not None:
+                torch.cuda.current_stream().wait_event(late_ready)
+            _, mod, eng, x, z, sv, _ = self.stages[i]
+            eng.forward_link(x, sv, self.ldj, self.link_fwd[k])
+        L.flow_lp_finish(self.prior.data_ptr(), self.ldj.data_ptr(), self.logdet.data_ptr(),
+                         0 if self.external_input else 1, self.lp.data_ptr(), self.ll_acc.data_ptr(), B, s)
+
+    def _issue_buckets(self, ci, n_coupling):
+        """the all-reduce buckets that coupling ci's gradients complete"""
+        if self.comm_stream is None:
+            return
+        for lo, hi in self.bucket_after.get(n_coupling - 1 - ci, ()):
+            # the bucket's weight gradients were written on the side
+            # stream (overlap) or the current one
+            ev = torch.cuda.Event()
+            ev.record(self.side if self.side is not None else torch.cuda.current_stream())
+            self.comm_stream.wait_event(ev)
+            with torch.cuda.stream(self.comm_stream):
+                if self.comm_events is not None:     # bench.py: per-bucket timing (eager)
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                self._reduce_bucket(lo, hi)
+                if self.comm_events is not None:
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e1.record()
+                    self.comm_events.append((hi - lo, e0, e1))
+
     def _backward(self):
+        if self.links is not None:
+            return self._backward_links()
         L = _lib.lib()
         s = stream_ptr()
         B = self.B
         gz = self._g(self.z)
         L.prior_logprob_bwd(self.z.data_ptr(), self.g_lp.data_ptr(), gz.data_ptr(), B, self.z[0].numel(), s)
-        n_coupling = sum(1 for st in self.stages if st[0] == "coupling")
+        n_coupling = len(self.cidx)
         ci = n_coupling
-        pending = []
         for i in reversed(range(len(self.stages))):
             st = self.stages[i]
             if st[0] == "coupling":
@@ -537,30 +644,10 @@ class FlowTrainer:
                 if self.adam_ranges is not None:
                     lo, hi = self.adam_ranges[ci]
                     after = (lambda lo=lo, hi=hi: self._adam_range(lo, hi))
-                prv = self.stages[i - 1] if self.chain.get(i - 1) is not None else None
                 opt = "defer" if (self.fused and self.pg is None) else None
                 eng.backward(sv, self._g(z), None, self.g_lp, block, gx=self._g(x), side=self.side, after=after,
-                             zero_at_end=True, defer=pending if self.side_group else None,
-                             chain_prev=None if prv is None else (prv[2], prv[5]),
-                             sums_ready=self.chain[i] is not None, opt=opt)
-                if self.side_group and (len(pending) >= self.side_group or ci == 0):
-                    self._flush_side(pending)
-                if self.comm_stream is not None:
-                    for lo, hi in self.bucket_after.get(n_coupling - 1 - ci, ()):
-                        # the bucket's weight gradients were written on the side
-                        # stream (overlap) or the current one
-                        ev = torch.cuda.Event()
-                        ev.record(self.side if self.side is not None else torch.cuda.current_stream())
-                        self.comm_stream.wait_event(ev)
-                        with torch.cuda.stream(self.comm_stream):
-                            if self.comm_events is not None:     # bench.py: per-bucket timing (eager)
-                                e0 = torch.cuda.Event(enable_timing=True)
-                                e0.record()
-                            self._reduce_bucket(lo, hi)
-                            if self.comm_events is not None:
-                                e1 = torch.cuda.Event(enable_timing=True)
-                                e1.record()
-                                self.comm_events.append((hi - lo, e0, e1))
+                             zero_at_end=True, opt=opt)
+                self._issue_buckets(ci, n_coupling)
             elif st[0] == "squeeze":
                 _, a, b = st
                 L.undo_squeeze(self._g(b).data_ptr(), self._g(a).data_ptr(), *a.shape, s)
@@ -574,6 +661,36 @@ class FlowTrainer:
                 _, on, off, full = st
                 L.factor_out(self._g(full).data_ptr(), self._g(on).data_ptr(), self._g(off).data_ptr(),
                              *full.shape, s)
+
+    def _backward_links(self):
+        """Backward over the coupling links, last coupling first: its link
+        backward (dL/dz from the consumer or the prior, then its out part),
+        its net's data gradients and its in part's reduction pass.  A
+        coupling's weight gradients (and, outside the fused single-process
+        pass, its weight-norm backward, which leaves its sums zero) run after
+        the previous coupling's link backward has read those sums; its
+        all-reduce buckets follow them."""
+        n_coupling = len(self.cidx)
+        opt = "defer" if (self.fused and self.pg is None) else None
+        pending, pending_ci = [], None
+        for k in reversed(range(n_coupling)):
+            _, mod, eng, x, z, sv, block = self.stages[self.cidx[k]]
+            mine = []
+            eng.backward_link(sv, self.link_bwd[k], block, self._g(x), self.g_lp, k == 0, mine, opt=opt)
+            self._run_pending(pending, pending_ci, n_coupling)
+            pending, pending_ci = mine, k
+        self._run_pending(pending, pending_ci, n_coupling)
+
+    def _run_pending(self, pending, ci, n_coupling):
+        if not pending:
+            return
+        if self.side is not None:
+            self._flush_side(pending)
+        else:
+            for f in pending:
+                f()
+            pending.clear()
+        self._issue_buckets(ci, n_coupling)
 
     def _flush_side(self, pending):
         """fork the deferred weight-gradient closures onto the side stream"""
@@ -792,6 +909,8 @@ class FlowTrainer:
     def set_pixels(self, pix):
         """Raw pixels in [0, 1]; the step applies logit_transform on the device."""
         self._check_mode(False)
+        if self.external_input:
+            self.logdet.zero_()   # the input pass adds the log-det (rnvp_flow_in_fwd)
         self.external_input = False
         self.pix.copy_(pix)
 

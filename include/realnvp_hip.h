@@ -36,7 +36,7 @@ int rnvp_version(void);
 /* sizeof the library's argument structs, in this order: rnvp_bn_src,
  * rnvp_bn_running, rnvp_conv_args, rnvp_wgrad_conv, rnvp_wgrad_group,
  * rnvp_bn_bwd_args, rnvp_wn_desc, rnvp_adam_args, rnvp_coupling_args,
- * rnvp_net_step, rnvp_range (-1 past the end).  A binding compares them with
+ * rnvp_net_step, rnvp_range, rnvp_link_args (-1 past the end).  A binding compares them with
  * its own mirrors at load time: a library built from another header revision
  * is refused instead of reading descriptor tables at the wrong stride. */
 int rnvp_struct_size(int which);
@@ -256,7 +256,9 @@ int rnvp_weight_norm_bwd(const rnvp_wn_desc* descs_device, int n_desc, int total
  *     layout) of w' = g' v' / ||v'|| for the next step; the data-gradient
  *     image then follows from rnvp_weight_norm_transpose.
  * blk0: prefix sums of rnvp_weight_norm_opt_blocks(cout, cin, ks) (negative:
- * the row does not fit the kernel's LDS -- use the unfused calls).
+ * the row does not fit the kernel's LDS -- use the unfused calls); the block
+ * count assumes the packed row layout cs_in == round_up(cin, 8), which every
+ * descriptor of this call must have (the binding checks its tables).
  * zero0 / zero1 as rnvp_weight_norm_bwd.  Replaces modules_realnvp.py:53-59
  * (weight_norm) and train.py:134, 200 (Adam) for the s/t convs. */
 typedef struct rnvp_adam_args {
@@ -329,14 +331,25 @@ typedef struct rnvp_coupling_args {
      * workgroup on one address); rnvp_coupling_in_bwd folds them into
      * g_scale / g_scale_shift (+=) and leaves them zero */
     double* gscale_part;
-    /* optional, chained couplings (see rnvp_coupling_out_in_fwd /
-     * rnvp_coupling_in_bwd_chain): [RNVP_COUPLING_SHARDS][2*Cb] fp64 sums of
-     * u and u^2 over the transformed positions (checkerboard; zeroed on entry),
-     * and bwd_sums_ready = 1 when bwd_sums were already reduced by the next
-     * coupling's chained in backward (rnvp_coupling_out_bwd then skips its
-     * reduction pass) */
-    double* next_sums;
-    int bwd_sums_ready;
+    /* optional, coupling links (rnvp_coupling_out_u, rnvp_coupling_link_fwd /
+     * _bwd; see "coupling links" below).  All [RNVP_COUPLING_SHARDS][...] fp64,
+     * zeroed on entry to the step that accumulates them:
+     *   cls_sums   [nclass][2][C]  sums of u and u^2 per (pixel class, channel),
+     *              every channel; pixel classes by nclass: 1 = one class,
+     *              2 = (i+j)&1, 4 = (i&1)*2+(j&1) at pixel (i, j)
+     *   prior_sums [nclass][2][C]  sums of -z*g_lp[b] and -z^2*g_lp[b] over the
+     *              elements the link hands to the prior (factored out / final)
+     *   outp_sums  [2][2][C]       sums of gx and gx*x per ((i+j)&1, channel) of
+     *              this coupling's direct input gradient (written by its out
+     *              part's link backward, read by the previous link's)
+     *   in_bwd_ext [2][Cb]         sums of dL/dxa and dL/dxa * xm over the
+     *              positions in_bn normalises (the kept squares / the
+     *              conditioning half) */
+    int nclass;
+    double* cls_sums;
+    double* prior_sums;
+    double* outp_sums;
+    double* in_bwd_ext;
 } rnvp_coupling_args;
 int rnvp_coupling_in_fwd(const rnvp_coupling_args* a, void* stream);   /* in_sums must be zeroed */
 int rnvp_coupling_out_fwd(const rnvp_coupling_args* a, void* stream);  /* out_sums must be zeroed */
@@ -344,27 +357,70 @@ int rnvp_coupling_reverse(const rnvp_coupling_args* a, void* stream);  /* z = in
 int rnvp_coupling_out_bwd(const rnvp_coupling_args* a, void* stream);  /* bwd_sums zeroed; writes gx, gst */
 int rnvp_coupling_in_bwd(const rnvp_coupling_args* a, void* stream);   /* in_bwd_sums zeroed; gx += */
 
-/* Chained couplings: coupling `next` directly consumes coupling a's output
- * (next->x == a->z; same kind and shape, the opposite mask -- the order
- * RealNVP.checkerboard_combo / channelwise_combo build, flow_realnvp.py:98-116).
- * Then next's input BatchNorm statistics are a closed form of a's out_bn
- * statistics: next's in_bn reads exactly the positions a transformed (its
- * kept checkerboard squares / its conditioning half = a's transformed half),
- * where z = (u - mean) * rstd, so sum z = rstd (S1 - n mean) and sum z^2 =
- * rstd^2 (S2 - 2 mean S1 + n mean^2) over those n positions (S1, S2: the sums
- * of u there; a's out_bn sums for channelwise, a->next_sums for checkerboard).
- *   rnvp_coupling_out_in_fwd = rnvp_coupling_out_fwd(a) + rnvp_coupling_in_fwd(next)
- *     in two launches instead of four: a's out part, then one pass writing
- *     z, a's log-det terms and running stats AND next's h0, next's in_bn
- *     running stats and next->in_sums (shard 0 = the closed-form sums; the
- *     other shards must be zero).  Requires training, coupling_bn, no ldj_full.
- *   rnvp_coupling_in_bwd_chain = rnvp_coupling_in_bwd(a) that also reduces
- *     the out_bn backward sums of the coupling `prev` whose output a consumed
- *     (prev->bwd_sums, zeroed on entry) from the final gradient it leaves in
- *     a->gx (= prev's gz); prev's rnvp_coupling_out_bwd then runs with
- *     bwd_sums_ready = 1.  Requires gl_full == NULL (per-sample gl). */
-int rnvp_coupling_out_in_fwd(const rnvp_coupling_args* a, const rnvp_coupling_args* next, void* stream);
-int rnvp_coupling_in_bwd_chain(const rnvp_coupling_args* a, const rnvp_coupling_args* prev, void* stream);
+/* ---- coupling links (the training step's flow program) ----------------------
+ * A link joins coupling a to what consumes its output z (flow_realnvp.py:252-327):
+ *   RNVP_LINK_SAME      coupling n with n->x = z (same kind and shape, the
+ *                       opposite mask: checkerboard_combo / channelwise_combo,
+ *                       flow_realnvp.py:98-116)
+ *   RNVP_LINK_SQUEEZE   checkerboard a -> channelwise n, n->x = squeeze(z)
+ *                       (flow_realnvp.py:260; squeeze 121-127)
+ *   RNVP_LINK_UNFACTOR  channelwise a -> the next scale's checkerboard n,
+ *                       (n->x, off) = factor_out(undo_squeeze(z)) (264-267, 167-177):
+ *                       n->x channel c = z channel 4c (c < K) / 4(c-K)+3, off
+ *                       channel c = z channel 4c+1 / 4(c-K)+2 (K = n->C/2); the
+ *                       off half goes to the prior
+ *   RNVP_LINK_FINAL     z is the last scale's output: all of it goes to the
+ *                       prior (312-327, 336-338)
+ * The squeeze / factor-out permutations live in the link's addressing: no
+ * permuted copy is made.  The prior log N(0,1) of what the link hands to the
+ * prior is added into prior[b] (fp64, flow_realnvp.py:336-338).
+ *
+ * Forward, per coupling a: rnvp_coupling_out_u(a) (after a's s/t net: the
+ * per-class sums of u and the per-sample sum of log_rescale) then
+ * rnvp_coupling_link_fwd(a, n, l): z = out_bn(u) (u recomputed from x and the
+ * net output), a's log-det constant and running statistics, n->x, n's in_bn
+ * statistics in closed form from a's class sums (n->in_sums shard 0; n's in_bn
+ * reads positions that are each wholly transformed or wholly kept by a), n's
+ * net input h0 and in_bn running statistics.  a->nclass must be
+ * rnvp_link_nclass(type, a->kind).
+ *
+ * Backward, per coupling a (n's backward done first): rnvp_coupling_link_bwd(a,
+ * n, l) forms dL/dz of a (n's direct input gradient n->gx + n's in_bn backward
+ * from n->gh0, or the prior's -z*g_lp) and runs a's out part with it (a->gx,
+ * a->gst, a's scale partials, a->outp_sums) -- the out_bn backward sums it needs
+ * are closed forms of n->outp_sums, n->in_bwd_sums, n->in_bwd_ext, n->in_sums and
+ * a's class / prior sums; block 0 writes n's in_bn affine gradients.  Then a's
+ * net backward and rnvp_coupling_in_bwd(a) with a->in_bwd_ext set (only the
+ * reduction pass runs when a->gx is NULL: the first coupling keeps the apply
+ * pass for dL/dx).  Requires training, coupling_bn, per-sample log-det. */
+enum { RNVP_LINK_SAME = 0, RNVP_LINK_SQUEEZE = 1, RNVP_LINK_UNFACTOR = 2, RNVP_LINK_FINAL = 3 };
+typedef struct rnvp_link_args {
+    int type;
+    const float* g_lp;       /* [B] dL/dlog_prob[b] (the prior's and every log-det's gradient weight) */
+    double* prior;           /* [B] += (UNFACTOR, FINAL) */
+    float* off;              /* UNFACTOR: [B, n->C, H, W] factored-out half, or NULL (not stored) */
+    float* z;                /* FINAL: a's output [B, C, H, W], or NULL (not stored) */
+} rnvp_link_args;
+int rnvp_link_nclass(int type, int kind);
+int rnvp_coupling_out_u(const rnvp_coupling_args* a, void* stream);
+int rnvp_coupling_link_fwd(const rnvp_coupling_args* a, const rnvp_coupling_args* n, const rnvp_link_args* l,
+                           void* stream);
+int rnvp_coupling_link_bwd(const rnvp_coupling_args* a, const rnvp_coupling_args* n, const rnvp_link_args* l,
+                           void* stream);
+/* only the in part's apply pass (rnvp_coupling_in_fwd without its statistics
+ * pass: a->in_sums already hold the batch sums, e.g. from rnvp_flow_in_fwd) */
+int rnvp_coupling_in_apply(const rnvp_coupling_args* a, void* stream);
+/* the step's input: logit_transform of raw pixels with device Philox noise
+ * (rnvp_logit_fwd semantics, logdet[b] += instead of =) fused with the first
+ * coupling's in_bn batch sums (first->in_sums +=, NULL = none; first->x must
+ * be y).  Spread over every CU (pixel tiles, not one workgroup per sample). */
+int rnvp_flow_in_fwd(const float* x, uint64_t seed, const long long* epoch, float constraint, float* y,
+                     float* logdet, const rnvp_coupling_args* first, int B, int C, int H, int W, void* stream);
+/* end of the forward: lp[b] = prior[b] + ldj[b]; ll_acc[0] += mean_b(lp[b] +
+ * logdet[b]) (fp64); prior and ldj are left zero for the next step, and
+ * logdet too when zero_logdet */
+int rnvp_flow_lp_finish(double* prior, float* ldj, float* logdet, int zero_logdet, float* lp, double* ll_acc, int B,
+                        void* stream);
 
 /* ---- regulariser and optimizer ------------------------------------------
  * weight_scale = sum over tensors of sum p^2  (flow_realnvp.py:362-369);

@@ -6,6 +6,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 from conftest import ROOT
 
 sys.path.insert(0, ROOT)
@@ -44,3 +46,26 @@ def test_rank_refuses_mismatched_world():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--launch-check"],
                        capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
+
+
+@pytest.mark.gpu
+def test_two_rank_line_is_complete():
+    """`bench.py --gpus 2` (ranks sharing the box's GPU over gloo, a small
+    custom model): rank 0's single JSON line carries the whole-job value, the
+    roofline, the data-parallel diagnostics AND the CPU baseline -- what the
+    driver's multi-GPU runs record."""
+    env = dict(os.environ, RNVP_BENCH_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "1",
+                        "--size", "32", "--res-blocks", "1", "--base-dim", "8", "--batch", "4", "--no-secondary",
+                        "--cpu-steps", "1", "--cpu-batch", "2"],
+                       capture_output=True, text=True, timeout=900, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["global_batch"] == 8
+    assert d["roofline"]["bound"] in ("hbm", "mfma") and d["roofline"]["peak"] > 0
+    assert d["dp"]["world_size_rccl"] == 2 and len(d["dp"]["rank_ms_per_step"]) == 2
+    cb = d["cpu_baseline"]
+    assert cb and cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port"

@@ -42,6 +42,55 @@ def test_invalid_arguments_return_status_without_launch():
     assert dll.rnvp_status_string(-1) == b"invalid argument"
 
 
+def test_stale_library_is_refused(monkeypatch):
+    """A library whose argument structs differ from the binding's mirrors
+    (built from another header revision) is refused at load time: reading a
+    descriptor table at the wrong stride faulted the GPU in round 5
+    (gpurun_out/r5_fm2)."""
+    from realnvp_hip import _lib
+
+    class Grown(ctypes.Structure):
+        _fields_ = list(_lib.CouplingArgs._fields_) + [("extra", ctypes.c_int)]
+    monkeypatch.setattr(_lib, "CouplingArgs", Grown)
+    with pytest.raises(RuntimeError, match="stale build"):
+        _lib._Lib()
+    monkeypatch.undo()
+    _lib._Lib()   # the real mirrors load
+
+
+def test_link_arguments_checked_without_launch():
+    """rnvp_coupling_link_fwd / _bwd / rnvp_coupling_out_u reject inconsistent
+    links before any HIP call: the class mode must be the link's, the
+    geometry must be the link type's (a squeeze quadruples the channels and
+    halves the size, a factor-out halves the channels), training with out_bn."""
+    from realnvp_hip import _lib
+    L = _lib._Lib()
+    assert [L.link_nclass(t, k) for t in range(4) for k in (0, 1)] == [2, 1, 4, 4, 2, 2, 2, 1]
+    f = ctypes.c_float(0.0)
+    d = ctypes.c_double(0.0)
+
+    def args(kind, C, S, cfg, nclass):
+        a = _lib.CouplingArgs()
+        a.kind, a.B, a.C, a.H, a.W, a.mask_config, a.coupling_bn, a.training, a.dtype = kind, 2, C, S, S, cfg, 1, 1, 1
+        a.x = a.st = a.scale = a.scale_shift = a.ldj_sample = ctypes.addressof(f)
+        a.h0 = a.in_sums = a.cls_sums = a.prior_sums = ctypes.addressof(d)
+        a.cs_st, a.cs_h0, a.nclass = 8 * ((2 * C + 7) // 8), 8 * ((2 * C + 8) // 8), nclass
+        return a
+    la = _lib.LinkArgs(_lib.RNVP_LINK_SQUEEZE, ctypes.addressof(f), ctypes.addressof(d), None, None)
+    a, n = args(0, 3, 8, 1, 4), args(1, 12, 4, 0, 1)
+    bad = [
+        (args(0, 3, 8, 1, 2), n),        # wrong class mode for a squeeze
+        (a, args(1, 12, 8, 0, 1)),       # consumer not half the size
+        (a, args(1, 6, 4, 0, 1)),        # consumer not 4x the channels
+        (args(1, 6, 8, 0, 4), n),        # a squeeze starts at a checkerboard coupling
+    ]
+    for x, y in bad:
+        st = L.dll.rnvp_coupling_link_fwd(ctypes.byref(x), ctypes.byref(y), ctypes.byref(la), None)
+        assert st == -1, st
+    a.training = 0
+    assert L.dll.rnvp_coupling_out_u(ctypes.byref(a), None) == -1
+
+
 def _hp(bd, rb, bott=True, skip=True, wn=True, cbn=True):
     import utils
     return utils.Hyperparameters(bd, rb, bott, skip, wn, cbn)

@@ -271,17 +271,12 @@ def check_projections_vs_truth(P, Pref, Ptrue, band=8e-2, tail=0.02):
 
 
 def _trainer(model, B, dtype, chain):
-    """FlowTrainer with consecutive couplings chained (the default,
-    rnvp_coupling_out_in_fwd / _in_bwd_chain) or every coupling's in and out
+    """FlowTrainer over coupling links (the default, rnvp_coupling_link_fwd /
+    _link_bwd) or every coupling's in and out
     parts launched on their own (chain=0)"""
     from realnvp_hip import trainer as TM
-    old = TM.CHAIN_COUPLING
-    TM.CHAIN_COUPLING = chain
-    try:
-        tr = TM.FlowTrainer(model, B, dtype=dtype)
-    finally:
-        TM.CHAIN_COUPLING = old
-    assert any(v is not None for v in tr.chain.values()) == bool(chain)
+    tr = TM.FlowTrainer(model, B, dtype=dtype, chain=bool(chain))
+    assert (tr.links is not None) == bool(chain)
     return tr
 
 
