@@ -293,9 +293,13 @@ def secondary(args, dev):
                                    dtype="fp32", steps=5)
     del tr
 
-    # the drop-in as train.py:176-200 drives it (eager autograd, torch Adam), fp32
+    # the drop-in as train.py:176-200 drives it (eager autograd): with torch's
+    # Adam as the reference builds it (train.py:134), then with the one-line
+    # change to realnvp_hip.FusedAdam (one launch over a flat arena)
+    from realnvp_hip import FusedAdam
     model.train()
-    opt = torch.optim.Adam(model.parameters(), lr=5e-4, weight_decay=5e-5)
+    opt = None
+
     def loop_step():
         x, ld = utils.logit_transform(pix)      # device noise, seed from torch's CPU generator
         opt.zero_grad()
@@ -303,12 +307,18 @@ def secondary(args, dev):
         loss = -(lp + ld).mean() + 5e-5 * ws
         loss.backward()
         opt.step()
+    opt = torch.optim.Adam(model.parameters(), lr=5e-4, weight_decay=5e-5)
+    dt = timed(loop_step, 3, 1)
+    out["drop_in_loop_torch_adam"] = dict(
+        value=round(3 * B / dt, 2), unit="images/sec", ms_per_step=round(dt / 3 * 1e3, 3), dtype="fp32", steps=3,
+        note="model(x) + loss.backward() + torch.optim.Adam, eager (train.py:176-200 unchanged); torch's default "
+             "(foreach) Adam over the 1,960 parameter tensors alone takes ~12.8 ms/step (tools/probe/adam_probe.py)")
+    opt = FusedAdam(model.parameters(), lr=5e-4, weight_decay=5e-5)
     dt = timed(loop_step, 3, 1)
     out["drop_in_loop"] = dict(value=round(3 * B / dt, 2), unit="images/sec", ms_per_step=round(dt / 3 * 1e3, 3),
                                dtype="fp32", steps=3,
-                               note="model(x) + loss.backward() + torch.optim.Adam, eager (train.py:176-200); "
-                                    "torch's default (foreach) Adam over the 1,960 parameter tensors alone takes "
-                                    "~12.8 ms/step (tools/probe/adam_probe.py)")
+                               note="model(x) + loss.backward() + realnvp_hip.FusedAdam (train.py:134 changed to "
+                                    "it), eager")
     # the same loop with the s/t net in bf16 (set_precision, the trainer's mode)
     model.set_precision("bf16")
     dt = timed(loop_step, 3, 1)

@@ -83,6 +83,22 @@ __global__ __launch_bounds__(256) void k_in_apply(rnvp_coupling_args a, int TP, 
         { const float v = a.x[xidx(e < total ? e : 0)]; xp[k] = e < total ? v : 0.f; }   // unconditional (clamped) load: no branch, no wait
     }
     in_bn_table(a, g, tab);
+    if (blockIdx.x == 0 && a.training && a.in_tab) {   // the in_bn table for the backward (coupling links)
+        for (int c = threadIdx.x; c < g.Cb; c += blockDim.x) {
+            float sc, sf, mean, rstd;
+            rnvp_bn_src s;
+            s.shards = RNVP_COUPLING_SHARDS;
+            s.sums = a.in_sums;
+            s.count = (double)g.B * g.HW;
+            s.mean = a.in_rmean; s.var = a.in_rvar;
+            s.gamma = a.in_gamma; s.beta = a.in_beta; s.eps = a.eps;
+            bn_affine(s, g.Cb, c, sc, sf, &mean, &rstd);
+            a.in_tab[c] = sc;
+            a.in_tab[g.Cb + c] = sf;
+            a.in_tab[2 * g.Cb + c] = mean;
+            a.in_tab[3 * g.Cb + c] = rstd;
+        }
+    }
     if (blockIdx.x == 0 && a.training && a.in_rmean) {
         const double cnt = (double)g.B * g.HW;
         for (int c = threadIdx.x; c < g.Cb; c += blockDim.x) {
@@ -583,9 +599,13 @@ __global__ __launch_bounds__(256) void k_in_bwd_red(rnvp_coupling_args a, int TP
         const int e = k * 256 + threadIdx.x;
         { const float v = a.x[xidx(e < total ? e : 0)]; xp[k] = e < total ? v : 0.f; }   // unconditional (clamped) load: no branch, no wait
     }
+    tile_copy_in<T>(a.gh0, t.m0, t.tp, a.cs_gh0, gh);   // in flight under the table's loads
     lds_zero(red, (ext ? 4 : 2) * g.Cb);
-    in_bn_table(a, g, tab);
-    tile_copy_in<T>(a.gh0, t.m0, t.tp, a.cs_gh0, gh);
+    if (a.training && a.in_tab) {   // the forward's table (coupling links): 4*Cb loads instead of the shard sums
+        for (int i = threadIdx.x; i < 4 * g.Cb; i += blockDim.x) tab[i] = a.in_tab[i];
+    } else {
+        in_bn_table(a, g, tab);
+    }
     if (blockIdx.x == 0 && a.gscale_part && threadIdx.x < 64) fold_gscale(a);
     __syncthreads();
     auto body = [&](int e0, float xv) {

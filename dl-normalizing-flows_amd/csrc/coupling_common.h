@@ -108,6 +108,36 @@ __device__ __forceinline__ void tile_copy_out(const T* lds, long long m0, int tp
     for (int i = threadIdx.x; i < n16; i += blockDim.x) d[i] = s[i];
 }
 
+// an NHWC tile's 16-B chunks loaded into registers (R per thread, clamped
+// unconditional loads) and stored to LDS later: the loads of several tiles
+// and tables go out together, one memory round trip for all of them
+template <int R>
+struct TileRegs {
+    u32x4 v[R];
+    int n16;
+};
+template <typename T, int R>
+__device__ __forceinline__ void tile_issue(const void* src, long long m0, int tp, int cs, TileRegs<R>& r) {
+    r.n16 = tp * cs * (int)sizeof(T) / 16;
+    const u32x4* s = (const u32x4*)((const T*)src + m0 * cs);
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const int i = (int)threadIdx.x + k * (int)blockDim.x;
+        r.v[k] = s[i < r.n16 ? i : 0];
+    }
+}
+template <typename T, int R>
+__device__ __forceinline__ void tile_commit(const TileRegs<R>& r, const void* src, long long m0, int cs, T* lds) {
+    u32x4* d = (u32x4*)lds;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const int i = (int)threadIdx.x + k * (int)blockDim.x;
+        if (i < r.n16) d[i] = r.v[k];
+    }
+    const u32x4* s = (const u32x4*)((const T*)src + m0 * cs);
+    for (int i = (int)threadIdx.x + R * (int)blockDim.x; i < r.n16; i += blockDim.x) d[i] = s[i];
+}
+
 __device__ __forceinline__ void lds_zero(double* p, int n) {
     for (int i = threadIdx.x; i < n; i += blockDim.x) p[i] = 0.0;
 }

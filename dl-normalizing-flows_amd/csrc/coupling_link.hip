@@ -28,6 +28,15 @@
 // (k_in_bwd_red with the extra kept-position sums this file's closed forms use).
 #include "coupling_common.h"
 
+// phase stamps for tools/probe/link_stamps.hip (compiled out of the product)
+#ifdef RNVP_LINK_STAMPS
+__device__ unsigned long long* g_link_stamps;
+#define LINK_STAMP(i) \
+    do { if (threadIdx.x == 0) g_link_stamps[blockIdx.x * 8 + (i)] = wall_clock64(); } while (0)
+#else
+#define LINK_STAMP(i) do {} while (0)
+#endif
+
 namespace {
 
 constexpr float LOG_SQRT_2PI = 0.91893853320467274178f;
@@ -63,6 +72,77 @@ __device__ __forceinline__ bool cls_tr(const Geo& g, int nc, int c, int q) {
 // out[i] = sum over the shards of entry i (LDS), spread over the block
 __device__ __forceinline__ void lds_shard_reduce(const double* sums, int width, double* out) {
     for (int i = threadIdx.x; i < width; i += blockDim.x) out[i] = csum(sums, width, i);
+}
+
+// the same over several arrays at once: their entries share one flat index
+// space over the block, so every thread's loads go out together (one memory
+// round trip for up to blockDim entries, not one per array)
+struct ShardArr {
+    const double* p;
+    int w;
+    double* out;
+};
+template <int N>
+__device__ __forceinline__ void lds_shard_reduce_multi(const ShardArr (&a)[N]) {
+    constexpr int K = 2;   // entries per thread per round: K * shards loads in flight (registers: occupancy)
+    int total = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) total += a[i].w;
+    for (int f0 = 0; f0 < total; f0 += K * (int)blockDim.x) {
+        const double* p[K];
+        double* o[K];
+        int w[K], off[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int f = f0 + k * (int)blockDim.x + (int)threadIdx.x;
+            int r = f < total ? f : 0;
+            p[k] = a[0].p;
+            o[k] = f < total ? a[0].out : nullptr;
+            w[k] = a[0].w;
+#pragma unroll
+            for (int i = 1; i < N; ++i) {
+                if (r >= w[k]) {
+                    r -= w[k];
+                    p[k] = a[i].p;
+                    if (o[k]) o[k] = a[i].out;
+                    w[k] = a[i].w;
+                }
+            }
+            off[k] = r;
+        }
+        double v[K][RNVP_COUPLING_SHARDS];
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int h = 0; h < RNVP_COUPLING_SHARDS; ++h) v[k][h] = p[k][(long long)h * w[k] + off[k]];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            double t = 0.0;
+#pragma unroll
+            for (int h = 0; h < RNVP_COUPLING_SHARDS; ++h) t += v[k][h];
+            if (o[k]) o[k][off[k]] = t;
+        }
+    }
+}
+
+// block-wide sums of two values (one pair of barriers); every thread gets them
+__device__ __forceinline__ void block_sum2(double& x, double& y, double* red /* >= 32 entries of LDS */) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    x = wave_sum(x);
+    y = wave_sum(y);
+    __syncthreads();
+    if (lane == 0) {
+        red[wid] = x;
+        red[16 + wid] = y;
+    }
+    __syncthreads();
+    double tx = 0.0, ty = 0.0;
+    for (int i = 0; i < nw; ++i) {
+        tx += red[i];
+        ty += red[16 + i];
+    }
+    x = tx;
+    y = ty;
 }
 
 // a's out_bn batch statistics of out_bn channel cb from the reduced class sums
@@ -181,10 +261,10 @@ __global__ __launch_bounds__(256) void k_out_u(rnvp_coupling_args a, int TP, int
         const float v = a.x[xidx(e < total ? e : 0)];   // unconditional (clamped) load
         xp[k] = e < total ? v : 0.f;
     }
+    const float sc = a.scale[0], ss = a.scale_shift[0];
     lds_zero(red, W2);
     tile_copy_in<T>(a.st, t.m0, t.tp, a.cs_st, st);
     __syncthreads();
-    const float sc = a.scale[0], ss = a.scale_shift[0];
     float sl = 0.f;
     auto body = [&](int e0, float xv) {
         const int e = e0 + threadIdx.x;
@@ -265,9 +345,19 @@ __global__ __launch_bounds__(256) void k_link_fwd(rnvp_coupling_args a, rnvp_cou
         xp[k] = e < total ? v : 0.f;
     }
     const float glp = (PRIOR && l.g_lp) ? l.g_lp[t.b] : 0.f;   // the prior's gradient weight
-    lds_shard_reduce(a.cls_sums, W2, cs);
+    const float sc = a.scale[0], ss = a.scale_shift[0];
+    const int ci = (int)threadIdx.x;   // this thread's in_bn channel of n in the table phase (Cbn <= 256 here)
+    const float gam0 = (TO_N && ci < Cbn && n.in_gamma) ? n.in_gamma[ci] : 1.f;
+    const float bet0 = (TO_N && ci < Cbn && n.in_beta) ? n.in_beta[ci] : 0.f;
+    // the tile's loads go out with the class sums' (one round trip), LDS stores after
+    TileRegs<2> rst;
+    tile_issue<T, 2>(a.st, t.m0, t.tp, a.cs_st, rst);
+    {
+        const ShardArr arrs[1] = {{a.cls_sums, W2, cs}};
+        lds_shard_reduce_multi(arrs);
+    }
+    tile_commit<T, 2>(rst, a.st, t.m0, a.cs_st, sta);
     if (PRIOR) lds_zero(pred, W2p);
-    tile_copy_in<T>(a.st, t.m0, t.tp, a.cs_st, sta);
     if constexpr (TO_N) {   // n's padding / mask channels of the h0 tile
         for (int e = threadIdx.x; e < tpn * csn; e += blockDim.x) {
             const int pl = e / csn, ch = e - pl * csn;
@@ -275,22 +365,29 @@ __global__ __launch_bounds__(256) void k_link_fwd(rnvp_coupling_args a, rnvp_cou
         }
     }
     __syncthreads();
+    // a's out_bn statistics; in the same phase n's in_bn statistics in closed form (the
+    // class it reads is wholly transformed -- z = (u - mean) * rstd with a's fp32 mean /
+    // rstd, recomputed here from the same sums -- or wholly kept: z = u)
     for (int cb = threadIdx.x; cb < Cba; cb += blockDim.x) {
         double mean, var;
         cls_out_stats(cs, ga, nc, cb, a.eps, mean, var);
+        const float rstd = (float)(1.0 / sqrt(var + (double)a.eps));
         ot[cb] = (float)mean;
-        ot[Cra + cb] = (float)(1.0 / sqrt(var + (double)a.eps));
+        ot[Cra + cb] = rstd;
         ot[2 * Cra + cb] = (float)(0.5 * log(var + (double)a.eps));
-        if (blockIdx.x == 0 && a.out_rmean) {
-            const double unb = cnt_a > 1 ? var * cnt_a / (cnt_a - 1) : var;
-            a.out_rmean[cb] = (1.f - a.momentum) * a.out_rmean[cb] + a.momentum * (float)mean;
-            a.out_rvar[cb] = (1.f - a.momentum) * a.out_rvar[cb] + a.momentum * (float)unb;
+        if (blockIdx.x == 0) {
+            if (a.out_tab) {   // for the link backward
+                a.out_tab[cb] = (float)mean;
+                a.out_tab[Cba + cb] = rstd;
+            }
+            if (a.out_rmean) {
+                const double unb = cnt_a > 1 ? var * cnt_a / (cnt_a - 1) : var;
+                a.out_rmean[cb] = (1.f - a.momentum) * a.out_rmean[cb] + a.momentum * (float)mean;
+                a.out_rvar[cb] = (1.f - a.momentum) * a.out_rvar[cb] + a.momentum * (float)unb;
+            }
         }
     }
-    __syncthreads();
     if (TO_N) {
-        // n's in_bn batch statistics in closed form: the class it reads is wholly
-        // transformed (z = (u - mean) * rstd with a's fp32 mean / rstd) or kept (z = u)
         for (int cb = threadIdx.x; cb < Cbn; cb += blockDim.x) {
             int ca, q;
             link_src<LT>(gn, cb, ca, q);
@@ -298,8 +395,10 @@ __global__ __launch_bounds__(256) void k_link_fwd(rnvp_coupling_args a, rnvp_cou
             double D1 = S1, D2 = S2;
             if (cls_tr(ga, nc, ca, q)) {
                 const int cba = ga.kind == 0 ? ca : ca - ga.on_base;
+                double am, av;
+                cls_out_stats(cs, ga, nc, cba, a.eps, am, av);
                 const double N = (double)ga.B * cls_count(nc, ga, q);
-                const double m = (double)ot[cba], r = (double)ot[Cra + cba];
+                const double m = (double)(float)am, r = (double)(float)(1.0 / sqrt(av + (double)a.eps));
                 D1 = r * (S1 - N * m);
                 D2 = r * r * (S2 - 2.0 * m * S1 + N * m * m);
                 if (D2 < 0) D2 = 0;
@@ -308,12 +407,19 @@ __global__ __launch_bounds__(256) void k_link_fwd(rnvp_coupling_args a, rnvp_cou
             double var = D2 / cnt_n - mean * mean;
             if (var < 0) var = 0;
             const float rstd = (float)(1.0 / sqrt(var + (double)n.eps));
-            const float gam = n.in_gamma ? n.in_gamma[cb] : 1.f, bet = n.in_beta ? n.in_beta[cb] : 0.f;
+            const float gam = cb == ci ? gam0 : (n.in_gamma ? n.in_gamma[cb] : 1.f);
+            const float bet = cb == ci ? bet0 : (n.in_beta ? n.in_beta[cb] : 0.f);
             it[cb] = gam * rstd;
             it[Crn + cb] = bet - (float)mean * gam * rstd;
             if (blockIdx.x == 0) {   // n's in_sums (shard 0 = the closed form; the others are zero) and running stats
                 n.in_sums[cb] = D1;
                 n.in_sums[Cbn + cb] = D2;
+                if (n.in_tab) {   // for n's in part backward and the link backward
+                    n.in_tab[cb] = gam * rstd;
+                    n.in_tab[Cbn + cb] = bet - (float)mean * gam * rstd;
+                    n.in_tab[2 * Cbn + cb] = (float)mean;
+                    n.in_tab[3 * Cbn + cb] = rstd;
+                }
                 if (n.in_rmean) {
                     const double iu = cnt_n > 1 ? var * cnt_n / (cnt_n - 1) : var;
                     n.in_rmean[cb] = (1.f - n.momentum) * n.in_rmean[cb] + n.momentum * (float)mean;
@@ -322,6 +428,7 @@ __global__ __launch_bounds__(256) void k_link_fwd(rnvp_coupling_args a, rnvp_cou
             }
         }
     }
+    __syncthreads();
     if (blockIdx.x == 0) {
         if (threadIdx.x == 0) {
             if (a.out_nbt) a.out_nbt[0] += 1;
@@ -333,8 +440,6 @@ __global__ __launch_bounds__(256) void k_link_fwd(rnvp_coupling_args a, rnvp_cou
         k = -k * (float)n_transformed(ga);
         for (int b = threadIdx.x; b < ga.B; b += blockDim.x) a.ldj_sample[b] += k;
     }
-    __syncthreads();
-    const float sc = a.scale[0], ss = a.scale_shift[0];
     double pacc = 0.0;
     float* nx = TO_N ? (float*)n.x : nullptr;
     auto body = [&](int e0, float xv) {
@@ -409,10 +514,11 @@ template <typename T, int LT>
 __global__ __launch_bounds__(256) void k_link_bwd(rnvp_coupling_args a, rnvp_coupling_args n, rnvp_link_args l, int TP,
                                                   int seg) {
     extern __shared__ double dsm[];
-    __shared__ double redl[16];
+    __shared__ double redl[32];
     __shared__ double gls_sh;
     constexpr bool TO_N = LT != RNVP_LINK_FINAL;
     constexpr bool PRIOR = LT == RNVP_LINK_UNFACTOR || LT == RNVP_LINK_FINAL;
+    LINK_STAMP(0);
     const Geo ga = geo(a);
     const Geo gn = TO_N ? geo(n) : ga;
     const Tile t = tile_of(ga, TP);
@@ -420,16 +526,15 @@ __global__ __launch_bounds__(256) void k_link_bwd(rnvp_coupling_args a, rnvp_cou
     const int nc = a.nclass, W2 = nc * 2 * ga.C, W2p = PRIOR ? W2 : 0;
     const int Cn = TO_N ? gn.C : 0, Cbn = TO_N ? gn.Cb : 0;
     const int Cba = ga.Cb, Cra = r4(Cba), Crn = r4(Cbn);
-    double* csa = dsm;               // a's class sums [nc][2][Ca]
-    double* psa = csa + W2;          // a's prior sums [nc][2][Ca]
+    double* psa = dsm;               // a's prior sums [nc][2][Ca]
     double* osn = psa + W2p;         // n's direct-gradient sums [2][2][Cn]
     double* ibn = osn + 4 * Cn;      // n's in_bwd_sums [2][Cbn]
     double* iex = ibn + 2 * Cbn;     // n's in_bwd_ext [2][Cbn]
-    double* isn = iex + 2 * Cbn;     // n's in_sums [2][Cbn]
+    double* isn = iex + 2 * Cbn;     // n's in_sums, shard 0 (the closed form of the forward) [2][Cbn]
     double* red = isn + 2 * Cbn;     // this block's direct-gradient sums of a [2][2][Ca]
     float* ta = (float*)(red + 4 * ga.C);   // a: mean | rstd | kA | kB [Cra each]
-    float* tn = ta + 4 * Cra;               // n: scale | shift | mean | rstd | coef | k1 | k2 [Crn each]
-    T* sta = (T*)(tn + 7 * Crn);            // a's net output tile [tp][cs_st]
+    float* tn = ta + 4 * Cra;               // n: scale | shift | mean | rstd | k1 | k2 [Crn each]
+    T* sta = (T*)(tn + 6 * Crn);            // a's net output tile [tp][cs_st]
     T* gs = sta + TP * a.cs_st;             // a's net output gradient tile [tp][cs_gst]
     T* gh = gs + TP * a.cs_gst;             // n's net input gradient tile [tpn][cs_gh0]
     const int pn0 = LT == RNVP_LINK_SQUEEZE ? t.p0 / 4 : t.p0;
@@ -450,6 +555,7 @@ __global__ __launch_bounds__(256) void k_link_bwd(rnvp_coupling_args a, rnvp_cou
         const float v = n.gx[i];
         return d.to_prior ? 0.f : v;
     };
+    // ---- phase 1: every global load of the table phase in flight together
     float xp[CP_K], gp[CP_K];
 #pragma unroll
     for (int k = 0; k < CP_K; ++k) {
@@ -458,65 +564,83 @@ __global__ __launch_bounds__(256) void k_link_bwd(rnvp_coupling_args a, rnvp_cou
         xp[k] = a.x[aidx(ec)];
         gp[k] = gn_ld(ec);
     }
+    const int tid = (int)threadIdx.x;
     const float glp = a.gl_sample ? a.gl_sample[t.b] : 0.f;           // log-det gradient of sample b
     const float gpr = (PRIOR && l.g_lp) ? l.g_lp[t.b] : 0.f;         // the prior's gradient weight
-    if (threadIdx.x < 64) {   // sum_b dL/dlog_prob[b]: the log-det gradient of every transformed position
-        double s = 0.0;
-        if (a.gl_sample)
-            for (int b = threadIdx.x; b < ga.B; b += 64) s += (double)a.gl_sample[b];
-        s = wave_sum(s);
-        if (threadIdx.x == 0) gls_sh = s;
+    const float sc = a.scale[0], ss = a.scale_shift[0];
+    float glv[4];   // wave 0: the per-sample log-det gradients (summed after the round trip)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int b = tid + 64 * k;
+        const float v = a.gl_sample ? a.gl_sample[b < ga.B ? b : 0] : 0.f;
+        glv[k] = (tid < 64 && b < ga.B) ? v : 0.f;
     }
-    lds_shard_reduce(a.cls_sums, W2, csa);
-    if (PRIOR) lds_shard_reduce(a.prior_sums, W2p, psa);
-    if (TO_N) {
-        lds_shard_reduce(n.outp_sums, 4 * Cn, osn);
-        lds_shard_reduce(n.in_bwd_sums, 2 * Cbn, ibn);
-        lds_shard_reduce(n.in_bwd_ext, 2 * Cbn, iex);
-        lds_shard_reduce(n.in_sums, 2 * Cbn, isn);
+    // the forward's tables: a's out_bn (mean, rstd), n's in_bn (scale, shift, mean, rstd),
+    // n's closed-form in_sums (shard 0); up to 2 / 4 / 2 entries per thread
+    const int nta = 2 * Cba, ntn = 4 * Cbn, nsn = 2 * Cbn;
+    float tav[2], tnv[2];
+    double snv[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int i = tid + 256 * k;
+        tav[k] = a.out_tab[i < nta ? i : 0];
+        tnv[k] = TO_N ? n.in_tab[i < ntn ? i : 0] : 0.f;
+        snv[k] = TO_N ? n.in_sums[i < nsn ? i : 0] : 0.0;
+    }
+    TileRegs<2> rst, rgh;
+    tile_issue<T, 2>(a.st, t.m0, t.tp, a.cs_st, rst);
+    if (TO_N) tile_issue<T, 2>(n.gh0, (long long)t.b * gn.HW + pn0, tpn, csg, rgh);
+    {
+        const ShardArr arrs[4] = {{PRIOR ? a.prior_sums : a.cls_sums, W2p, psa},
+                                  {TO_N ? n.outp_sums : a.cls_sums, 4 * Cn, osn},
+                                  {TO_N ? n.in_bwd_sums : a.cls_sums, 2 * Cbn, ibn},
+                                  {TO_N ? n.in_bwd_ext : a.cls_sums, 2 * Cbn, iex}};
+        lds_shard_reduce_multi(arrs);
+    }
+    // (every load above has returned: commit to LDS)
+    tile_commit<T, 2>(rst, a.st, t.m0, a.cs_st, sta);
+    if (TO_N) tile_commit<T, 2>(rgh, n.gh0, (long long)t.b * gn.HW + pn0, csg, gh);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int i = tid + 256 * k;
+        if (i < nta) ta[(i / Cba) * Cra + i % Cba] = tav[k];
+        if constexpr (TO_N) {
+            if (i < ntn) tn[(i / Cbn) * Crn + i % Cbn] = tnv[k];
+        }
+        if (i < nsn) isn[i] = snv[k];
+    }
+    if constexpr (TO_N) {
+        for (int i = tid + 512; i < ntn; i += blockDim.x) tn[(i / Cbn) * Crn + i % Cbn] = n.in_tab[i];   // > 128 ch.
+    }
+    if (tid < 64) {   // sum_b dL/dlog_prob[b]: the log-det gradient of every transformed position
+        double s = (double)glv[0] + (double)glv[1] + (double)glv[2] + (double)glv[3];
+        if (a.gl_sample)
+            for (int b = tid + 256; b < ga.B; b += 64) s += (double)a.gl_sample[b];
+        s = wave_sum(s);
+        if (tid == 0) gls_sh = s;
     }
     lds_zero(red, 4 * ga.C);
-    tile_copy_in<T>(a.st, t.m0, t.tp, a.cs_st, sta);
-    for (int e = threadIdx.x; e < t.tp * a.cs_gst; e += blockDim.x) stv(&gs[e], 0.f);
-    if (TO_N) tile_copy_in<T>(n.gh0, (long long)t.b * gn.HW + pn0, tpn, csg, gh);
+    for (int e = tid; e < t.tp * a.cs_gst; e += blockDim.x) stv(&gs[e], 0.f);
     __syncthreads();
-    for (int cb = threadIdx.x; cb < Cba; cb += blockDim.x) {
-        double mean, var;
-        cls_out_stats(csa, ga, nc, cb, a.eps, mean, var);
-        ta[cb] = (float)mean;
-        ta[Cra + cb] = (float)(1.0 / sqrt(var + (double)a.eps));
-    }
-    if (TO_N) {
-        for (int cb = threadIdx.x; cb < Cbn; cb += blockDim.x) {
-            // n's in_bn table as the in part formed it (bn_affine of its in_sums)
-            const double mean = isn[cb] / cnt_n;
-            double var = isn[Cbn + cb] / cnt_n - mean * mean;
-            if (var < 0) var = 0;
-            const float rstd = (float)(1.0 / sqrt(var + (double)n.eps));
-            const float gam = n.in_gamma ? n.in_gamma[cb] : 1.f, bet = n.in_beta ? n.in_beta[cb] : 0.f;
-            tn[cb] = gam * rstd;
-            tn[Crn + cb] = bet - (float)mean * gam * rstd;
-            tn[2 * Crn + cb] = (float)mean;
-            tn[3 * Crn + cb] = rstd;
-            tn[4 * Crn + cb] = gam * rstd;
-            tn[5 * Crn + cb] = (float)(ibn[cb] / cnt_n);
-            tn[6 * Crn + cb] = (float)(ibn[Cbn + cb] / cnt_n);
-            if (blockIdx.x == 0) {   // n's in_bn affine gradients (k_in_bwd_apply's block 0)
-                if (n.g_in_beta) n.g_in_beta[cb] = (float)ibn[cb];
-                if (n.g_in_gamma) n.g_in_gamma[cb] = (float)ibn[Cbn + cb];
-            }
+    LINK_STAMP(1);
+    // ---- phase 2: n's in_bn backward coefficients; a's out_bn backward coefficients from
+    // closed-form sums of dL/dz and dL/dz * xhat over a's transformed positions (what
+    // k_out_bwd_red would reduce); k1 / k2 as the in part rounds them
+    for (int cb = tid; cb < Cbn; cb += blockDim.x) {
+        tn[4 * Crn + cb] = (float)(ibn[cb] / cnt_n);
+        tn[5 * Crn + cb] = (float)(ibn[Cbn + cb] / cnt_n);
+        if (blockIdx.x == 0) {   // n's in_bn affine gradients (k_in_bwd_apply's block 0)
+            if (n.g_in_beta) n.g_in_beta[cb] = (float)ibn[cb];
+            if (n.g_in_gamma) n.g_in_gamma[cb] = (float)ibn[Cbn + cb];
         }
     }
-    __syncthreads();
-    // a's out_bn backward coefficients from closed-form sums of dL/dz and dL/dz * xhat
-    // over a's transformed positions (what k_out_bwd_red would reduce)
-    for (int cb = threadIdx.x; cb < Cba; cb += blockDim.x) {
+    for (int cb = tid; cb < Cba; cb += blockDim.x) {
         const int ca = ga.kind == 0 ? cb : ga.on_base + cb;
         double A = 0.0, Bs = 0.0;
         for (int q = 0; q < nc; ++q) {
             if (!cls_tr(ga, nc, ca, q)) continue;
             const Dst d = link_dst<LT>(ga, gn, ca, 0);   // channel routing only (pixel 0)
-            bool prior_cls = PRIOR && (LT == RNVP_LINK_FINAL || d.to_prior);
+            const bool prior_cls = PRIOR && (LT == RNVP_LINK_FINAL || d.to_prior);
             if (prior_cls) {
                 A += psa[(2 * q) * ga.C + ca];
                 Bs += psa[(2 * q + 1) * ga.C + ca];
@@ -543,8 +667,8 @@ __global__ __launch_bounds__(256) void k_link_bwd(rnvp_coupling_args a, rnvp_cou
                 // n's in_bn backward over its whole normalised set S (= this class)
                 const double NS = (double)gn.B * (gn.kind == 0 ? (double)gn.HW - n_transformed(gn) : (double)gn.HW);
                 const double GA = iex[cbn], GAV = iex[Cbn + cbn], SV = isn[cbn], SV2 = isn[Cbn + cbn];
-                const double mi = tn[2 * Crn + cbn], ri = tn[3 * Crn + cbn], coef = tn[4 * Crn + cbn];
-                const double k1 = tn[5 * Crn + cbn], k2 = tn[6 * Crn + cbn];
+                const double coef = tn[cbn], mi = tn[2 * Crn + cbn], ri = tn[3 * Crn + cbn];
+                const double k1 = (float)(ibn[cbn] / cnt_n), k2 = (float)(ibn[Cbn + cbn] / cnt_n);
                 const double Sxh = ri * (SV - NS * mi), Sxhv = ri * (SV2 - mi * SV);
                 A += coef * (GA - NS * k1 - k2 * Sxh);
                 Bs += coef * (GAV - k1 * SV - k2 * Sxhv);
@@ -555,7 +679,7 @@ __global__ __launch_bounds__(256) void k_link_bwd(rnvp_coupling_args a, rnvp_cou
         ta[3 * Cra + cb] = (float)((Bs + G) / cnt_a);
     }
     __syncthreads();
-    const float sc = a.scale[0], ss = a.scale_shift[0];
+    LINK_STAMP(2);
     double gsc = 0.0, gss = 0.0;
     auto body = [&](int e0, float xv, float gnv) {
         const int e = e0 + threadIdx.x;
@@ -587,7 +711,7 @@ __global__ __launch_bounds__(256) void k_link_bwd(rnvp_coupling_args a, rnvp_cou
                     const float g1 = ldv(&gh[pnl * csg + cbn]), g2 = ldv(&gh[pnl * csg + Cbn + cbn]);
                     const float gxa = (xa > 0.f ? g1 : 0.f) - (xa < 0.f ? g2 : 0.f);
                     const float xh = (v - tn[2 * Crn + cbn]) * tn[3 * Crn + cbn];
-                    gz = gnv + tn[4 * Crn + cbn] * (gxa - tn[5 * Crn + cbn] - xh * tn[6 * Crn + cbn]);
+                    gz = gnv + tn[cbn] * (gxa - tn[4 * Crn + cbn] - xh * tn[5 * Crn + cbn]);
                 }
             }
         }
@@ -628,8 +752,10 @@ __global__ __launch_bounds__(256) void k_link_bwd(rnvp_coupling_args a, rnvp_cou
         const float xv = a.x[aidx(ec)], gv = gn_ld(ec);
         body(e0, e < total ? xv : 0.f, e < total ? gv : 0.f);
     }
-    const float dsc = (float)block_sum(gsc, redl);   // (barriers also publish gs and red)
-    const float dss = (float)block_sum(gss, redl);
+    LINK_STAMP(3);
+    block_sum2(gsc, gss, redl);   // (barriers also publish gs and red)
+    const float dsc = (float)gsc, dss = (float)gss;
+    LINK_STAMP(4);
     tile_copy_out<T>(gs, t.m0, t.tp, a.cs_gst, a.gst);
     if (threadIdx.x == 0 && (dsc != 0.f || dss != 0.f)) {
         double* sp = a.gscale_part + 2 * (blockIdx.x % RNVP_COUPLING_SHARDS);
@@ -640,6 +766,8 @@ __global__ __launch_bounds__(256) void k_link_bwd(rnvp_coupling_args a, rnvp_cou
         double* dst = cshard(a.outp_sums, 4 * ga.C);
         for (int i = threadIdx.x; i < 4 * ga.C; i += blockDim.x) atomicAdd(&dst[i], red[i]);
     }
+    __syncthreads();
+    LINK_STAMP(5);
 }
 
 // ---------------------------------------------------------------------------
@@ -755,8 +883,9 @@ extern "C" int rnvp_coupling_link_fwd(const rnvp_coupling_args* a, const rnvp_co
                                       const rnvp_link_args* l, void* stream) {
     if (link_check(a, n, l)) return RNVP_E_INVALID;
     const bool to_n = l->type != RNVP_LINK_FINAL, prior = l->type == RNVP_LINK_UNFACTOR || l->type == RNVP_LINK_FINAL;
-    if (!a->ldj_sample || (prior && (!l->prior || !a->prior_sums))) return RNVP_E_INVALID;
-    if (to_n && (!n->h0 || !n->in_sums || n->cs_h0 < (n->kind == 0 ? 2 * n->C + 1 : n->C))) return RNVP_E_INVALID;
+    if (!a->ldj_sample || !a->out_tab || (prior && (!l->prior || !a->prior_sums))) return RNVP_E_INVALID;
+    if (to_n && (!n->h0 || !n->in_sums || !n->in_tab || n->cs_h0 < (n->kind == 0 ? 2 * n->C + 1 : n->C)))
+        return RNVP_E_INVALID;
     if (a->B == 0) return RNVP_OK;
     const int nrun = a->net_running ? a->n_net_running : 0;
     if (nrun < 0 || (nrun > 0 && a->net_running_cmax <= 0)) return RNVP_E_INVALID;
@@ -786,8 +915,9 @@ extern "C" int rnvp_coupling_link_bwd(const rnvp_coupling_args* a, const rnvp_co
     if (link_check(a, n, l)) return RNVP_E_INVALID;
     const bool to_n = l->type != RNVP_LINK_FINAL, prior = l->type == RNVP_LINK_UNFACTOR || l->type == RNVP_LINK_FINAL;
     const int Cba = a->kind == 0 ? a->C : a->C / 2;
-    if (!a->gx || !a->gst || a->cs_gst < 2 * Cba || !a->gscale_part || (prior && !a->prior_sums)) return RNVP_E_INVALID;
-    if (to_n && (!n->gx || !n->gh0 || !n->in_sums || !n->in_bwd_sums || !n->in_bwd_ext || !n->outp_sums ||
+    if (!a->gx || !a->gst || a->cs_gst < 2 * Cba || !a->gscale_part || (prior && !a->prior_sums) || !a->out_tab)
+        return RNVP_E_INVALID;
+    if (to_n && (!n->gx || !n->gh0 || !n->in_sums || !n->in_tab || !n->in_bwd_sums || !n->in_bwd_ext || !n->outp_sums ||
                  n->cs_gh0 < (n->kind == 0 ? 2 * n->C : n->C)))
         return RNVP_E_INVALID;
     if (a->B == 0) return RNVP_OK;
@@ -797,8 +927,8 @@ extern "C" int rnvp_coupling_link_bwd(const rnvp_coupling_args* a, const rnvp_co
     const int Cn = to_n ? n->C : 0, Cbn = to_n ? (n->kind == 0 ? n->C : n->C / 2) : 0;
     const int W2 = a->nclass * 2 * a->C;
     const int tpn = sq ? tc.TP / 4 : tc.TP;
-    const size_t shm = 8 * (size_t)(W2 + (prior ? W2 : 0) + 4 * Cn + 6 * Cbn + 4 * a->C) +
-                       4 * (size_t)(4 * r4(Cba) + 7 * r4(Cbn)) + (size_t)tc.TP * (a->cs_st + a->cs_gst) * esz +
+    const size_t shm = 8 * (size_t)((prior ? W2 : 0) + 4 * Cn + 6 * Cbn + 4 * a->C) +
+                       4 * (size_t)(4 * r4(Cba) + 6 * r4(Cbn)) + (size_t)tc.TP * (a->cs_st + a->cs_gst) * esz +
                        (to_n ? (size_t)tpn * n->cs_gh0 * esz : 0);
     if (shm > 160 * 1024) return RNVP_E_UNSUPPORTED;
     hipStream_t s = (hipStream_t)stream;

@@ -7,5 +7,7 @@ Layout:
   functions.py   autograd Functions for the drop-in modules
   trainer.py     fused NLL training step (flat parameter arena, fused Adam,
                  HIP-graph capture, RCCL data parallelism)
+  optim.py       FusedAdam: torch.optim.Adam drop-in for the reference loop
 """
 from ._lib import LIB_PATH, lib  # noqa: F401
+from .optim import FusedAdam  # noqa: F401

@@ -116,7 +116,8 @@ class CouplingArgs(C.Structure):
                 ("in_bwd_sums", vp), ("g_in_gamma", vp), ("g_in_beta", vp),
                 ("net_running", vp), ("n_net_running", i32), ("net_running_cmax", i32),
                 ("gscale_part", vp),
-                ("nclass", i32), ("cls_sums", vp), ("prior_sums", vp), ("outp_sums", vp), ("in_bwd_ext", vp)]
+                ("nclass", i32), ("cls_sums", vp), ("prior_sums", vp), ("outp_sums", vp), ("in_bwd_ext", vp),
+                ("out_tab", vp), ("in_tab", vp)]
 
 
 RNVP_LINK_SAME, RNVP_LINK_SQUEEZE, RNVP_LINK_UNFACTOR, RNVP_LINK_FINAL = 0, 1, 2, 3

@@ -13,7 +13,6 @@ Parameter gradients go to a flat fp32 "grad block" laid out like the
 coupling's named_parameters() (frozen weight_g included, never written).
 """
 import ctypes as C
-import os
 from collections import OrderedDict
 
 import torch
@@ -28,12 +27,13 @@ COUPLING_SHARDS = 32      # RNVP_COUPLING_SHARDS (include/realnvp_hip.h)
 BN_MOMENTUM = 0.1
 
 DTYPES = {"fp32": (RNVP_F32, 4, torch.float32), "bf16": (RNVP_BF16, 2, torch.bfloat16)}
-# conv kernel family override for A/B diagnostics (rnvp_conv_args.variant):
+# conv kernel family override for A/B diagnostics (rnvp_conv_args.variant; set
+# programmatically by tests / tools, never from the environment):
 # 0 = per-shape tuned dispatch, 1 = generic LDS-tiled kernels only
-CONV_VARIANT = int(os.environ.get("RNVP_CONV_VARIANT", "0"))
-# grouped launches of independent 1x1 convs (rnvp_net_group); RNVP_NET_GROUP=0
-# launches them one by one
-NET_GROUP = int(os.environ.get("RNVP_NET_GROUP", "1"))
+CONV_VARIANT = 0
+# grouped launches of independent 1x1 convs (rnvp_net_group); False launches
+# them one by one (tests/test_gpu_group.py compares the two)
+NET_GROUP = True
 
 
 def stream_ptr():
@@ -330,6 +330,8 @@ class CouplingEngine:
         # coupling links (rnvp_coupling_out_u / _link_fwd): u's sums per pixel class, the prior's sums
         ar.add("cls_sums", COUPLING_SHARDS * 4 * 2 * self.C * 8)
         ar.add("prior_sums", COUPLING_SHARDS * 4 * 2 * self.C * 8)
+        ar.add("out_tab", 2 * self.Cb * 4)     # the forward's out_bn / in_bn tables for the link backward
+        ar.add("in_tab", 4 * self.Cb * 4)
         sh = stat_shards(M)
         for bn, spec in self.P.bns.items():
             ar.add("s:" + bn, sh * 2 * spec.c * 8)
@@ -905,6 +907,7 @@ class CouplingEngine:
         a = self._coupling_args(T, x, B, H, W, dtype, True)
         a.in_sums, a.h0, a.st = ar.ptr("in_sums"), ar.ptr("h0"), ar.ptr("st")
         a.cls_sums, a.prior_sums = ar.ptr("cls_sums"), ar.ptr("prior_sums")
+        a.out_tab, a.in_tab = ar.ptr("out_tab"), ar.ptr("in_tab")
         a.gst, a.cs_gst = sar.ptr("g:st"), chan_stride(self.P.buf_ch["st"])
         a.gh0, a.cs_gh0 = sar.ptr("g:h0"), chan_stride(self.P.buf_ch["h0"])
         a.in_bwd_sums, a.in_bwd_ext = sar.ptr("in_bwd_sums"), sar.ptr("in_bwd_ext")

@@ -292,7 +292,7 @@ int rnvp_adam_gather(const rnvp_adam_args* adam, const long long* idx, long long
  * st = [shift | log_rescale] (2*Cb channels). */
 /* the coupling's per-channel fp64 reductions are spread over this many
  * shards (workgroup % shards) so no word takes more than ~32 atomic adders */
-#define RNVP_COUPLING_SHARDS 32
+#define RNVP_COUPLING_SHARDS 8
 typedef struct rnvp_coupling_args {
     int kind, B, C, H, W, mask_config, coupling_bn, training, dtype;
     float momentum, eps;
@@ -344,12 +344,18 @@ typedef struct rnvp_coupling_args {
      *              part's link backward, read by the previous link's)
      *   in_bwd_ext [2][Cb]         sums of dL/dxa and dL/dxa * xm over the
      *              positions in_bn normalises (the kept squares / the
-     *              conditioning half) */
+     *              conditioning half)
+     * and two fp32 tables the forward leaves for the backward (written by the
+     * link launch that computes them, or rnvp_coupling_in_apply):
+     *   out_tab    [2][Cb]         out_bn batch mean, 1/sqrt(var + eps)
+     *   in_tab     [4][Cb]         in_bn scale, shift, mean, 1/sqrt(var + eps) */
     int nclass;
     double* cls_sums;
     double* prior_sums;
     double* outp_sums;
     double* in_bwd_ext;
+    float* out_tab;
+    float* in_tab;
 } rnvp_coupling_args;
 int rnvp_coupling_in_fwd(const rnvp_coupling_args* a, void* stream);   /* in_sums must be zeroed */
 int rnvp_coupling_out_fwd(const rnvp_coupling_args* a, void* stream);  /* out_sums must be zeroed */

@@ -1,5 +1,5 @@
 """Grouped launches of independent 1x1 convs (rnvp_net_group, csrc/conv_deep.hip)
-against the same convs launched one by one (RNVP_NET_GROUP=0).
+against the same convs launched one by one (engine.NET_GROUP = False).
 
 The engine groups each core_skips[i] forward with the next block's first 1x1
 and the data gradients of in_skip + every core_skips[i]

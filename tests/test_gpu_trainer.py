@@ -285,6 +285,54 @@ def test_optimizer_checkpoint_roundtrip_with_torch_adam():
     assert float((pc - pb).norm() / pb.norm()) < 1e-3
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_fused_adam_matches_torch_adam(dtype):
+    """realnvp_hip.FusedAdam in the reference loop (train.py:134, 176-200:
+    model(x), loss.backward(), optimizer.step()) against torch.optim.Adam on
+    the same drop-in model: the same per-step log-likelihood and parameters
+    after 3 steps -- bf16: the s/t net's gradients are deterministic, so the
+    trajectories agree to the update's fp32 rounding; fp32: the grouped weight
+    gradient adds slab partials with atomics, so gradients that are zero in
+    exact arithmetic (conv biases before a BatchNorm) are rounding noise whose
+    sign Adam turns into +-lr steps (bounded as in
+    test_optimizer_checkpoint_roundtrip_with_torch_adam).  Then each
+    optimizer's state_dict continues inside the other."""
+    from realnvp_hip import FusedAdam
+    ma, mb = make_model(32, 8, 1).train(), make_model(32, 8, 1).train()
+    ma.set_precision(dtype)
+    mb.set_precision(dtype)
+    oa = torch.optim.Adam(ma.parameters(), lr=5e-4, weight_decay=5e-5)
+    ob = FusedAdam(mb.parameters(), lr=5e-4, weight_decay=5e-5)
+    assert isinstance(ob, torch.optim.Optimizer)
+
+    def cmp(steps):
+        pa = torch.cat([p.detach().reshape(-1) for p in ma.parameters()])
+        pb = torch.cat([p.detach().reshape(-1) for p in mb.parameters()])
+        assert float((pa - pb).abs().max()) <= steps * 2 * 5e-4 * 1.01
+        assert float((pa - pb).norm() / pa.norm()) < (1e-6 if dtype == "bf16" else 1e-3)
+    for s in range(3):
+        la, lb = _torch_step(ma, oa, s), _torch_step(mb, ob, s)
+        np.testing.assert_allclose(lb, la, rtol=1e-5)
+    cmp(3)
+    assert int(ob.step_t.item()) == 3
+    # state dicts cross over: torch Adam's into FusedAdam and back
+    sa, sb = oa.state_dict(), ob.state_dict()
+    assert sorted(sa["state"]) == sorted(sb["state"])
+    assert all(float(sb["state"][k]["step"]) == 3.0 for k in sa["state"])
+    for name in ("exp_avg", "exp_avg_sq"):
+        va = torch.cat([sa["state"][k][name].reshape(-1) for k in sorted(sa["state"])])
+        vb = torch.cat([sb["state"][k][name].reshape(-1) for k in sorted(sa["state"])])
+        assert float((va - vb).norm() / va.norm()) < (1e-4 if dtype == "bf16" else 2e-2), name
+    ob.load_state_dict(sa)
+    oa.load_state_dict(sb)
+    with torch.no_grad():
+        for p, q in zip(mb.parameters(), ma.parameters()):
+            p.copy_(q)
+    la, lb = _torch_step(ma, oa, 3), _torch_step(mb, ob, 3)
+    np.testing.assert_allclose(lb, la, rtol=1e-5)
+    cmp(1)
+
+
 def test_capture_restores_state_and_fixes_input_mode():
     """capture() leaves parameters, moments, step counter and BN buffers as
     they were (ADVICE: warm-up steps used to train silently), and a graph

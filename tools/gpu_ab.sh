@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU box: A/B of bench.py variants.  VARIANTS: ';'-separated "ENV=.. ARGS" items,
-# e.g. VARIANTS='|--overlap|RNVP_SIDE_GROUP=7 --overlap'.  Each run under its own limit.
+# e.g. VARIANTS='|--overlap|--overlap --comm split'.  Each run under its own limit.
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/${TAG:-ab}
 mkdir -p $O
