@@ -8,9 +8,13 @@ The fp32 oracle (realnvp_oracle.py) with the engine's bf16 roundings at the
 places its kernels round (stored conv outputs and their gradients, packed
 BatchNorm+ReLU operands, packed weights in the forward, the net input and the
 s/t output); BatchNorm statistics, couplings, log-det, prior and weight norm
-stay fp32.  Emu(wide=True) accumulates every conv in fp64 (a second,
-equally valid summation order: the spread between the two is the floor any
-bf16 implementation is held to).
+stay fp32.  As in the engine, a BatchNorm's batch statistics are those of the
+UNROUNDED conv output (the conv epilogue reduces its fp32 accumulators
+before the bf16 store), applied to the stored bf16 values; its backward is
+the usual formula on the stored values, rounded once (_BNStat).
+Emu(wide=True) accumulates every conv in fp64 (a second, equally valid
+summation order: the spread between the two is the floor any bf16
+implementation is held to).
 """
 import os
 import sys
@@ -48,6 +52,50 @@ class _RF(torch.autograd.Function):
         return g
 
 
+class _BNStat(torch.autograd.Function):
+    """Training-mode BatchNorm (realnvp_oracle.batch_norm semantics) that
+    normalises the stored values `xs` with the batch statistics of the raw,
+    unrounded values `xr` they were rounded from (the engine's rounding
+    point).  Backward: dL/dxs by the BatchNorm formula on the stored values
+    (the engine's BN-backward apply / dgrad epilogue), nothing to xr (the
+    rounding is straight-through: the caller's _R passes dL/dxs back to xr,
+    rounded once)."""
+    @staticmethod
+    def forward(ctx, xs, xr, w, b):
+        mean = xr.mean(dim=(0, 2, 3))
+        var = (xr - mean.view(1, -1, 1, 1)).pow(2).mean(dim=(0, 2, 3))
+        rstd = 1.0 / torch.sqrt(var + O.BN_EPS)
+        xhat = (xs - mean.view(1, -1, 1, 1)) * rstd.view(1, -1, 1, 1)
+        ctx.save_for_backward(xhat, rstd, w)
+        ctx.stats = (mean.detach(), var.detach())
+        return xhat * w.view(1, -1, 1, 1) + b.view(1, -1, 1, 1)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xhat, rstd, w = ctx.saved_tensors
+        n = dy.numel() // dy.shape[1]
+        db = dy.sum(dim=(0, 2, 3))
+        dw = (dy * xhat).sum(dim=(0, 2, 3))
+        dxs = (w * rstd).view(1, -1, 1, 1) * (dy - (db / n).view(1, -1, 1, 1) - xhat * (dw / n).view(1, -1, 1, 1))
+        return dxs, None, dw, db
+
+
+def _bn_stat(S, p, xs, xr, training):
+    """ReLU-less BatchNorm of stored xs with xr's batch statistics; running
+    statistics updated from them as nn.BatchNorm2d does."""
+    if not training:
+        return O.batch_norm(S, p, xs, training)
+    y = _BNStat.apply(xs, xr, S[p + "weight"], S[p + "bias"])
+    n = xr.numel() // xr.shape[1]
+    with torch.no_grad():
+        mean = xr.detach().mean(dim=(0, 2, 3))
+        var = (xr.detach() - mean.view(1, -1, 1, 1)).pow(2).mean(dim=(0, 2, 3))
+        S[p + "running_mean"].mul_(1 - O.BN_MOMENTUM).add_(O.BN_MOMENTUM * mean)
+        S[p + "running_var"].mul_(1 - O.BN_MOMENTUM).add_(O.BN_MOMENTUM * var * (n / max(n - 1, 1)))
+        S[p + "num_batches_tracked"].add_(1)
+    return y
+
+
 class Emu:
     """The oracle's residual module with the engine's bf16 rounding points;
     wide=True accumulates every conv in fp64 (the summation-order variant)."""
@@ -63,36 +111,42 @@ class Emu:
             return _Wide.apply(x, w, pad) + (b.view(1, -1, 1, 1) if b is not None else 0.0)
         return F.conv2d(x, w, b, padding=pad)
 
-    def operand(self, S, p, x, training):
-        """ReLU(BN(x)) as the MFMA operand (rounded when packed)."""
-        return _R.apply(F.relu(O.batch_norm(S, p, x, training)))
+    def operand(self, S, p, x, xr, training):
+        """ReLU(BN(x)) as the MFMA operand (rounded when packed); x the stored
+        bf16 activation, xr the unrounded value whose statistics the engine's
+        producing epilogue reduced"""
+        return _R.apply(F.relu(_bn_stat(S, p, x, xr, training)))
 
-    def block(self, S, p, x, training, bottleneck, skip_in, skip_p):
+    def block(self, S, p, x, xr, training, bottleneck, skip_in, skip_p):
         r = p + "res_block."
-        h = self.operand(S, p + "in_block.0.", x, training)
+        h = self.operand(S, p + "in_block.0.", x, xr, training)
         if bottleneck:
-            h = _R.apply(self.conv_raw(S, r + "0.", h))
-            h = self.operand(S, r + "1.", h, training)
-            h = _R.apply(self.conv_raw(S, r + "3.", h))
-            h = self.operand(S, r + "4.", h, training)
-            y = _R.apply(self.conv_raw(S, r + "6.", h) + x)       # residual in the epilogue
+            hr = self.conv_raw(S, r + "0.", h)
+            h = self.operand(S, r + "1.", _R.apply(hr), hr, training)
+            hr = self.conv_raw(S, r + "3.", h)
+            h = self.operand(S, r + "4.", _R.apply(hr), hr, training)
+            yr = self.conv_raw(S, r + "6.", h) + x        # residual in the epilogue
         else:
-            h = _R.apply(self.conv_raw(S, r + "0.", h))
-            h = self.operand(S, r + "1.", h, training)
-            y = _R.apply(self.conv_raw(S, r + "3.", h) + x)
-        out = None
+            hr = self.conv_raw(S, r + "0.", h)
+            h = self.operand(S, r + "1.", _R.apply(hr), hr, training)
+            yr = self.conv_raw(S, r + "3.", h) + x
+        y = _R.apply(yr)
+        out = outr = None
         if skip_in is not None:
-            out = _R.apply(skip_in + self.conv_raw(S, skip_p, y))  # skip accumulation
-        return y, out
+            outr = skip_in + self.conv_raw(S, skip_p, y)   # skip accumulation
+            out = _R.apply(outr)
+        return y, yr, out, outr
 
     def module(self, S, p, h0, training, hp):
         assert hp.res_blocks > 0 and hp.skip, "config-1 net (skip, res_blocks > 0)"
-        x = _R.apply(self.conv_raw(S, p + "in_block.", h0))
-        out = _R.apply(self.conv_raw(S, p + "in_skip.", x))
+        xr = self.conv_raw(S, p + "in_block.", h0)
+        x = _R.apply(xr)
+        outr = self.conv_raw(S, p + "in_skip.", x)
+        out = _R.apply(outr)
         for i in range(hp.res_blocks):
-            x, out = self.block(S, p + "core_block.%d." % i, x, training, hp.bottleneck, out,
-                                p + "core_skips.%d." % i)
-        h = self.operand(S, p + "out_block.0.", out, training)
+            x, xr, out, outr = self.block(S, p + "core_block.%d." % i, x, xr, training, hp.bottleneck, out,
+                                          p + "core_skips.%d." % i)
+        h = self.operand(S, p + "out_block.0.", out, outr, training)
         return _R.apply(self.conv_raw(S, p + "out_block.2.", h))
 
 
