@@ -1,0 +1,133 @@
+"""The benchmarked bf16 step trains like the fp32 reference-precision step,
+and the graph-replayed step is the eager step (config 1: 64x64x3, R4, D32,
+batch 64 -- the shape bench.py times; train.py:176-207 is the loop).
+
+* test_bf16_training_tracks_fp32: 200 graph-replayed steps from one
+  initialisation over a fixed set of structured synthetic images.  The bound
+  is measured first: three fp32 runs that differ only in the dequantisation
+  noise stream (Philox seed) give, per 10-step window, the run-to-run scatter
+  of the bits/dim curve (a per-window standard deviation of three runs,
+  bounded below by its median over the curve: three samples make a noisy
+  estimate); the bf16 run (a fourth noise seed) must stay within 3x that
+  scatter of the fp32 runs' mean in every window, and its final bits/dim must
+  be as low as the fp32 runs' within the same allowance.  (Measured: the fp32
+  runs scatter by ~0.013 bpd per window while the curve falls from 6.4 to 2.5
+  bpd over the 200 steps.)
+* test_graph_replay_equals_eager_step: one captured + replayed bf16 step
+  against the same step run eagerly from the same state: the same per-sample
+  log-prob, gradient arena, parameters and Adam moments up to the rounding
+  that the fp64 batch-statistic atomics' order can flip (measured between
+  two eager runs of that step, bound max(2x that, 1e-6) relative L2).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+B, S = 64, 64
+
+
+def structured_images(n, seed=7):
+    """n 64x64x3 8-bit images of a few random low-frequency sinusoids per
+    channel (learnable structure, unlike uniform noise), as k/255"""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    yy, xx = np.meshgrid(np.arange(S), np.arange(S), indexing="ij")
+    out = np.empty((n, 3, S, S), dtype=np.float32)
+    for i in range(n):
+        for c in range(3):
+            v = np.full((S, S), rng.uniform(-0.5, 0.5))
+            for _ in range(3):
+                fy, fx = rng.uniform(0.5, 3.0, size=2) * 2 * math.pi / S
+                v += rng.uniform(0.2, 0.6) * np.sin(fy * yy + fx * xx + rng.uniform(0, 2 * math.pi))
+            k = np.clip(np.round((v + 1.5) / 3.0 * 255.0), 0, 255)
+            out[i, c] = k / 255.0
+    return torch.from_numpy(out)
+
+
+def _model():
+    import flow_realnvp
+    import utils
+    torch.manual_seed(0)
+    prior = torch.distributions.Normal(torch.tensor(0.0, device=DEV), torch.tensor(1.0, device=DEV),
+                                       validate_args=False)
+    hp = utils.Hyperparameters(32, 4, True, True, True, True)
+    with torch.device(DEV):
+        return flow_realnvp.RealNVP(3, S, prior, hp)
+
+
+def _train_curve(dtype, seed, batches, steps=200, window=10):
+    from realnvp_hip.trainer import FlowTrainer
+    tr = FlowTrainer(_model(), B, dtype=dtype, seed=seed)
+    tr.set_pixels(batches[0])
+    tr.capture(warmup=1)
+    curve = []
+    tr.reset_metrics()
+    for k in range(steps):
+        tr.set_pixels(batches[k % len(batches)])
+        tr.step()
+        if (k + 1) % window == 0:
+            curve.append(tr.bits_per_dim(tr.mean_logll(window)))
+            tr.reset_metrics()
+    del tr
+    torch.cuda.empty_cache()
+    return np.array(curve)
+
+
+def test_bf16_training_tracks_fp32():
+    imgs = structured_images(8 * B).to(DEV)
+    batches = [imgs[i * B:(i + 1) * B].contiguous() for i in range(8)]
+    f32 = np.stack([_train_curve("fp32", 1000 + s, batches) for s in range(3)])
+    b16 = _train_curve("bf16", 1003, batches)
+    mu, sd = f32.mean(axis=0), f32.std(axis=0, ddof=1)
+    # three runs give a noisy per-window estimate: pooled over the curve (its
+    # median) as the lower bound of every window's scatter
+    allow = 3 * np.maximum(np.maximum(sd, np.median(sd)), 2e-3)
+    print("fp32 bpd windows", np.round(f32, 4).tolist())
+    print("bf16 bpd windows", np.round(b16, 4).tolist())
+    print("scatter (fp32 sd)", np.round(sd, 5).tolist())
+    # the curves go somewhere: training lowers bits/dim on this data
+    assert f32[:, -1].max() < f32[:, 0].min() - 0.2, f32[:, [0, -1]]
+    dev = np.abs(b16 - mu) / allow
+    assert (dev <= 1).all(), (np.round(dev, 2).tolist())
+    assert b16[-1] <= f32[:, -1].max() + allow[-1]
+
+
+def _state(tr):
+    return dict(lp=tr.lp.double().clone(), grad=tr.grad.double().clone(), param=tr.param.double().clone(),
+                m=tr.exp_avg.double().clone(), v=tr.exp_avg_sq.double().clone())
+
+
+def test_graph_replay_equals_eager_step():
+    from realnvp_hip.trainer import FlowTrainer
+    imgs = structured_images(B, seed=9).to(DEV)
+    tr = FlowTrainer(_model(), B, dtype="bf16", seed=5)
+    tr.set_pixels(imgs)
+    snap = tr._snapshot()
+
+    def eager():
+        tr._restore(snap)
+        tr._packed_token = None          # the packed images follow the restored parameters
+        tr.step_eager()
+        torch.cuda.synchronize()
+        return _state(tr)
+    e1 = eager()
+    e2 = eager()
+    tr._restore(snap)
+    tr._packed_token = None
+    tr.capture(warmup=1)                 # restores the snapshot state itself
+    tr.step()
+    torch.cuda.synchronize()
+    g = _state(tr)
+
+    def rel(a, b):
+        return float((a - b).norm() / b.norm().clamp_min(1e-30))
+    for k in e1:
+        floor = rel(e2[k], e1[k])
+        d = rel(g[k], e1[k])
+        same = int((g[k] == e1[k]).sum()), g[k].numel()
+        print("%-6s graph vs eager %.3g (bitwise equal %d / %d), eager vs eager %.3g" % (k, d, same[0], same[1],
+                                                                                           floor))
+        assert d <= max(2 * floor, 1e-6), (k, d, floor)
