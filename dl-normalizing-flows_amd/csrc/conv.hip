@@ -1845,9 +1845,8 @@ __global__ void k_wn_bwd(const rnvp_wn_desc* __restrict__ descs, int n_desc, flo
 
 inline bool al16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
 
-}  // namespace
-
-extern "C" int rnvp_conv2d(const rnvp_conv_args* a, void* stream) {
+// argument checks shared by rnvp_conv2d and rnvp_conv2d_check
+int conv_args_status(const rnvp_conv_args* a) {
     if (!a || !a->x || !a->w || !a->y) return RNVP_E_INVALID;
     if (a->variant < 0 || (a->variant > RNVP_VARIANT_DEEP && a->variant < RNVP_VARIANT_DEEP0) ||
         a->variant >= RNVP_VARIANT_DEEP0 + RNVP_DEEP_CFGS)
@@ -1861,9 +1860,57 @@ extern "C" int rnvp_conv2d(const rnvp_conv_args* a, void* stream) {
     if (!al16(a->x) || !al16(a->w)) return RNVP_E_INVALID;
     if (a->epi_relu_bn_bwd && !a->epi_x) return RNVP_E_INVALID;
     if ((long long)a->B * a->H * a->W >= (1ll << 31)) return RNVP_E_UNSUPPORTED;
+    if (a->bp) {
+        if (!a->bp_x || !al16(a->bp_x) || (a->bp_out && !al16(a->bp_out))) return RNVP_E_INVALID;
+        if (a->bp_bn.sums && (!a->bp_sums || a->bp_shards < 1 || a->bp_bn.count <= 0)) return RNVP_E_INVALID;
+        if (!a->bp_bn.sums && (!a->bp_bn.mean || !a->bp_bn.var)) return RNVP_E_INVALID;
+        if (a->pro_bn_relu) return RNVP_E_INVALID;
+    }
+    return RNVP_OK;
+}
+
+// the configuration a BatchNorm-backward prologue runs on: the deep family's
+// data-gradient tiles only (the other families have no such prologue).  The
+// tuned dispatch folds where that measured faster than the apply's launch +
+// the plain conv (tools/probe/deep_stamps.py bp): the 3x3 tiles and the
+// 8-wave tiles; the 4-wave 1x1 tiles (M > 1024) lose waves per SIMD to the
+// prologue's registers (a forced deep configuration still runs it)
+int bp_cfg_of(const rnvp_conv_args* a) {
+    if (a->variant >= RNVP_VARIANT_DEEP0) {
+        const int cfg = a->variant - RNVP_VARIANT_DEEP0;
+        return (cfg == 0 || cfg == 4) ? cfg : -1;
+    }
+    if (a->variant != 0 && a->variant != RNVP_VARIANT_DEEP) return -1;
+    const int cfg = rnvp_deep_auto_cfg(a);
+    if (cfg == 4 || (cfg == 0 && a->ks == 3)) return cfg;
+    return -1;
+}
+
+}  // namespace
+
+extern "C" int rnvp_conv2d(const rnvp_conv_args* a, void* stream) {
+    const int st = conv_args_status(a);
+    if (st != RNVP_OK) return st;
     if (a->B == 0) return RNVP_OK;
     hipStream_t s = (hipStream_t)stream;
+    if (a->bp) {
+        const int cfg = bp_cfg_of(a);
+        if (cfg >= 0) return rnvp_deep_launch(a, s, cfg);
+        // the wide scales' streaming 1x1 (bf16) has the prologue too
+        return a->variant == 0 ? rnvp_conv_s1_launch(a, s) : RNVP_E_UNSUPPORTED;
+    }
     return a->dtype == RNVP_F32 ? dispatch_conv<float>(a, s) : dispatch_conv<bf16_t>(a, s);
+}
+
+extern "C" int rnvp_conv2d_check(const rnvp_conv_args* a) {
+    const int st = conv_args_status(a);
+    if (st != RNVP_OK || a->B == 0) return st;
+    if (a->bp) {
+        const int cfg = bp_cfg_of(a);
+        if (cfg >= 0) return rnvp_deep_launch(a, nullptr, cfg, true);
+        return a->variant == 0 ? rnvp_conv_s1_launch(a, nullptr, true) : RNVP_E_UNSUPPORTED;
+    }
+    return RNVP_OK;   // the dispatch has a family for every shape that passes the checks
 }
 
 #ifndef RNVP_SLAB_PX

@@ -414,7 +414,7 @@ __device__ __forceinline__ void bn_bwd_body(const rnvp_bn_bwd_args& a, double* d
 // deep-scale conv family (conv_deep.hip): number of configurations and the
 // launcher of configuration cfg (RNVP_E_UNSUPPORTED when it does not apply)
 constexpr int RNVP_DEEP_CFGS = 7;
-int rnvp_deep_launch(const rnvp_conv_args* a, hipStream_t s, int cfg);
+int rnvp_deep_launch(const rnvp_conv_args* a, hipStream_t s, int cfg, bool dry = false);
 int rnvp_deep_auto_cfg(const rnvp_conv_args* a);
 
 // tap-shared bf16 weight gradients (wgrad_tap.hip): RNVP_E_UNSUPPORTED when a
@@ -422,8 +422,8 @@ int rnvp_deep_auto_cfg(const rnvp_conv_args* a);
 int rnvp_wgrad_tap_launch(rnvp_wgrad_group* g, hipStream_t s);
 
 // register-pipelined streaming 1x1 conv (conv_s1.hip): RNVP_E_UNSUPPORTED
-// outside bf16 / 1x1 / <= 64 channels / M >= 16k
-int rnvp_conv_s1_launch(const rnvp_conv_args* a, hipStream_t s);
+// outside bf16 / 1x1 / <= 64 channels / M >= 16k; dry: checks only
+int rnvp_conv_s1_launch(const rnvp_conv_args* a, hipStream_t s, bool dry = false);
 
 // fan-out groups of 1x1 convs sharing one input at the wide scales (conv_s1.hip):
 // the M > 16k branch of rnvp_net_group_prepare / rnvp_net_group (klass bit 12)

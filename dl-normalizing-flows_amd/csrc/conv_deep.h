@@ -23,12 +23,13 @@ constexpr int DEEP_MAX_CS = 1024;    // prologue BN table capacity (channels)
 template <typename T>
 __host__ __device__ constexpr int deep_pitch(int cs) { return lds_mfma_pitch(cs, Mf<T>::CH); }
 
+// bp: the BatchNorm-backward prologue's table (3 floats per channel, not 2)
 template <typename T, int BN, int NW, int WK, int BM = DEEP_BM>
-size_t deep_lds_bytes(int cs, int W, int ks) {
+size_t deep_lds_bytes(int cs, int W, int ks, bool bp = false) {
     constexpr int TM = BM / 16, WM = NW / WK;
     constexpr int G = WK > 1 ? TM : WM;
     const int hal = (ks / 2) * (W + 1), R = BM + 2 * hal;
-    const size_t head = 4 * (5 * (size_t)BN) + 8 * (2 * (size_t)G * BN) + 4 * 2 * (size_t)cs;
+    const size_t head = 4 * (5 * (size_t)BN) + 8 * (2 * (size_t)G * BN) + 4 * (bp ? 3 : 2) * (size_t)cs;
     const size_t zrow = (size_t)deep_pitch<T>(cs) * sizeof(T);
     size_t act = (size_t)R * deep_pitch<T>(cs) * sizeof(T);
     const size_t red = WK > 1 ? (size_t)WK * BM * (BN + 4) * 4 : 0;
@@ -48,7 +49,12 @@ size_t deep_lds_bytes(int cs, int W, int ks) {
 // 3x3 tiles to ~37 GB/s of weights per CU (TA busy ~55 cycles per load)
 // BM: pixels per tile (64; 128 for the 3x3 tiles of cfg 6, which read each
 // weight slice for twice the pixels: half the weight stream per launch)
-template <typename T, int BN, int KSZ, bool PRO, int NW, int WK, int DK, int NC, bool FM = false, int BM = DEEP_BM>
+// BP: the BatchNorm-backward prologue (rnvp_conv_args.bp; data gradients, so
+// never with PRO): the staged operand is dL/dt = coef (g - k1 - xhat k2) of
+// the gradient g (a.x) and the BatchNorm input t (a.bp_x), formed in
+// registers as the rows go to LDS; channel tile 0 also stores it (a.bp_out)
+template <typename T, int BN, int KSZ, bool PRO, int NW, int WK, int DK, int NC, bool FM = false, int BM = DEEP_BM,
+          bool BP = false>
 __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, int xa, int xb, int vb, int nvb,
                                           char* lds) {
     constexpr int NT = 64 * NW;
@@ -69,7 +75,7 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
     // the operand's channel stride is NC * WK * KS exactly (launcher): the BN
     // table needs ceil(cs / NT) channels per thread, not DEEP_MAX_CS's
     constexpr int CPT = (NC * WK * KS + NT - 1) / NT;
-    constexpr int SB = (20 * 256) / NT;          // staged chunks per thread per batch
+    static_assert(!(BP && PRO), "BatchNorm-backward prologue: data gradients only");
     constexpr int NSTEP = KSZ * KSZ * NC;        // k-steps of one wave (static: fully unrolled)
     const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -110,8 +116,8 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
     float* etab = (float*)lds;                   // scale | shift | mean | rstd [BN each]
     float* btab = etab + 4 * BN;                 // bias [BN]
     double* sred = (double*)(btab + BN);         // [G][BN][2]
-    float* bnp = (float*)(sred + G * BN * 2);    // prologue scale | shift [cs each]
-    T* zrow = (T*)(bnp + 2 * cs);                // [pitch] zeros
+    float* bnp = (float*)(sred + G * BN * 2);    // prologue scale | shift [cs each] (BP: A | B | C)
+    T* zrow = (T*)(bnp + (BP ? 3 : 2) * cs);     // [pitch] zeros
     T* act = zrow + pitch;                       // [R][pitch]; after the K loop: red [WK][BM][RP] f32
 
     // ---- prologue: every independent load at once (weight ring, BN-table
@@ -123,8 +129,18 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
     constexpr int CPR = NC * WK * 4;
     static_assert(NT % CPR == 0, "fixed chunk column per thread");
     constexpr int RSTEP = NT / CPR;
+    // staged chunks per thread per batch.  BP (two operands per chunk): the
+    // slots one batch needs -- the 64 rows of a 1x1 tile, the rows of a 3x3
+    // tile + halo up to 16 pixels wide (wider images loop) -- at most 12 (8
+    // for the 4-wave tiles, whose 3x3 kernels otherwise pass 256 registers
+    // and drop to one wave per SIMD: a second batch costs less)
+    constexpr int SBP = KSZ == 1 ? (BM + RSTEP - 1) / RSTEP : (BM + 2 * 17 + RSTEP - 1) / RSTEP;
+    constexpr int SBC = NT == 256 ? 8 : 12;
+    constexpr int SB = BP ? (SBP < SBC ? SBP : SBC) : 20 * 256 / NT;
     const int cfix = tid % CPR, rbase = tid / CPR;
     u32x4 sv[SB];
+    u32x4 sx[BP ? SB : 1];
+    const T* __restrict__ XT = (const T*)a.bp_x;
     // loads past the staged rows are not issued at all (a uniform skip): at
     // 128 channels the rows fill ~6 of the SB slots, and every wasted load
     // counts against the 63 outstanding vector memory operations a wave can
@@ -136,10 +152,18 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
             const int r = r0 + rbase + u * RSTEP;
             const int p = m0 - hal + r;
             const bool ok = (r < R) & (p >= 0) & (p < M);
-            sv[u] = *(const u32x4*)(X + (ok ? (long long)p * cs + cfix * CH : 0));
+            const long long o = ok ? (long long)p * cs + cfix * CH : 0;
+            sv[u] = *(const u32x4*)(X + o);
+            if constexpr (BP) sx[u] = *(const u32x4*)(XT + o);
         }
     };
     float scv[CH], shv[CH];
+    // BP coefficients of the thread's channels: dL/dt = A g - (B t + C) with
+    // A = gamma rstd, B = A rstd k2, C = A (k1 - rstd k2 mean) (rnvp_bn_bwd_apply's
+    // A (g - k1 - (t - mean) rstd k2), regrouped: three registers per channel)
+    float bca[BP ? CH : 1], bcb[BP ? CH : 1], bcc[BP ? CH : 1];
+    T* __restrict__ BPO = (T*)a.bp_out;
+    const bool bp_store = BP && BPO != nullptr && nt == 0;
     auto stage_store = [&](int r0) {
 #pragma unroll
         for (int u = 0; u < SB; ++u) {
@@ -157,6 +181,17 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
                     for (int e = 0; e < CH; ++e) f[e] = fmaxf(f[e] * scv[e] + shv[e], 0.f);
                     w = pack(f, T());
                 }
+            }
+            if constexpr (BP) {
+                float gv[CH], xv[CH], d[CH];
+                unpack(w, gv, T());
+                unpack(sx[u], xv, T());
+#pragma unroll
+                for (int e = 0; e < CH; ++e) d[e] = fmaf(bca[e], gv[e], -fmaf(bcb[e], xv[e], bcc[e]));
+                w = pack(d, T());
+                // each interior pixel once (its own tile's rows, channel tile 0)
+                if (bp_store && r >= hal && r < hal + BM && p < M)
+                    *(u32x4*)(BPO + (long long)p * cs + cfix * CH) = w;
             }
             const uint32_t keep = (p >= 0 && p < M) ? ~0u : 0u;
             *(u32x4*)(act + r * pitch + cfix * CH) = w & u32x4{keep, keep, keep, keep};
@@ -183,6 +218,17 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
     BnTab<CPT> ptab;
     BnTab<1> etb;
     if (PRO) tab_issue<CPT, NT>(a.pro, a.cin, 0, cs, ptab);
+    // BP: the BatchNorm's batch statistics and the gradient sums, as two
+    // BatchNorm sources (a sums source with no affine reads nothing else)
+    BnTab<BP ? CPT : 1> btb, gtb;
+    rnvp_bn_src gsrc = {};
+    if constexpr (BP) {
+        gsrc.sums = a.bp_sums;
+        gsrc.count = a.bp_bn.count;
+        gsrc.shards = a.bp_shards;
+        tab_issue<CPT, NT>(a.bp_bn, a.cin, 0, cs, btb);
+        tab_issue<CPT, NT>(gsrc, a.cin, 0, cs, gtb);
+    }
     if (epi_bn) tab_issue<1, NT>(a.epi, N, n0, BN, etb);
     const float bval = (tid < BN && a.bias && n0 + tid < N) ? a.bias[n0 + tid] : 0.f;
     EpiPre pre[NE];
@@ -220,6 +266,45 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
     for (int u = 0; u < DK; ++u)
         if (u < NSTEP) bload(u);
     if (PRO) tab_finish<CPT, NT>(a.pro, a.cin, 0, cs, ptab, bnp, bnp + cs, nullptr, nullptr);
+    if constexpr (BP) {
+        // A | B | C per channel (padding channels: 0)
+#pragma unroll
+        for (int j = 0; j < CPT; ++j) {
+            const int c = tid + NT * j;
+            if (c >= cs) continue;
+            float coef = 0.f, k1 = 0.f, k2 = 0.f, mo = 0.f, ro = 1.f;
+            if (c < a.cin) {
+                double mean, var;
+                if (a.bp_bn.sums) {
+                    const double s1 = btb.a1[j] + (a.bp_bn.shards > 1 ? btb.b1[j] : 0.0);
+                    const double s2 = btb.a2[j] + (a.bp_bn.shards > 1 ? btb.b2[j] : 0.0);
+                    mean = s1 / a.bp_bn.count;   // (rnvp_bn_bwd_apply's rounding)
+                    var = s2 / a.bp_bn.count - mean * mean;
+                    if (var < 0) var = 0;
+                } else {
+                    mean = btb.a1[j];
+                    var = btb.a2[j];
+                }
+                ro = (float)(1.0 / sqrt(var + (double)a.bp_bn.eps));
+                mo = (float)mean;
+                coef = btb.gam[j] * ro;
+                const double g1 = gtb.a1[j] + (a.bp_shards > 1 ? gtb.b1[j] : 0.0);
+                const double g2 = gtb.a2[j] + (a.bp_shards > 1 ? gtb.b2[j] : 0.0);
+                if (a.bp_bn.sums) {   // train mode: batch statistics carry gradient
+                    k1 = (float)(g1 / a.bp_bn.count);
+                    k2 = (float)(g2 / a.bp_bn.count);
+                }
+                if (vb == 0) {
+                    if (a.bp_dbeta) a.bp_dbeta[c] = (float)g1;
+                    if (a.bp_dgamma) a.bp_dgamma[c] = (float)g2;
+                }
+            }
+            const double rk2 = (double)ro * (double)k2;
+            bnp[c] = coef;
+            bnp[cs + c] = (float)((double)coef * rk2);
+            bnp[2 * cs + c] = (float)((double)coef * ((double)k1 - rk2 * (double)mo));
+        }
+    }
     if (epi_bn) tab_finish<1, NT>(a.epi, N, n0, BN, etb, etab, etab + BN, etab + 2 * BN, etab + 3 * BN);
     if (tid < BN) btab[tid] = bval;
     for (int c = tid * CH; c < pitch; c += NT * CH) *(u32x4*)(zrow + c) = u32x4{0u, 0u, 0u, 0u};
@@ -230,6 +315,14 @@ __device__ __forceinline__ void deep_tile(const rnvp_conv_args& a, int shards, i
         for (int e = 0; e < CH; ++e) {
             scv[e] = bnp[cfix * CH + e];
             shv[e] = bnp[cs + cfix * CH + e];
+        }
+    }
+    if constexpr (BP) {
+#pragma unroll
+        for (int e = 0; e < CH; ++e) {
+            bca[e] = bnp[cfix * CH + e];
+            bcb[e] = bnp[cs + cfix * CH + e];
+            bcc[e] = bnp[2 * cs + cfix * CH + e];
         }
     }
 

@@ -21,16 +21,24 @@
 
 namespace {
 
-template <typename T, int BN, int KSZ, bool PRO, int NW, int WK, int DK, int NC, bool FM = false, int BM = DEEP_BM>
+template <typename T, int BN, int KSZ, bool PRO, int NW, int WK, int DK, int NC, bool FM = false, int BM = DEEP_BM,
+          bool BP = false>
 __global__ __launch_bounds__(64 * NW) void k_conv_deep(rnvp_conv_args a, int shards, int xa, int xb) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
-    deep_tile<T, BN, KSZ, PRO, NW, WK, DK, NC, FM, BM>(a, shards, xa, xb, blockIdx.x, gridDim.x, lds);
+    deep_tile<T, BN, KSZ, PRO, NW, WK, DK, NC, FM, BM, BP>(a, shards, xa, xb, blockIdx.x, gridDim.x, lds);
 }
 
+// the BatchNorm-backward prologue (a->bp) is compiled for the data-gradient
+// configurations only: 32-channel tiles, whole tile per wave, 64 pixels
+// (rnvp_deep_auto_cfg's cfg 0 / 4)
+template <int BN, int NW, int WK, int BM>
+constexpr bool bp_cfg() { return BN == 32 && WK == NW && BM == DEEP_BM; }
+
+// dry: every check, nothing launched (rnvp_conv2d_check)
 template <typename T, int BN, int NW, int WK, int DK, int NC, int KSZ, int BM = DEEP_BM>
-int launch_deep_nc(const rnvp_conv_args* a, hipStream_t s) {
+int launch_deep_nc(const rnvp_conv_args* a, hipStream_t s, bool dry) {
     const long long M = (long long)a->B * a->H * a->W;
-    const size_t shm = deep_lds_bytes<T, BN, NW, WK, BM>(a->cs_in, a->W, a->ks);
+    const size_t shm = deep_lds_bytes<T, BN, NW, WK, BM>(a->cs_in, a->W, a->ks, a->bp != 0);
     if (shm > 160 * 1024) return RNVP_E_UNSUPPORTED;
     const long long gm = (M + BM - 1) / BM, gn = (a->n + BN - 1) / BN;
     const unsigned grid = (unsigned)(gm * gn);
@@ -38,6 +46,24 @@ int launch_deep_nc(const rnvp_conv_args* a, hipStream_t s) {
     const dim3 blk(64 * NW);
     int xa, xb;
     xcd_blocks(a, (int)gm, (int)gn, BN, sizeof(T), &xa, &xb, BM);
+    if (a->bp) {
+        if constexpr (bp_cfg<BN, NW, WK, BM>()) {
+            if (dry) return RNVP_OK;
+            if constexpr (sizeof(T) == 2 && NC <= 4) {
+                if (a->w_frag) {
+                    k_conv_deep<T, BN, KSZ, false, NW, WK, DK, NC, true, BM, true><<<grid, blk, shm, s>>>(*a, sh, xa, xb);
+                    RNVP_LAUNCH_CHECK();
+                    return RNVP_OK;
+                }
+            }
+            k_conv_deep<T, BN, KSZ, false, NW, WK, DK, NC, false, BM, true><<<grid, blk, shm, s>>>(*a, sh, xa, xb);
+            RNVP_LAUNCH_CHECK();
+            return RNVP_OK;
+        } else {
+            return RNVP_E_UNSUPPORTED;
+        }
+    }
+    if (dry) return RNVP_OK;
     // the fragment-major weight image where the caller provides one (bf16)
     if constexpr (sizeof(T) == 2 && NC <= 4) {
         if (a->w_frag) {
@@ -56,30 +82,31 @@ int launch_deep_nc(const rnvp_conv_args* a, hipStream_t s) {
 // channel chunks per wave NC = cs / (WK * KS), a template parameter (the
 // k-step sequence is unrolled): the channel strides of the RealNVP nets
 template <typename T, int BN, int NW, int WK, int DK>
-int launch_deep(const rnvp_conv_args* a, hipStream_t s) {
+int launch_deep(const rnvp_conv_args* a, hipStream_t s, bool dry) {
     constexpr int KS = 4 * Mf<T>::CH;
     const long long M = (long long)a->B * a->H * a->W;
     if (M > 65536 || a->n < BN / 2 || a->cs_in % (WK * KS)) return RNVP_E_UNSUPPORTED;
     if (a->pro_bn_relu && a->pro.sums && a->pro.shards > 2) return RNVP_E_UNSUPPORTED;
     if (a->epi_relu_bn_bwd && a->epi.sums && a->epi.shards > 2) return RNVP_E_UNSUPPORTED;
     if (a->cs_in > DEEP_MAX_CS) return RNVP_E_UNSUPPORTED;
+    if (a->bp && (a->pro_bn_relu || (a->bp_bn.sums && a->bp_bn.shards > 2) || a->bp_shards > 2)) return RNVP_E_UNSUPPORTED;
     const int nc = a->cs_in / (WK * KS);
     if (a->ks == 1) {
         switch (nc) {
-            case 1: return launch_deep_nc<T, BN, NW, WK, DK, 1, 1>(a, s);
-            case 2: return launch_deep_nc<T, BN, NW, WK, DK, 2, 1>(a, s);
-            case 4: return launch_deep_nc<T, BN, NW, WK, DK, 4, 1>(a, s);
-            case 8: return launch_deep_nc<T, BN, NW, WK, DK, 8, 1>(a, s);
-            case 16: return launch_deep_nc<T, BN, NW, WK, DK, 16, 1>(a, s);
+            case 1: return launch_deep_nc<T, BN, NW, WK, DK, 1, 1>(a, s, dry);
+            case 2: return launch_deep_nc<T, BN, NW, WK, DK, 2, 1>(a, s, dry);
+            case 4: return launch_deep_nc<T, BN, NW, WK, DK, 4, 1>(a, s, dry);
+            case 8: return launch_deep_nc<T, BN, NW, WK, DK, 8, 1>(a, s, dry);
+            case 16: return launch_deep_nc<T, BN, NW, WK, DK, 16, 1>(a, s, dry);
         }
         return RNVP_E_UNSUPPORTED;
     }
     if constexpr (WK == NW) {   // 3x3: whole-tile-per-wave configurations only
         switch (nc) {
-            case 1: return launch_deep_nc<T, BN, NW, WK, DK, 1, 3>(a, s);
-            case 2: return launch_deep_nc<T, BN, NW, WK, DK, 2, 3>(a, s);
-            case 4: return launch_deep_nc<T, BN, NW, WK, DK, 4, 3>(a, s);
-            case 8: return launch_deep_nc<T, BN, NW, WK, DK, 8, 3>(a, s);
+            case 1: return launch_deep_nc<T, BN, NW, WK, DK, 1, 3>(a, s, dry);
+            case 2: return launch_deep_nc<T, BN, NW, WK, DK, 2, 3>(a, s, dry);
+            case 4: return launch_deep_nc<T, BN, NW, WK, DK, 4, 3>(a, s, dry);
+            case 8: return launch_deep_nc<T, BN, NW, WK, DK, 8, 3>(a, s, dry);
         }
     }
     return RNVP_E_UNSUPPORTED;
@@ -88,7 +115,7 @@ int launch_deep(const rnvp_conv_args* a, hipStream_t s) {
 // 128-pixel 3x3 tiles (bf16, <= 4 channel chunks per wave): each weight
 // slice serves twice the pixels of the 64-pixel tiles
 template <typename T, int BN, int NW, int WK, int DK>
-int launch_deep_tall(const rnvp_conv_args* a, hipStream_t s) {
+int launch_deep_tall(const rnvp_conv_args* a, hipStream_t s, bool dry) {
     constexpr int KS = 4 * Mf<T>::CH;
     if constexpr (sizeof(T) != 2) {
         return RNVP_E_UNSUPPORTED;
@@ -98,9 +125,9 @@ int launch_deep_tall(const rnvp_conv_args* a, hipStream_t s) {
         if (a->pro_bn_relu && a->pro.sums && a->pro.shards > 2) return RNVP_E_UNSUPPORTED;
         if (a->epi_relu_bn_bwd && a->epi.sums && a->epi.shards > 2) return RNVP_E_UNSUPPORTED;
         switch (a->cs_in / (WK * KS)) {
-            case 1: return launch_deep_nc<T, BN, NW, WK, DK, 1, 3, 128>(a, s);
-            case 2: return launch_deep_nc<T, BN, NW, WK, DK, 2, 3, 128>(a, s);
-            case 4: return launch_deep_nc<T, BN, NW, WK, DK, 4, 3, 128>(a, s);
+            case 1: return launch_deep_nc<T, BN, NW, WK, DK, 1, 3, 128>(a, s, dry);
+            case 2: return launch_deep_nc<T, BN, NW, WK, DK, 2, 3, 128>(a, s, dry);
+            case 4: return launch_deep_nc<T, BN, NW, WK, DK, 4, 3, 128>(a, s, dry);
         }
         return RNVP_E_UNSUPPORTED;
     }
@@ -115,15 +142,15 @@ int launch_deep_tall(const rnvp_conv_args* a, hipStream_t s) {
 // cfg 5                 64   8   8   6   cfg 1 with 8 waves
 // cfg 6                 32   4   4   8   cfg 0 on 128-pixel tiles (bf16 3x3)
 template <typename T>
-int launch_cfg(const rnvp_conv_args* a, hipStream_t s, int cfg) {
+int launch_cfg(const rnvp_conv_args* a, hipStream_t s, int cfg, bool dry) {
     switch (cfg) {
-        case 0: return launch_deep<T, 32, 4, 4, 8>(a, s);
-        case 1: return launch_deep<T, 64, 4, 4, 6>(a, s);
-        case 2: return a->ks == 1 ? launch_deep<T, 64, 4, 1, 8>(a, s) : RNVP_E_UNSUPPORTED;
-        case 3: return a->ks == 1 ? launch_deep<T, 32, 4, 2, 8>(a, s) : RNVP_E_UNSUPPORTED;
-        case 4: return launch_deep<T, 32, 8, 8, 8>(a, s);
-        case 5: return launch_deep<T, 64, 8, 8, 6>(a, s);
-        case 6: return launch_deep_tall<T, 32, 4, 4, 8>(a, s);
+        case 0: return launch_deep<T, 32, 4, 4, 8>(a, s, dry);
+        case 1: return launch_deep<T, 64, 4, 4, 6>(a, s, dry);
+        case 2: return a->ks == 1 ? launch_deep<T, 64, 4, 1, 8>(a, s, dry) : RNVP_E_UNSUPPORTED;
+        case 3: return a->ks == 1 ? launch_deep<T, 32, 4, 2, 8>(a, s, dry) : RNVP_E_UNSUPPORTED;
+        case 4: return launch_deep<T, 32, 8, 8, 8>(a, s, dry);
+        case 5: return launch_deep<T, 64, 8, 8, 6>(a, s, dry);
+        case 6: return launch_deep_tall<T, 32, 4, 4, 8>(a, s, dry);
     }
     return RNVP_E_INVALID;
 }
@@ -209,6 +236,9 @@ extern "C" int rnvp_net_group_prepare(rnvp_net_step* steps, int n, int* klass, i
     if (!steps || n <= 0 || n > RNVP_NET_GROUP_MAX || !klass || !grid || !lds_bytes) return RNVP_E_INVALID;
     const rnvp_conv_args& a0 = steps[0].conv;
     const long long M = (long long)a0.B * a0.H * a0.W;
+    // the grouped tiles have no BatchNorm-backward prologue
+    for (int i = 0; i < n; ++i)
+        if (steps[i].conv.bp) return RNVP_E_UNSUPPORTED;
     // wide scales: convs sharing one input run as a fan-out (conv_s1.hip)
     if (M > 16384) return rnvp_s1_fanout_prepare(steps, n, klass, grid, lds_bytes);
     if (M <= 0) return RNVP_E_UNSUPPORTED;
@@ -329,7 +359,7 @@ int rnvp_deep_auto_cfg(const rnvp_conv_args* a) {
     return a->cs_in % (8 * kc) == 0 ? 5 : 1;
 }
 
-int rnvp_deep_launch(const rnvp_conv_args* a, hipStream_t s, int cfg) {
+int rnvp_deep_launch(const rnvp_conv_args* a, hipStream_t s, int cfg, bool dry) {
     if (cfg < 0 || cfg >= RNVP_DEEP_CFGS) return RNVP_E_INVALID;
-    return a->dtype == RNVP_F32 ? launch_cfg<float>(a, s, cfg) : launch_cfg<bf16_t>(a, s, cfg);
+    return a->dtype == RNVP_F32 ? launch_cfg<float>(a, s, cfg, dry) : launch_cfg<bf16_t>(a, s, cfg, dry);
 }

@@ -23,6 +23,15 @@
 
 namespace {
 
+// phase stamps for tools/probe/s1_stamps.hip (compiled out of the product)
+#ifdef RNVP_S1_STAMPS
+__device__ unsigned long long* g_s1_stamps;
+#define S1_STAMP(i) \
+    do { if (threadIdx.x == 0) g_s1_stamps[blockIdx.x * 8 + (i)] = wall_clock64(); } while (0)
+#else
+#define S1_STAMP(i) do {} while (0)
+#endif
+
 // NOPS epilogue operand streams per element (residual, previous y, the dgrad
 // epilogue's pre-BN x -- in that order, those present)
 // two waves per SIMD (<= 256 registers) unless that would spill
@@ -35,7 +44,12 @@ constexpr int s1_min_blocks() { return (NKS == 2 && (NOPS == 3 || (NT == 4 && NO
 // -- with both paths in one function the compiler's wait tracking merges
 // them and waits for every load in flight (the first tile's included)
 // before the table sums.
-template <int NT, int NKS, int TW, int NOPS, bool TP>
+// BP: the BatchNorm-backward prologue of a data gradient (rnvp_conv_args.bp):
+// x is the pre-apply gradient g, bp_x the BatchNorm input t; each chunk becomes
+// dL/dt = A g - (B t + C) in registers (the deep tiles' form, conv_deep.h) and
+// is stored once to bp_out (a workgroup covers every output channel, so every
+// pixel chunk is transformed exactly once)
+template <int NT, int NKS, int TW, int NOPS, bool TP, bool BP = false>
 __global__ __launch_bounds__(256, (s1_min_blocks<NT, NKS, NOPS>())) void k_conv_s1(rnvp_conv_args a, int shards) {
     constexpr int CH = 8, KS = 32;            // bf16: 8 channels per 16-B chunk, 32 per k-step
     constexpr int NC = 16 * NT;
@@ -44,13 +58,14 @@ __global__ __launch_bounds__(256, (s1_min_blocks<NT, NKS, NOPS>())) void k_conv_
     __shared__ double tabred[(2 * 4 * 256 > 4 * NC * 2) ? 2 * 4 * 256 : 4 * NC * 2];
     double (*red)[NC][2] = (double (*)[NC][2])tabred;
     __shared__ double tmp[2 * 64];
-    __shared__ __attribute__((aligned(16))) float bnp[2 * 64];
+    __shared__ __attribute__((aligned(16))) float bnp[3 * 64];   // pro: scale | shift; BP: A | B | C
     __shared__ float etab[4 * NC];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, li = lane & 15;
     const int M = a.B * a.H * a.W;             // < 2^31 (host)
     const int N = a.n, cs = a.cs_in, cso = a.cs_out;
     const bool pro = a.pro_bn_relu != 0, epi_bn = a.epi_relu_bn_bwd != 0;
     const bool has_acc = a.accumulate != 0;
+    S1_STAMP(0);
 
     // the BN tables' shard sums first: their wait does not queue behind the
     // weight and tile loads (vmcnt completes in issue order)
@@ -60,6 +75,12 @@ __global__ __launch_bounds__(256, (s1_min_blocks<NT, NKS, NOPS>())) void k_conv_
     const bool epi_pre = TP && epi_bn;
     if (pro_pre) shard_issue<4>(a.pro.sums, a.cin, a.pro.shards, 0, pnv, pro_l);
     if (epi_pre) shard_issue<4>(a.epi.sums, N, a.epi.shards, 0, min(NC, N), epi_l);
+    ShardLoads<BP ? 4 : 1> bpb_l, bpg_l;
+    if constexpr (BP) {
+        shard_issue<4>(a.bp_bn.sums, a.cin, a.bp_bn.shards, 0, pnv, bpb_l);
+        shard_issue<4>(a.bp_sums, a.cin, a.bp_shards, 0, pnv, bpg_l);
+    }
+    const BnAff bp_a = BP ? bn_aff_issue(a.bp_bn, a.cin, 0, a.w) : BnAff{1.f, 0.f};
     // the tables' affine parameters in the same batch (cs, NC <= 64 < 256)
     const BnAff pro_a = bn_aff_issue(a.pro, a.cin, 0, a.w);
     const BnAff epi_a = bn_aff_issue(a.epi, N, 0, a.w);
@@ -101,10 +122,14 @@ __global__ __launch_bounds__(256, (s1_min_blocks<NT, NKS, NOPS>())) void k_conv_
                                                   0x00020000);
     }
     constexpr int OOB = 0x7ffffff0;
+    const __amdgpu_buffer_rsrc_t TR = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(BP ? a.bp_x : a.x), 0,
+                                                                        (int)((long long)M * cs * 2), 0x00020000);
+    bf16_t* __restrict__ BPO = (bf16_t*)a.bp_out;
 
     // ---- tile ring: pixel chunks + epilogue operands of two tiles ----
     struct Tile {
         u32x4 x[TW][NKS];
+        u32x4 t[BP ? TW : 1][BP ? NKS : 1];
         uint2 o[NOPS > 0 ? NOPS : 1][TW][NT];
     };
     Tile ring[2];
@@ -121,7 +146,9 @@ __global__ __launch_bounds__(256, (s1_min_blocks<NT, NKS, NOPS>())) void k_conv_
 #pragma unroll
             for (int s = 0; s < NKS; ++s) {
                 const int k = s * KS + g * CH;
-                T.x[i][s] = __builtin_amdgcn_raw_buffer_load_b128(XR, (okm & (k < cs)) ? (m * cs + k) * 2 : OOB, 0, 0);
+                const int off = (okm & (k < cs)) ? (m * cs + k) * 2 : OOB;
+                T.x[i][s] = __builtin_amdgcn_raw_buffer_load_b128(XR, off, 0, 0);
+                if constexpr (BP) T.t[i][s] = __builtin_amdgcn_raw_buffer_load_b128(TR, off, 0, 0);
             }
 #pragma unroll
             for (int j = 0; j < NT; ++j) {
@@ -156,7 +183,26 @@ __global__ __launch_bounds__(256, (s1_min_blocks<NT, NKS, NOPS>())) void k_conv_
 #pragma unroll
             for (int s = 0; s < NKS; ++s) {
                 u32x4 v = T.x[i][s];
-                if (pro) {
+                if constexpr (BP) {
+                    const int c0 = s * KS + g * CH;
+                    const int m = t * (16 * TW) + i * 16 + li, k = c0;
+                    float gv[CH], tv[CH], d[CH];
+                    unpack(v, gv, bf16_t());
+                    unpack(T.t[i][s], tv, bf16_t());
+                    const float4 qa = *(const float4*)&bnp[c0], qb = *(const float4*)&bnp[c0 + 4];
+                    const float4 ra = *(const float4*)&bnp[64 + c0], rb = *(const float4*)&bnp[64 + c0 + 4];
+                    const float4 ua = *(const float4*)&bnp[128 + c0], ub = *(const float4*)&bnp[128 + c0 + 4];
+                    const float A[CH] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
+                    const float Bv[CH] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
+                    const float Cv[CH] = {ua.x, ua.y, ua.z, ua.w, ub.x, ub.y, ub.z, ub.w};
+#pragma unroll
+                    for (int e = 0; e < CH; ++e) d[e] = fmaf(A[e], gv[e], -fmaf(Bv[e], tv[e], Cv[e]));
+                    v = pack(d, bf16_t());
+                    const bool in = (m < M) & (k < cs);
+                    if (in && BPO) *(u32x4*)(BPO + (long long)m * cs + k) = v;
+                    const uint32_t keep = in ? ~0u : 0u;
+                    v &= u32x4{keep, keep, keep, keep};
+                } else if (pro) {
                     // prologue coefficients from LDS (registers go to the tile ring)
                     const int c0 = s * KS + g * CH;
                     const float4 sa = *(const float4*)&bnp[c0], sb = *(const float4*)&bnp[c0 + 4];
@@ -228,6 +274,37 @@ __global__ __launch_bounds__(256, (s1_min_blocks<NT, NKS, NOPS>())) void k_conv_
 
     // ---- tables (every thread: block-wide reductions), their loads in flight
     // behind the weights and the first tile's ----
+    if constexpr (BP) {
+        // dL/dt = A g - (B t + C): A = gamma rstd, B = A rstd k2, C = A (k1 - rstd k2 mean)
+        // (rnvp_bn_bwd_apply's A (g - k1 - (t - mean) rstd k2) regrouped)
+        shard_sum_tab<4>(bpb_l, pnv, a.bp_bn.shards, tabred, tmp, tmp + cs);
+        const double S1 = tid < pnv ? tmp[tid] : 0.0, S2 = tid < pnv ? tmp[cs + tid] : 0.0;
+        __syncthreads();
+        shard_sum_tab<4>(bpg_l, pnv, a.bp_shards, tabred, tmp, tmp + cs);
+        if (tid < cs) {
+            float A = 0.f, Bc = 0.f, Cc = 0.f;
+            if (tid < pnv) {
+                const double g1 = tmp[tid], g2 = tmp[cs + tid], cnt = a.bp_bn.count;
+                const double mean = S1 / cnt;
+                double var = S2 / cnt - mean * mean;
+                if (var < 0) var = 0;
+                const float rstd = (float)(1.0 / sqrt(var + (double)a.bp_bn.eps));
+                A = (a.bp_bn.gamma ? bp_a.g : 1.f) * rstd;
+                const float k1 = (float)(g1 / cnt), k2 = (float)(g2 / cnt);
+                const double rk2 = (double)rstd * (double)k2;
+                Bc = (float)((double)A * rk2);
+                Cc = (float)((double)A * ((double)k1 - rk2 * (double)(float)mean));
+                if (blockIdx.x == 0) {
+                    if (a.bp_dbeta) a.bp_dbeta[tid] = (float)g1;
+                    if (a.bp_dgamma) a.bp_dgamma[tid] = (float)g2;
+                }
+            }
+            bnp[tid] = A;
+            bnp[64 + tid] = Bc;
+            bnp[128 + tid] = Cc;
+        }
+        __syncthreads();
+    }
     if constexpr (TP) {
         if (pro) {
             shard_sum_tab<4>(pro_l, pnv, a.pro.shards, tabred, tmp, tmp + cs);
@@ -242,6 +319,7 @@ __global__ __launch_bounds__(256, (s1_min_blocks<NT, NKS, NOPS>())) void k_conv_
         if (epi_bn) block_bn_table(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp);
     }
     __syncthreads();
+    S1_STAMP(1);
 
     while (t < ntiles) {
         if (t + nwaves < ntiles) load(t + nwaves, I1{});
@@ -252,6 +330,7 @@ __global__ __launch_bounds__(256, (s1_min_blocks<NT, NKS, NOPS>())) void k_conv_
         run(t, I1{});
         t += nwaves;
     }
+    S1_STAMP(2);
 
     // ---- batch statistics: DPP row sums, LDS across waves, sharded fp64 atomics ----
     const bool want_sums = a.out_sums || (epi_bn && a.epi_sums);
@@ -279,10 +358,12 @@ __global__ __launch_bounds__(256, (s1_min_blocks<NT, NKS, NOPS>())) void k_conv_
             atomicAdd(&sums[N + n], t2);
         }
     }
+    S1_STAMP(3);
 }
 
-template <int NT, int NKS, int TW, int NOPS, bool TP>
-int launch_s1(const rnvp_conv_args* a, hipStream_t s) {
+template <int NT, int NKS, int TW, int NOPS, bool TP, bool BP = false>
+int launch_s1(const rnvp_conv_args* a, hipStream_t s, bool dry) {
+    if (dry) return RNVP_OK;
     const long long M = (long long)a->B * a->H * a->W;
     const long long ntiles = (M + 16 * TW - 1) / (16 * TW);
     // one resident wave of workgroups, one tile per wave and step with the
@@ -290,14 +371,14 @@ int launch_s1(const rnvp_conv_args* a, hipStream_t s) {
     // pipeline; more tiles per wave measured slower, profiles/r4_step_ab.txt)
     static const int per_cu = [] {
         int n = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_conv_s1<NT, NKS, TW, NOPS, TP>, 256, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_conv_s1<NT, NKS, TW, NOPS, TP, BP>, 256, 0) != hipSuccess ||
             n < 1)
             n = 1;
         return n;
     }();
     long long grid = (ntiles + 3) / 4;
     if (grid > 256LL * per_cu) grid = 256LL * per_cu;
-    k_conv_s1<NT, NKS, TW, NOPS, TP><<<(unsigned)grid, 256, 0, s>>>(*a, rnvp_stat_shards(M));
+    k_conv_s1<NT, NKS, TW, NOPS, TP, BP><<<(unsigned)grid, 256, 0, s>>>(*a, rnvp_stat_shards(M));
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
 }
@@ -305,24 +386,38 @@ int launch_s1(const rnvp_conv_args* a, hipStream_t s) {
 // every BN table from batch sums whose shards fit shard_issue<4> (256 threads)
 inline bool s1_tables_pre(const rnvp_conv_args* a, int NC) {
     auto fits = [](int nc, int shards) { return (long long)nc * (shards < 1 ? 1 : shards) <= 4LL * 256; };
+    if (a->bp) {
+        const int nc = a->cs_in < a->cin ? a->cs_in : a->cin;
+        if (!a->bp_bn.sums || !a->bp_sums || !fits(nc, a->bp_bn.shards) || !fits(nc, a->bp_shards)) return false;
+    }
     if (a->pro_bn_relu && !(a->pro.sums && fits(a->cs_in < a->cin ? a->cs_in : a->cin, a->pro.shards))) return false;
     if (a->epi_relu_bn_bwd && !(a->epi.sums && fits(NC < a->n ? NC : a->n, a->epi.shards))) return false;
     return true;
 }
 
 template <int NT, int NKS, int TW, int NOPS>
-int launch_s1(const rnvp_conv_args* a, hipStream_t s) {
-    return s1_tables_pre(a, 16 * NT) ? launch_s1<NT, NKS, TW, NOPS, true>(a, s) : launch_s1<NT, NKS, TW, NOPS, false>(a, s);
+int launch_s1(const rnvp_conv_args* a, hipStream_t s, bool dry) {
+    if (a->bp) return RNVP_E_UNSUPPORTED;
+    return s1_tables_pre(a, 16 * NT) ? launch_s1<NT, NKS, TW, NOPS, true>(a, s, dry)
+                                     : launch_s1<NT, NKS, TW, NOPS, false>(a, s, dry);
+}
+
+// the BatchNorm-backward prologue: a data gradient with the ReLU/BN epilogue
+// as its one operand stream, every table in a shard table
+template <int NT, int NKS, int TW>
+int launch_s1_bp(const rnvp_conv_args* a, hipStream_t s, bool dry) {
+    if (!a->epi_relu_bn_bwd || a->residual || a->accumulate || !s1_tables_pre(a, 16 * NT)) return RNVP_E_UNSUPPORTED;
+    return launch_s1<NT, NKS, TW, 1, true, true>(a, s, dry);
 }
 
 template <int NT, int NKS, int TW>
-int launch_s1_ops(const rnvp_conv_args* a, hipStream_t s) {
+int launch_s1_ops(const rnvp_conv_args* a, hipStream_t s, bool dry) {
     const int nops = (a->residual ? 1 : 0) + (a->accumulate ? 1 : 0) + (a->epi_relu_bn_bwd ? 1 : 0);
     switch (nops) {
-        case 0: return launch_s1<NT, NKS, TW, 0>(a, s);
-        case 1: return launch_s1<NT, NKS, TW, 1>(a, s);
-        case 2: return launch_s1<NT, NKS, TW, 2>(a, s);
-        default: return launch_s1<NT, NKS, TW, 3>(a, s);
+        case 0: return launch_s1<NT, NKS, TW, 0>(a, s, dry);
+        case 1: return launch_s1<NT, NKS, TW, 1>(a, s, dry);
+        case 2: return launch_s1<NT, NKS, TW, 2>(a, s, dry);
+        default: return launch_s1<NT, NKS, TW, 3>(a, s, dry);
     }
 }
 
@@ -577,15 +672,21 @@ int rnvp_s1_fanout_launch(const rnvp_group_kargs& g, int klass, int grid, int ld
 }
 
 // 1x1, bf16, N <= 64, cs_in <= 64, M >= 16k: the register-pipelined stream
-int rnvp_conv_s1_launch(const rnvp_conv_args* a, hipStream_t s) {
+int rnvp_conv_s1_launch(const rnvp_conv_args* a, hipStream_t s, bool dry) {
     if (a->dtype != RNVP_BF16 || a->ks != 1 || a->n > 64 || a->cs_in > 64 || a->cs_out > 64) return RNVP_E_UNSUPPORTED;
     const long long M = (long long)a->B * a->H * a->W;
     if (M < 16384 || M * 64 * 2 >= (1ll << 31)) return RNVP_E_UNSUPPORTED;
     if (((uintptr_t)a->y & 7) || (a->residual && ((uintptr_t)a->residual & 7)) ||
         (a->epi_relu_bn_bwd && ((uintptr_t)a->epi_x & 7)))
         return RNVP_E_UNSUPPORTED;
+    if (a->bp && a->pro_bn_relu) return RNVP_E_UNSUPPORTED;
     const bool k1 = a->cs_in <= 32;
-    if (a->n <= 16) return k1 ? launch_s1_ops<1, 1, 4>(a, s) : launch_s1_ops<1, 2, 4>(a, s);
-    if (a->n <= 32) return k1 ? launch_s1_ops<2, 1, 4>(a, s) : launch_s1_ops<2, 2, 4>(a, s);
-    return k1 ? launch_s1_ops<4, 1, 2>(a, s) : launch_s1_ops<4, 2, 2>(a, s);
+    if (a->bp) {   // the prologue's second operand stream: half-width tiles (registers)
+        if (a->n <= 16) return k1 ? launch_s1_bp<1, 1, 2>(a, s, dry) : launch_s1_bp<1, 2, 2>(a, s, dry);
+        if (a->n <= 32) return k1 ? launch_s1_bp<2, 1, 2>(a, s, dry) : launch_s1_bp<2, 2, 2>(a, s, dry);
+        return k1 ? launch_s1_bp<4, 1, 1>(a, s, dry) : launch_s1_bp<4, 2, 1>(a, s, dry);
+    }
+    if (a->n <= 16) return k1 ? launch_s1_ops<1, 1, 4>(a, s, dry) : launch_s1_ops<1, 2, 4>(a, s, dry);
+    if (a->n <= 32) return k1 ? launch_s1_ops<2, 1, 4>(a, s, dry) : launch_s1_ops<2, 2, 4>(a, s, dry);
+    return k1 ? launch_s1_ops<4, 1, 2>(a, s, dry) : launch_s1_ops<4, 2, 2>(a, s, dry);
 }

@@ -4,7 +4,7 @@
 
 #include "coupling_common.h"
 
-extern "C" int rnvp_version(void) { return 106; }
+extern "C" int rnvp_version(void) { return 107; }
 
 extern "C" int rnvp_struct_size(int which) {
     switch (which) {

@@ -42,7 +42,9 @@ class ConvArgs(C.Structure):
                 ("pro_bn_relu", i32), ("pro", BNSrc),
                 ("out_sums", vp),
                 ("epi_relu_bn_bwd", i32), ("epi_x", vp), ("epi", BNSrc), ("epi_sums", vp),
-                ("ws", vp), ("ws_elems", i64), ("variant", i32), ("w_frag", vp)]
+                ("ws", vp), ("ws_elems", i64), ("variant", i32), ("w_frag", vp),
+                ("bp", i32), ("bp_x", vp), ("bp_bn", BNSrc), ("bp_sums", vp), ("bp_shards", i32),
+                ("bp_out", vp), ("bp_dgamma", vp), ("bp_dbeta", vp)]
 
 
 class BNBwdArgs(C.Structure):
@@ -151,6 +153,7 @@ _SIGS = {
     "rnvp_bn_running_update": (i32, [vp, i32, i32, f32, vp]),
     "rnvp_stat_shards": (i32, [i64]),
     "rnvp_conv2d": (i32, [C.POINTER(ConvArgs), vp]),
+    "rnvp_conv2d_check": (i32, [C.POINTER(ConvArgs)]),
     "rnvp_wgrad_slabs": (i32, [i64]),
     "rnvp_wgrad_replicas": (i32, [i32]),
     "rnvp_conv2d_wgrad_grouped": (i32, [C.POINTER(WgradGroup), vp]),
@@ -198,7 +201,7 @@ class _Lib:
             fn.restype = res
             fn.argtypes = args
             raw = name in ("rnvp_version", "rnvp_struct_size", "rnvp_stat_shards", "rnvp_wgrad_slabs", "rnvp_wgrad_replicas",
-                           "rnvp_link_nclass",
+                           "rnvp_link_nclass", "rnvp_conv2d_check",
                            "rnvp_weight_norm_tiles", "rnvp_weight_norm_opt_blocks",
                            "rnvp_net_group_prepare") or res is not i32
             setattr(self, name[len("rnvp_"):], fn if raw else self._wrap(name, fn))

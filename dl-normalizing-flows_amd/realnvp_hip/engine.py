@@ -23,7 +23,7 @@ from ._lib import (BNBwdArgs, BNRunning, BNSrc, ConvArgs, CouplingArgs, NetStep,
 from .net import backward_program, build_program, chan_stride, round_up
 
 BN_EPS = 1e-5
-COUPLING_SHARDS = 32      # RNVP_COUPLING_SHARDS (include/realnvp_hip.h)
+COUPLING_SHARDS = 8       # RNVP_COUPLING_SHARDS (include/realnvp_hip.h; tests/test_boundary_cpu.py)
 BN_MOMENTUM = 0.1
 
 DTYPES = {"fp32": (RNVP_F32, 4, torch.float32), "bf16": (RNVP_BF16, 2, torch.bfloat16)}
@@ -34,6 +34,10 @@ CONV_VARIANT = 0
 # grouped launches of independent 1x1 convs (rnvp_net_group); False launches
 # them one by one (tests/test_gpu_group.py compares the two)
 NET_GROUP = True
+# BatchNorm-backward applies folded into their consumer's data-gradient
+# operand staging where the library supports it (rnvp_conv_args.bp, deep
+# scales); False keeps every apply a launch of its own (tests compare the two)
+FOLD_BN = True
 
 
 def stream_ptr():
@@ -420,6 +424,7 @@ class CouplingEngine:
             ar.add("g:" + b, M * chan_stride(ch) * esz)
         cmax = max([chan_stride(s.cin) for s in self.P.convs.values()])
         ar.add("gtmp", M * cmax * esz)
+        ar.add("gtmp2", M * cmax * esz)     # the other pre-apply temp of a folded BatchNorm backward
         ar.alloc(device, zero=True)
         # grouped weight-gradient partial sums: [nrep][cout][kp_f] (+ bias [nrep][cout])
         nz = int(_lib.lib().wgrad_slabs(M))
@@ -646,41 +651,34 @@ class CouplingEngine:
         # the net's data-gradient chain and grouped weight gradients: argument
         # structs cached per (saved arena, scratch, weight set); only the
         # BatchNorm-affine gradient pointers follow this call's grad block
-        key = (ws["key"], id(sc), bool(training))
+        key = (ws["key"], id(sc), bool(training), FOLD_BN)
         plan = sv.get("bwd_plan")
         if plan is None or plan[0] != key:
             plan = (key, self._bwd_args(T, sv, sc, ws, training))
             sv["bwd_plan"] = plan
         items, groups, wg_bytes, wg_flops = plan[1]
         if len(plan) < 3:
-            steps, rw = [], []
-            bsteps = [st for st in self.steps if st.kind != "wgrad"]
-            for (kind, c, nb, fl, bn), bst in zip(items, bsteps):
+            steps = []
+            for kind, c, nb, fl, bn, rw in items:
                 st = NetStep()
                 st.dgamma_off = st.dbeta_off = -1
-                op = bst.op
-                dst = bst.tmp if (kind == "dgrad" and bst.tmp) else bst.gx
-                reads = ({bst.residual} if bst.residual else set()) | ({dst} if bst.accumulate else set())
                 if kind == "dgrad":
                     st.kind = RNVP_STEP_CONV
                     st.conv = c
-                    reads |= {bst.gy} | ({op.x} if op.pro_bn else set())
-                    writes = {dst} | ({"e:" + op.pro_bn} if op.pro_bn else set())
                 else:
                     st.kind = RNVP_STEP_BN_BWD
                     st.bn = c
                     st.dgamma_off = self.layout[bn + "weight"][0]
                     st.dbeta_off = self.layout[bn + "bias"][0]
-                    reads |= {bst.tmp, op.x, "e:" + bn}
-                    writes = {dst}
                 steps.append(st)
-                rw.append((reads, writes))
-            plan = plan + (plan_launches(steps, x.device, rw),)
+            plan = plan + (plan_launches(steps, x.device, [it[5] for it in items]),)
             sv["bwd_plan"] = plan
         for g in plan[2]:
             if g[0] == "single":
-                kind, c, nb, fl, bn = items[g[1]]
+                kind, c, nb, fl, bn, _ = items[g[1]]
                 if kind == "dgrad":
+                    if bn is not None:      # folded BatchNorm backward: its parameter gradients
+                        c.bp_dgamma, c.bp_dbeta = gp(bn + "weight"), gp(bn + "bias")
                     _launch("conv_dgrad", nb, fl, L.conv2d, C.byref(c), s)
                 else:
                     c.dgamma, c.dbeta = gp(bn + "weight"), gp(bn + "bias")
@@ -737,8 +735,9 @@ class CouplingEngine:
     # --------------------------------------------------------------- backward
     def _bwd_args(self, T, sv, sc, ws, training):
         """(items, wgrad groups, wgrad bytes, wgrad flops) of the net backward:
-        items are ("dgrad", ConvArgs, bytes, flops, None) or ("bn", BNBwdArgs,
-        bytes, 0, bn name) in launch order; grouped weight gradients: one launch
+        items are ("dgrad", ConvArgs, bytes, flops, folded bn name or None, rw)
+        or ("bn", BNBwdArgs, bytes, 0, bn name, rw) in launch order, rw =
+        (buffers read, buffers written); grouped weight gradients: one launch
         per WGRAD_GROUP_MAX convs (the group travels as a by-value kernel
         argument); R >= 6 nets have more."""
         B, H, W, dtype = sv["B"], sv["H"], sv["W"], sv["dtype"]
@@ -747,6 +746,7 @@ class CouplingEngine:
         esz = DTYPES[dtype][1]
         ar, sar, war = sv["arena"], sc["arena"], ws["arena"]
         items, groups = [], []
+        ent = []        # [kind, args, bytes, flops, bn, reads, writes, BwdStep, tmp name]
         wg_bytes = wg_flops = 0.0
         wbase = sc["wg_ws"].data_ptr()
         for st in self.steps:
@@ -773,7 +773,12 @@ class CouplingEngine:
                 c.variant = CONV_VARIANT
                 nb = esz * (M * cs_out + spec.cin * kp_d + M * cs_in * (1 + int(bool(op.pro_bn)) + int(bool(
                     st.residual)) + int(st.accumulate)))
-                items.append(("dgrad", c, nb, 2.0 * M * spec.cout * spec.ks * spec.ks * spec.cin, None))
+                dst = st.tmp if st.tmp else st.gx
+                reads = {st.gy} | ({op.x} if op.pro_bn else set()) | ({st.residual} if st.residual else set()) | (
+                    {dst} if st.accumulate else set())
+                writes = {dst} | ({"e:" + op.pro_bn} if op.pro_bn else set())
+                ent.append(["dgrad", c, nb, 2.0 * M * spec.cout * spec.ks * spec.ks * spec.cin, None, reads, writes, st,
+                            st.tmp])
             elif st.kind == "bn_apply":
                 bn = op.pro_bn
                 c = BNBwdArgs()
@@ -785,7 +790,10 @@ class CouplingEngine:
                 c.dx = sar.ptr(st.gx)
                 c.residual = sar.ptr(st.residual) if st.residual else None
                 c.accumulate = int(st.accumulate)
-                items.append(("bn", c, esz * M * cs_in * (3 + int(bool(st.residual)) + int(st.accumulate)), 0.0, bn))
+                reads = {st.tmp, op.x, "e:" + bn} | ({st.residual} if st.residual else set()) | (
+                    {st.gx} if st.accumulate else set())
+                ent.append(["bn", c, esz * M * cs_in * (3 + int(bool(st.residual)) + int(st.accumulate)), 0.0, bn,
+                            reads, {st.gx}, st, st.tmp])
             else:
                 if not groups or groups[-1].n_conv >= WGRAD_GROUP_MAX:
                     grp = WgradGroup()
@@ -804,7 +812,57 @@ class CouplingEngine:
                 c.wsb = wbase + 4 * ob if ob is not None else None
                 wg_bytes += esz * (M * cs_in + M * cs_out) + 4 * sc["wg_nz"] * spec.cout * spec.ks * spec.ks * cs_in
                 wg_flops += 2.0 * M * spec.cout * spec.ks * spec.ks * spec.cin
+        if FOLD_BN and training:
+            self._fold_bn(ent, sar, esz * M)
+        items = [(e[0], e[1], e[2], e[3], e[4], (e[5], e[6])) for e in ent if e[0] != "folded"]
         return items, groups, wg_bytes, wg_flops
+
+    @staticmethod
+    def _fold_bn(ent, sar, m_bytes):
+        """Fold each BatchNorm-backward apply whose only data-gradient reader
+        is the very next conv (a plain write: no accumulation, no residual)
+        into that conv's operand staging (rnvp_conv_args.bp) where the library
+        supports it (rnvp_conv2d_check).  The conv reads the apply's input
+        temp and the BatchNorm input instead of the applied gradient, stores
+        the applied gradient as a side output (the weight gradient reads it)
+        and writes the BatchNorm's parameter gradients; its own pre-apply
+        output moves to the other temp (gtmp / gtmp2) when it would overwrite
+        the one it reads."""
+        L = _lib.lib()
+        other = {"gtmp": "gtmp2", "gtmp2": "gtmp"}
+        for i in range(len(ent) - 1):
+            e, d = ent[i], ent[i + 1]
+            if e[0] != "bn" or d[0] != "dgrad" or e[7].accumulate or e[7].residual or d[7].gy != e[7].gx:
+                continue
+            if any(e[7].gx in ent[k][5] for k in range(i + 2, len(ent))):
+                continue    # more data-gradient readers (the skip convs of d out): they stay grouped
+            b, c = e[1], d[1]
+            tin = e[8]
+            assert b.g == sar.ptr(tin)
+            retarget = d[8] is not None and d[8] == tin
+            if retarget:
+                nxt = ent[i + 2]
+                assert nxt[0] == "bn" and nxt[7].op is d[7].op and nxt[8] == tin
+            old_x, old_y = c.x, c.y
+            c.bp, c.bp_x, c.bp_bn, c.bp_sums, c.bp_shards = 1, b.x, b.bn, b.sums, b.sum_shards
+            c.bp_out, c.x = old_x, b.g
+            if retarget:
+                c.y = sar.ptr(other[tin])
+            if L.conv2d_check(C.byref(c)) != 0:
+                c.bp, c.bp_x, c.bp_sums, c.bp_out, c.x, c.y = 0, None, None, None, old_x, old_y
+                continue
+            if retarget:
+                tn = other[tin]
+                nxt[1].g = sar.ptr(tn)
+                nxt[5] = (nxt[5] - {tin}) | {tn}
+                nxt[8] = tn
+                d[6] = (d[6] - {tin}) | {tn}
+                d[8] = tn
+            d[4] = e[4]
+            d[5] = (d[5] - {e[7].gx}) | {tin} | (e[5] - {tin})
+            d[6] = d[6] | {e[7].gx}
+            d[2] += 2 * m_bytes * c.cs_in
+            e[0] = "folded"
 
     def backward(self, sv, gz, gl_full, gl_sample, grad_block, gx=None, side=None, after=None, zero_at_end=False,
                  defer=None, opt=None):

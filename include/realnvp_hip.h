@@ -155,8 +155,26 @@ typedef struct rnvp_conv_args {
      * 16 rows with zeros).  The bf16 3x3 deep-scale kernels read it instead of
      * w: each weight load of a wave is one contiguous KiB in MFMA lane order. */
     const void* w_frag;
+    /* optional BatchNorm-backward prologue (bp = 1; data-gradient convs of
+     * the deep family only, see rnvp_conv2d_check): x is the gradient g of
+     * BatchNorm bp_bn's OUTPUT (the producing dgrad's relu/BN epilogue
+     * output), bp_x that BatchNorm's saved input t (both [M][cs_in]), and the
+     * conv's operand is dL/dt = gamma rstd (g - k1 - xhat k2) with
+     * k1 = sum g / count, k2 = sum g xhat / count from bp_sums (the producing
+     * epilogue's epi_sums, bp_shards shards <= 2) -- rnvp_bn_bwd_apply's
+     * formula, formed while the operand tile is staged, so that apply's
+     * launch and its dL/dt round trip disappear.  Workgroups of output
+     * channel tile 0 store dL/dt to bp_out ([M][cs_in], for the weight
+     * gradient); workgroup 0 writes bp_dbeta[c] = sum g and bp_dgamma[c] =
+     * sum g xhat (BatchNorm2d's parameter gradients, modules_realnvp.py:36-52). */
+    int bp; const void* bp_x; rnvp_bn_src bp_bn; const double* bp_sums; int bp_shards;
+    void* bp_out; float* bp_dgamma; float* bp_dbeta;
 } rnvp_conv_args;
 int rnvp_conv2d(const rnvp_conv_args* a, void* stream);
+/* RNVP_OK when rnvp_conv2d(a) would launch (argument checks and the
+ * dispatch's own support limits, nothing launched): the host uses it to
+ * decide which BatchNorm-backward applies fold into their consumer (bp). */
+int rnvp_conv2d_check(const rnvp_conv_args* a);
 
 /* grouped weight gradient: the wgrads of every conv of one coupling's s/t
  * network in ONE launch (they are independent of each other once the

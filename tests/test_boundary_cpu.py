@@ -91,6 +91,47 @@ def test_link_arguments_checked_without_launch():
     assert L.dll.rnvp_coupling_out_u(ctypes.byref(a), None) == -1
 
 
+def test_bn_fold_support_query_without_launch():
+    """rnvp_conv2d_check answers the engine's fold question on the host: a
+    BatchNorm-backward prologue (bp) runs on the deep family's data-gradient
+    tiles and the wide scales' streaming 1x1 -- accepted where it pays,
+    refused (UNSUPPORTED) for the band 3x3, the 4-wave 1x1 tiles or a forced
+    non-deep variant, INVALID without the
+    BatchNorm input; the coupling shard count mirrors the header's."""
+    from realnvp_hip import _lib, engine
+    L = _lib._Lib()
+    hdr = open(os.path.join(ROOT, "include", "realnvp_hip.h")).read()
+    assert int(re.search(r"#define RNVP_COUPLING_SHARDS (\d+)", hdr).group(1)) == engine.COUPLING_SHARDS
+    buf = (ctypes.c_double * 64)()
+    p = ctypes.addressof(buf)
+
+    def args(B, S, c, ks, bp=1, bp_x=True, variant=0, epi=False):
+        a = _lib.ConvArgs()
+        a.dtype, a.B, a.H, a.W, a.ks = 1, B, S, S, ks
+        a.x, a.cs_in, a.cin, a.w, a.kp = p, c, c, p, (ks * ks * c + 63) // 64 * 64
+        a.y, a.cs_out, a.n = p, c, c
+        a.variant = variant
+        a.bp, a.bp_x, a.bp_sums, a.bp_shards = bp, p if bp_x else None, p, 1
+        a.bp_bn = _lib.BNSrc(p, float(B * S * S), None, None, None, None, 1e-5, 1)
+        if epi:   # the data gradient's ReLU/BN epilogue
+            a.epi_relu_bn_bwd, a.epi_x, a.epi_sums = 1, p, p
+            a.epi = _lib.BNSrc(p, float(B * S * S), None, None, None, None, 1e-5, 1)
+        return a
+    ok = [args(64, 4, 512, 1), args(64, 4, 512, 3), args(64, 8, 256, 3), args(64, 16, 128, 3),
+          args(64, 16, 128, 1, variant=16)]          # a forced 4-wave 1x1 tile (RNVP_VARIANT_DEEP0)
+    for a in ok:
+        assert L.conv2d_check(ctypes.byref(a)) == 0
+    # the tuned dispatch keeps the apply before 4-wave 1x1 tiles (measured slower folded)
+    assert L.conv2d_check(ctypes.byref(args(64, 16, 128, 1))) == -2
+    # wide scales: the streaming 1x1 (bf16) folds a data gradient with the ReLU/BN epilogue
+    assert L.conv2d_check(ctypes.byref(args(64, 32, 64, 1, epi=True))) == 0
+    assert L.conv2d_check(ctypes.byref(args(64, 32, 64, 1))) == -2
+    assert L.conv2d_check(ctypes.byref(args(64, 32, 64, 3, epi=True))) == -2   # the band 3x3 has no prologue
+    assert L.conv2d_check(ctypes.byref(args(64, 8, 256, 3, variant=1))) == -2
+    assert L.conv2d_check(ctypes.byref(args(64, 8, 256, 3, bp_x=False))) == -1
+    assert L.conv2d_check(ctypes.byref(args(64, 32, 64, 1, bp=0))) == 0
+
+
 def _hp(bd, rb, bott=True, skip=True, wn=True, cbn=True):
     import utils
     return utils.Hyperparameters(bd, rb, bott, skip, wn, cbn)

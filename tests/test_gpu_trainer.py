@@ -189,7 +189,10 @@ def test_process_group_step_matches_single_process(nccl_world1, comm, graph, sid
     assert float((tr.param - ref.param).abs().max()) <= 2 * ref.lr * 1.01
     assert d(tr.param, ref.param) < max(1e-5, 4 * d(ref2.param, ref.param))
     assert int(tr.step_t.item()) == 1
-    np.testing.assert_allclose(tr.mean_logll(1), ref.mean_logll(1), rtol=1e-6)
+    # the linked forward adds each coupling's per-sample log-det with fp32
+    # atomics (their order varies run to run): the identical-run spread, 1e-5 floor
+    ll, ll2 = ref.mean_logll(1), ref2.mean_logll(1)
+    np.testing.assert_allclose(tr.mean_logll(1), ll, rtol=max(1e-5, 4 * abs(ll2 - ll) / abs(ll)))
 
 
 def test_capture_issues_no_eager_collective(nccl_world1, monkeypatch):

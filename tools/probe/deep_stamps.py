@@ -21,7 +21,7 @@ lib.probe_deep.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
 PH = ["tab+stage ld", "ring+act st", "k-loop", "reduce+epi", "stats", ]
 
 
-def case(name, B, H, W, cin, cout, ks, cfg, pro=False, stats=False, residual=False, acc=False, dgrad=False):
+def case(name, B, H, W, cin, cout, ks, cfg, pro=False, stats=False, residual=False, acc=False, dgrad=False, bp=False):
     dev = "cuda"
     M = B * H * W
     csi, cso = chan_stride(cin), chan_stride(cout)
@@ -54,6 +54,13 @@ def case(name, B, H, W, cin, cout, ks, cfg, pro=False, stats=False, residual=Fal
         a.epi_x = r.data_ptr()
         a.epi = BNSrc(sums_in.data_ptr(), float(M), None, None, gam.data_ptr(), bet.data_ptr(), 1e-5, sh)
         a.epi_sums = sums_out.data_ptr()
+    if bp:   # BatchNorm-backward prologue (rnvp_conv_args.bp): x is the pre-apply gradient
+        t = torch.randn(M, csi, device=dev).to(torch.bfloat16)
+        side = torch.zeros(M, csi, device=dev).to(torch.bfloat16)
+        dgb = torch.zeros(2, cin, device=dev)
+        a.bp, a.bp_x, a.bp_sums, a.bp_shards = 1, t.data_ptr(), sums_in.data_ptr(), sh
+        a.bp_bn = BNSrc(sums_in.data_ptr(), float(M), None, None, gam.data_ptr(), bet.data_ptr(), 1e-5, sh)
+        a.bp_out, a.bp_dgamma, a.bp_dbeta = side.data_ptr(), dgb[0].data_ptr(), dgb[1].data_ptr()
     st = torch.zeros(8192 * 8, dtype=torch.int64, device=dev)
     s = torch.cuda.current_stream().cuda_stream
     for _ in range(5):
@@ -82,7 +89,24 @@ CASES = [
     ("s3 3x3 pro+stats", 64, 16, 16, 128, 128, 3, dict(pro=True, stats=True)),
 ]
 
+BP_CASES = [
+    ("s5 1x1 dgrad", 64, 4, 4, 512, 512, 1, dict(dgrad=True)),
+    ("s5 1x1 dgrad+bp", 64, 4, 4, 512, 512, 1, dict(dgrad=True, bp=True)),
+    ("s5 3x3 dgrad", 64, 4, 4, 512, 512, 3, dict(dgrad=True)),
+    ("s5 3x3 dgrad+bp", 64, 4, 4, 512, 512, 3, dict(dgrad=True, bp=True)),
+    ("s4 3x3 dgrad", 64, 8, 8, 256, 256, 3, dict(dgrad=True)),
+    ("s4 3x3 dgrad+bp", 64, 8, 8, 256, 256, 3, dict(dgrad=True, bp=True)),
+    ("s3 3x3 dgrad", 64, 16, 16, 128, 128, 3, dict(dgrad=True)),
+    ("s3 3x3 dgrad+bp", 64, 16, 16, 128, 128, 3, dict(dgrad=True, bp=True)),
+    ("s3 1x1 dgrad", 64, 16, 16, 128, 128, 1, dict(dgrad=True)),
+    ("s3 1x1 dgrad+bp", 64, 16, 16, 128, 128, 1, dict(dgrad=True, bp=True)),
+]
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "bp":
+        for name, B, H, W, ci, co, ks, fl in BP_CASES:
+            case(name, B, H, W, ci, co, ks, 4 if B * H * W <= 1024 else 0, **fl)
+        sys.exit(0)
     for name, B, H, W, ci, co, ks, fl in CASES:
         for cfg in (0, 1, 2, 3, 4, 5):
             try:
