@@ -231,15 +231,28 @@ class CouplingEngine:
             self.layout[n] = (off, p.numel())
             off += p.numel()
         self.n_params = off
+        # (name, the owning module's _parameters / _buffers dict, key) of every
+        # parameter and buffer, walked once: the per-call lookups are plain
+        # dict reads (named_parameters() / named_buffers() recursed the module
+        # tree on every call: ~30 % of the drop-in loop's host time)
+        self._pslots = [(pre + ("." if pre else "") + k, m._parameters, k)
+                        for pre, m in mod.named_modules() for k, v in m._parameters.items() if v is not None]
+        self._bslots = [(pre + ("." if pre else "") + k, m._buffers, k)
+                        for pre, m in mod.named_modules() for k, v in m._buffers.items() if v is not None]
+        assert [n for n, _, _ in self._pslots] == list(self.layout), "parameter walk order"
         self._weights = {}
         self._scratch = {}
         self._saved_pool = {}
 
     # ------------------------------------------------------------------ params
     def _tensors(self):
-        d = dict(self.mod.named_parameters())
-        d.update(dict(self.mod.named_buffers()))
+        d = {n: dd[k] for n, dd, k in self._pslots}
+        d.update({n: dd[k] for n, dd, k in self._bslots})
         return d
+
+    def params(self):
+        """the module's parameters in named_parameters() order (as _tensors)"""
+        return [dd[k] for _, dd, k in self._pslots]
 
     def _conv_names(self, spec):
         p = spec.name + "conv."

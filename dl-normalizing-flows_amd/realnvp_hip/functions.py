@@ -54,12 +54,8 @@ class _Coupling(torch.autograd.Function):
         grad_block = torch.zeros(eng.n_params, device=x.device, dtype=torch.float32)
         gx = eng.backward(sv, gz, gl if ctx.full else None, None if ctx.full else gl, grad_block)
         grads = []
-        for n, p in eng.mod.named_parameters():
-            if p.requires_grad:
-                off, cnt = eng.layout[n]
-                grads.append(grad_block[off:off + cnt].view_as(p))
-            else:
-                grads.append(None)
+        for (off, cnt), p in zip(eng.layout.values(), eng.params()):
+            grads.append(grad_block[off:off + cnt].view_as(p) if p.requires_grad else None)
         ctx.sv = None
         eng.release(sv)
         return (gx, None, None, None, None) + tuple(grads)
@@ -70,7 +66,7 @@ def coupling_apply(mod, x, full_ldj):
     per-sample sum [B]."""
     _check_device(x, type(mod).__name__)
     x = x.contiguous()
-    params = tuple(mod.parameters())
+    params = tuple(mod.engine().params())
     return _Coupling.apply(x, mod, mod.training, mod.compute_dtype, full_ldj, *params)
 
 

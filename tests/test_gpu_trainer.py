@@ -452,7 +452,9 @@ def test_checkpoint_carries_the_noise_stream():
         t.reset_metrics()
         t.step()
     torch.cuda.synchronize()
-    np.testing.assert_allclose(tb.mean_logll(1), ta.mean_logll(1), rtol=1e-6)
+    # (1e-5: the linked forward adds the per-sample log-det with fp32 atomics,
+    # whose order varies run to run -- measured up to 1.6e-6 between identical steps)
+    np.testing.assert_allclose(tb.mean_logll(1), ta.mean_logll(1), rtol=1e-5)
     assert torch.equal(tb.xl, ta.xl)    # the same noise was drawn
     assert float((tb.param - ta.param).abs().max()) <= 2 * ta.lr * 1.01
 

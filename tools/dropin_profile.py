@@ -2,7 +2,9 @@
 loss.backward(), torch.optim.Adam): host time of each call vs device time of
 each phase, fp32 and bf16, config 1 (64x64x3, R4, D32, B=64).
 
-    python3 tools/dropin_profile.py [steps]
+    python3 tools/dropin_profile.py [steps] [fused]
+
+"fused": realnvp_hip.FusedAdam in place of torch.optim.Adam (train.py:134 changed).
 """
 import os
 import sys
@@ -26,7 +28,11 @@ def main():
         model = build_model(64, 4, 32, 5, dev, 0)
         model.set_precision(dtype)
         model.train()
-        opt = torch.optim.Adam(model.parameters(), lr=5e-4, weight_decay=5e-5)
+        if len(sys.argv) > 2 and sys.argv[2] == "fused":
+            import realnvp_hip
+            opt = realnvp_hip.FusedAdam(model.parameters(), lr=5e-4, weight_decay=5e-5)
+        else:
+            opt = torch.optim.Adam(model.parameters(), lr=5e-4, weight_decay=5e-5)
         ev = {k: [torch.cuda.Event(enable_timing=True) for _ in range(2)] for k in ("fwd", "bwd", "opt")}
         host = {k: 0.0 for k in ("fwd", "bwd", "opt")}
         dev_t = {k: 0.0 for k in ("fwd", "bwd", "opt")}
