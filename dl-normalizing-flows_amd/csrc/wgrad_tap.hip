@@ -29,6 +29,17 @@
 
 namespace {
 
+// compile-time loop: f(std::integral_constant<int, i>) for i = 0 .. N-1
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for_impl(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for_impl<I + 1, N>(f);
+    }
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) { static_for_impl<0, N>(f); }
+
 constexpr int WT_NT = 512;     // 8 waves
 #ifndef WT_C0_DEPTH
 #define WT_C0_DEPTH 1   // 2 (per-tap B fragments, a second stage in flight) measured slower: profiles/r3_experiments.txt
@@ -44,8 +55,14 @@ template <int C> struct WtCfg;
 // 3x3 class, spent on a second stage of global loads in flight)
 template <> struct WtCfg<0> { static constexpr int TCO = 64, TCI = 64, KS = 3, WCO = 2, WCI = 4, WTG = 1, NX = 5, DEPTH = WT_C0_DEPTH, BALL = WT_C0_DEPTH == 1; };
 template <> struct WtCfg<1> { static constexpr int TCO = 128, TCI = 128, KS = 1, WCO = 2, WCI = 4, WTG = 1, NX = 4, DEPTH = 1, BALL = 1; };
-template <> struct WtCfg<2> { static constexpr int TCO = 32, TCI = 32, KS = 3, WCO = 2, WCI = 2, WTG = 2, NX = 4, DEPTH = 2, BALL = 1; };
-template <> struct WtCfg<3> { static constexpr int TCO = 64, TCI = 64, KS = 1, WCO = 2, WCI = 4, WTG = 1, NX = 2, DEPTH = 2, BALL = 1; };
+#ifndef WT_SMALL_DEPTH
+// stages of loads in flight for the wide scales' 32 / 64-channel classes (3
+// measured no step change: 19.60 vs 19.58 ms, gpurun_out/r6_wgd3 -- the stage
+// loop is not load-latency bound)
+#define WT_SMALL_DEPTH 2
+#endif
+template <> struct WtCfg<2> { static constexpr int TCO = 32, TCI = 32, KS = 3, WCO = 2, WCI = 2, WTG = 2, NX = 4, DEPTH = WT_SMALL_DEPTH, BALL = 1; };
+template <> struct WtCfg<3> { static constexpr int TCO = 64, TCI = 64, KS = 1, WCO = 2, WCI = 4, WTG = 1, NX = 2, DEPTH = WT_SMALL_DEPTH, BALL = 1; };
 
 inline int wt_class_base(int ks, int cs_in, int cs_dy) {
     if (ks == 3) return (cs_in <= 32 && cs_dy <= 32) ? 2 : 0;
@@ -397,9 +414,10 @@ __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int 
     // stage pipeline: DEPTH stages of global loads in flight (register slots
     // s % DEPTH), LDS double buffer (s & 1), one barrier per stage
     using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, DEPTH - 1>;
-    if (ns > 0) gload(0, I0{});
-    if (DEPTH == 2 && ns > 1) gload(1, I1{});
+    static_for<DEPTH>([&](auto D) {
+        constexpr int d = decltype(D)::value;
+        if (d < ns) gload(d, D);
+    });
     if (ns > 0) lstore(0, I0{});
     __syncthreads();
     auto iter = [&](int s, auto SLC) {
@@ -411,8 +429,10 @@ __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int 
         __syncthreads();
     };
     for (int s = 0; s < ns; s += DEPTH) {
-        iter(s, I0{});
-        if (DEPTH == 2 && s + 1 < ns) iter(s + 1, I1{});
+        static_for<DEPTH>([&](auto D) {
+            constexpr int d = decltype(D)::value;
+            if (s + d < ns) iter(s + d, D);
+        });
     }
 
     // ---- epilogue: D rows = co, cols = ci; k = tap * cs_in + ci ----
