@@ -1872,9 +1872,11 @@ int conv_args_status(const rnvp_conv_args* a) {
 // the configuration a BatchNorm-backward prologue runs on: the deep family's
 // data-gradient tiles only (the other families have no such prologue).  The
 // tuned dispatch folds where that measured faster than the apply's launch +
-// the plain conv (tools/probe/deep_stamps.py bp): the 3x3 tiles and the
-// 8-wave tiles; the 4-wave 1x1 tiles (M > 1024) lose waves per SIMD to the
-// prologue's registers (a forced deep configuration still runs it)
+// the plain conv (tools/probe/deep_stamps.py bp / bp8, profiles/r6_bnfold.txt):
+// the 3x3 tiles, the 8-wave tiles and the 4-wave 1x1 tiles up to 4096 pixels
+// (+2.8 us against a ~5.7 us apply); at 16384 pixels the 4-wave 1x1 tile loses
+// a wave per SIMD to the prologue's registers (+7.8 us) and keeps the apply (a
+// forced deep configuration still runs it)
 int bp_cfg_of(const rnvp_conv_args* a) {
     if (a->variant >= RNVP_VARIANT_DEEP0) {
         const int cfg = a->variant - RNVP_VARIANT_DEEP0;
@@ -1882,7 +1884,8 @@ int bp_cfg_of(const rnvp_conv_args* a) {
     }
     if (a->variant != 0 && a->variant != RNVP_VARIANT_DEEP) return -1;
     const int cfg = rnvp_deep_auto_cfg(a);
-    if (cfg == 4 || (cfg == 0 && a->ks == 3)) return cfg;
+    const long long M = (long long)a->B * a->H * a->W;
+    if (cfg == 4 || (cfg == 0 && (a->ks == 3 || M <= 4096))) return cfg;
     return -1;
 }
 

@@ -23,7 +23,7 @@ from ._lib import (BNBwdArgs, BNRunning, BNSrc, ConvArgs, CouplingArgs, NetStep,
 from .net import backward_program, build_program, chan_stride, round_up
 
 BN_EPS = 1e-5
-COUPLING_SHARDS = 8       # RNVP_COUPLING_SHARDS (include/realnvp_hip.h; tests/test_boundary_cpu.py)
+COUPLING_SHARDS = 16      # RNVP_COUPLING_SHARDS (include/realnvp_hip.h; tests/test_boundary_cpu.py)
 BN_MOMENTUM = 0.1
 
 DTYPES = {"fp32": (RNVP_F32, 4, torch.float32), "bf16": (RNVP_BF16, 2, torch.bfloat16)}

@@ -310,7 +310,9 @@ int rnvp_adam_gather(const rnvp_adam_args* adam, const long long* idx, long long
  * st = [shift | log_rescale] (2*Cb channels). */
 /* the coupling's per-channel fp64 reductions are spread over this many
  * shards (workgroup % shards) so no word takes more than ~32 atomic adders */
-#define RNVP_COUPLING_SHARDS 8
+#ifndef RNVP_COUPLING_SHARDS
+#define RNVP_COUPLING_SHARDS 16
+#endif
 typedef struct rnvp_coupling_args {
     int kind, B, C, H, W, mask_config, coupling_bn, training, dtype;
     float momentum, eps;

@@ -117,11 +117,11 @@ def test_bn_fold_support_query_without_launch():
             a.epi_relu_bn_bwd, a.epi_x, a.epi_sums = 1, p, p
             a.epi = _lib.BNSrc(p, float(B * S * S), None, None, None, None, 1e-5, 1)
         return a
-    ok = [args(64, 4, 512, 1), args(64, 4, 512, 3), args(64, 8, 256, 3), args(64, 16, 128, 3),
+    ok = [args(64, 4, 512, 1), args(64, 4, 512, 3), args(64, 8, 256, 3), args(64, 8, 256, 1), args(64, 16, 128, 3),
           args(64, 16, 128, 1, variant=16)]          # a forced 4-wave 1x1 tile (RNVP_VARIANT_DEEP0)
     for a in ok:
         assert L.conv2d_check(ctypes.byref(a)) == 0
-    # the tuned dispatch keeps the apply before 4-wave 1x1 tiles (measured slower folded)
+    # the tuned dispatch keeps the apply before the 16384-pixel 1x1 tiles (measured slower folded)
     assert L.conv2d_check(ctypes.byref(args(64, 16, 128, 1))) == -2
     # wide scales: the streaming 1x1 (bf16) folds a data gradient with the ReLU/BN epilogue
     assert L.conv2d_check(ctypes.byref(args(64, 32, 64, 1, epi=True))) == 0

@@ -198,8 +198,8 @@ def test_coupling_fold_matches_unfolded(case, dtype):
     r1, a1, f1 = _run(case, dtype, True)
     assert f0 == 0 and a1 == a0 - f1, (a0, a1, f1)
     # per residual block (4), deep scales: res_block.4 into the 3x3's data
-    # gradient, and res_block.1 into the first 1x1's where that is an 8-wave tile (M <= 1024;
-    # the tuned dispatch keeps the apply before 4-wave 1x1 tiles); fp32 3x3
+    # gradient, and res_block.1 into the first 1x1's up to 4096 pixels (the
+    # tuned dispatch keeps the apply before the 16384-pixel 1x1 tiles); fp32 3x3
     # tiles at 512 channels exceed the LDS with the fold's table
     _, _, _, mid, size, B = case
     M = B * size * size
@@ -207,7 +207,7 @@ def test_coupling_fold_matches_unfolded(case, dtype):
     if M > 16384:   # wide: res_block.1 into the streaming 1x1 (bf16 only)
         want = 4 if dtype == "bf16" else 0
     else:
-        want = 4 * (int(small) + int(not (small and dtype == "fp32")))
+        want = 4 * (int(M <= 4096) + int(not (small and dtype == "fp32")))
     assert f1 == want, (f1, want)
     y0, l0, gx0, g0 = r0
     y1, l1, gx1, g1 = r1
