@@ -1899,8 +1899,10 @@ extern "C" int rnvp_conv2d(const rnvp_conv_args* a, void* stream) {
     if (a->bp) {
         const int cfg = bp_cfg_of(a);
         if (cfg >= 0) return rnvp_deep_launch(a, s, cfg);
-        // the wide scales' streaming 1x1 (bf16) has the prologue too
-        return a->variant == 0 ? rnvp_conv_s1_launch(a, s) : RNVP_E_UNSUPPORTED;
+        // the wide scales' streaming 1x1 and band 3x3 (bf16) have the prologue too
+        if (a->variant != 0) return RNVP_E_UNSUPPORTED;
+        const int r = rnvp_conv_s1_launch(a, s);
+        return r != RNVP_E_UNSUPPORTED ? r : rnvp_conv_band2_launch(a, s);
     }
     return a->dtype == RNVP_F32 ? dispatch_conv<float>(a, s) : dispatch_conv<bf16_t>(a, s);
 }
@@ -1911,7 +1913,9 @@ extern "C" int rnvp_conv2d_check(const rnvp_conv_args* a) {
     if (a->bp) {
         const int cfg = bp_cfg_of(a);
         if (cfg >= 0) return rnvp_deep_launch(a, nullptr, cfg, true);
-        return a->variant == 0 ? rnvp_conv_s1_launch(a, nullptr, true) : RNVP_E_UNSUPPORTED;
+        if (a->variant != 0) return RNVP_E_UNSUPPORTED;
+        const int r = rnvp_conv_s1_launch(a, nullptr, true);
+        return r != RNVP_E_UNSUPPORTED ? r : rnvp_conv_band2_launch(a, nullptr, true);
     }
     return RNVP_OK;   // the dispatch has a family for every shape that passes the checks
 }

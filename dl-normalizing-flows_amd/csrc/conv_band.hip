@@ -95,7 +95,12 @@ template <> struct Raw4<float> {
 // its pixels; 2: wave pairs split them).  WREG: the wave's weight fragments
 // of every k-step in registers (read from LDS once per workgroup), so the
 // k-loop reads only activation fragments from LDS.
-template <typename T, int NT, int TM, int CS, int HF, bool WREG, bool PRO, int NOPS>
+// BP: the BatchNorm-backward prologue of a data gradient (rnvp_conv_args.bp,
+// conv_deep.h's form): x is the pre-apply gradient g, bp_x the BatchNorm input
+// t; each staged chunk becomes dL/dt = A g - (B t + C) (coefficients from
+// LDS), and a band's own rows (not its halo) are stored once to bp_out.  Half
+// the staged chunks per thread per operand (the launcher checks the rows fit)
+template <typename T, int NT, int TM, int CS, int HF, bool WREG, bool PRO, int NOPS, bool BP = false>
 __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards, int per) {
     using RT = typename Raw4<T>::type;
     using G = BandGeo<T, NT, TM, HF>;
@@ -105,7 +110,8 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
     constexpr int KPL = lds_mfma_pitch(NSTEP * KS, CH);
     constexpr int NTW = NT / HF;                // channel tiles per wave
     constexpr int NTH = 512;
-    constexpr int SB = 8;                       // staged 16-B chunks per thread per band (checked by the launcher)
+    static_assert(!(BP && PRO), "BatchNorm-backward prologue: data gradients only");
+    constexpr int SB = BP ? 4 : 8;              // staged 16-B chunks per thread per band (checked by the launcher)
     constexpr int WB = 10;                      // weight chunks per thread (launcher: NC * kpl / CH <= WB * NTH)
     static_assert(NT % HF == 0 && (HF == 1 || HF == 2), "channel groups");
     extern __shared__ double dsm[];
@@ -140,6 +146,10 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
     const int cfix = tid % cpr, rbase = tid / cpr;
     constexpr int rstep = NTH / cpr;
     u32x4 sv[SB];
+    u32x4 sx[BP ? SB : 1];
+    const T* __restrict__ XT = (const T*)a.bp_x;
+    T* __restrict__ BPO = (T*)a.bp_out;
+    const float* ctab = (const float*)tmp;      // BP: C [cs] (the table scratch, after the tables)
     auto stage_load = [&](int band) {
         const int m0 = band * BM;
 #pragma unroll
@@ -148,7 +158,9 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
             const int r = rbase + u * rstep;
             const int p = m0 - hal + r;
             const bool ok = (r < R) & (p >= 0) & (p < M);
-            sv[u] = *(const u32x4*)(X + (ok ? (long long)p * cs + cfix * CH : 0));
+            const long long o = ok ? (long long)p * cs + cfix * CH : 0;
+            sv[u] = *(const u32x4*)(X + o);
+            if constexpr (BP) sx[u] = *(const u32x4*)(XT + o);
         }
     };
     float scv[CH], shv[CH];
@@ -161,6 +173,19 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
             if (r >= R) continue;
             const int p = m0 - hal + r;
             u32x4 w = sv[u];
+            if constexpr (BP) {
+                float gv[CH], tv[CH], d[CH];
+                unpack(w, gv, T());
+                unpack(sx[u], tv, T());
+#pragma unroll
+                for (int e = 0; e < CH; ++e) {
+                    const int c = cfix * CH + e;
+                    d[e] = fmaf(bnp[c], gv[e], -fmaf(bnp[cs + c], tv[e], ctab[c]));
+                }
+                w = pack(d, T());
+                // the band's own rows, once (the halo rows are a neighbour band's)
+                if (BPO && r >= hal && r < hal + BM && p < M) *(u32x4*)(BPO + (long long)p * cs + cfix * CH) = w;
+            }
             if (PRO) {
                 if constexpr (sizeof(T) == 2) {
                     w = bn_relu_bf16x8(w, scv, shv);
@@ -187,6 +212,13 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
     const bool epi_pre = epi_bn && a.epi.sums && shard_fits(min(NC, N), a.epi.shards, 2);
     if (pro_pre) shard_issue<2>(a.pro.sums, a.cin, a.pro.shards, 0, pnv, pro_l);
     if (epi_pre) shard_issue<2>(a.epi.sums, N, a.epi.shards, 0, min(NC, N), epi_l);
+    // BP: the BatchNorm's statistics and the gradient sums (launcher: both fit shard_issue<2>)
+    ShardLoads<BP ? 2 : 1> bpb_l, bpg_l;
+    if constexpr (BP) {
+        shard_issue<2>(a.bp_bn.sums, a.cin, a.bp_bn.shards, 0, pnv, bpb_l);
+        shard_issue<2>(a.bp_sums, a.cin, a.bp_shards, 0, pnv, bpg_l);
+    }
+    const BnAff bp_a = BP ? bn_aff_issue(a.bp_bn, a.cin, 0, a.w) : BnAff{1.f, 0.f};
     // the tables' affine parameters and the bias, in the same batch (no
     // global round trip left between the reductions and the first band)
     static_assert(NC <= NTH, "one table channel per thread");
@@ -219,6 +251,36 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
             block_bn_finish_aff(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp, epi_a);
         } else {
             block_bn_table(a.epi, N, 0, NC, etab, etab + NC, etab + 2 * NC, etab + 3 * NC, tmp);
+        }
+    }
+    if constexpr (BP) {
+        // A | B -> bnp, C -> the table scratch (read by stage_store): dL/dt =
+        // A g - (B t + C), A = gamma rstd, B = A rstd k2, C = A (k1 - rstd k2 mean)
+        double* gsm = red;                       // [2][cs] gradient sums (red is free until the statistics)
+        shard_finish<2>(bpb_l, cs, tmp, tmp + cs);
+        shard_finish<2>(bpg_l, cs, gsm, gsm + cs);
+        float A = 0.f, Bc = 0.f, Cc = 0.f;
+        if (tid < pnv) {
+            const double cnt = a.bp_bn.count, g1 = gsm[tid], g2 = gsm[cs + tid];
+            const double mean = tmp[tid] / cnt;
+            double var = tmp[cs + tid] / cnt - mean * mean;
+            if (var < 0) var = 0;
+            const float rstd = (float)(1.0 / sqrt(var + (double)a.bp_bn.eps));
+            A = (a.bp_bn.gamma ? bp_a.g : 1.f) * rstd;
+            const float k1 = (float)(g1 / cnt), k2 = (float)(g2 / cnt);
+            const double rk2 = (double)rstd * (double)k2;
+            Bc = (float)((double)A * rk2);
+            Cc = (float)((double)A * ((double)k1 - rk2 * (double)(float)mean));
+            if (blockIdx.x == 0) {
+                if (a.bp_dbeta) a.bp_dbeta[tid] = (float)g1;
+                if (a.bp_dgamma) a.bp_dgamma[tid] = (float)g2;
+            }
+        }
+        __syncthreads();                         // every thread has read tmp / gsm
+        if (tid < cs) {
+            bnp[tid] = A;
+            bnp[cs + tid] = Bc;
+            ((float*)tmp)[tid] = Cc;
         }
     }
 #pragma unroll
@@ -429,15 +491,15 @@ __global__ __launch_bounds__(512) void k_conv_band2(rnvp_conv_args a, int shards
 }
 
 template <typename T, int NT, int TM, int CS, int HF, bool WREG>
-int launch_band2(const rnvp_conv_args* a, hipStream_t s) {
+int launch_band2(const rnvp_conv_args* a, hipStream_t s, bool dry) {
     using G = BandGeo<T, NT, TM, HF>;
     const long long M = (long long)a->B * a->H * a->W;
     const size_t shm = band2_lds_bytes<T, NT, TM, HF>(a->cs_in, a->W);
     if (shm > 160 * 1024) return RNVP_E_UNSUPPORTED;
-    // every staged row of a band in SB chunks per thread, every weight chunk in WB
+    // every staged row of a band in SB chunks per thread (BP: 4 per operand), every weight chunk in WB
     const int cpr = a->cs_in / G::CH;
     const int R = G::BM + 2 * (a->W + 1);
-    if ((long long)R * cpr > 8LL * 512) return RNVP_E_UNSUPPORTED;
+    if ((long long)R * cpr > (a->bp ? 4LL : 8LL) * 512) return RNVP_E_UNSUPPORTED;
     if ((long long)G::NC * (band2_kpl<T>(a->cs_in) / G::CH) > 10LL * 512) return RNVP_E_UNSUPPORTED;
     const long long nbands = (M + G::BM - 1) / G::BM;
     const long long grid = nbands < 256 ? nbands : 256;
@@ -445,6 +507,22 @@ int launch_band2(const rnvp_conv_args* a, hipStream_t s) {
     const unsigned ng = (unsigned)((nbands + per - 1) / per);
     const int sh = rnvp_stat_shards(M);
     const int nops = (a->residual ? 1 : 0) + (a->accumulate ? 1 : 0) + (a->epi_relu_bn_bwd ? 1 : 0);
+    if (a->bp) {
+        // a data gradient with the ReLU/BN epilogue only; the tables' shards fit shard_issue<2>
+        const int pnv = a->cs_in < a->cin ? a->cs_in : a->cin;
+        auto fits = [&](int sh_) { return (long long)pnv * (sh_ < 1 ? 1 : sh_) <= 2LL * 512; };
+        if (a->pro_bn_relu || !a->epi_relu_bn_bwd || nops != 1 || !a->bp_bn.sums || !a->bp_sums ||
+            !fits(a->bp_bn.shards) || !fits(a->bp_shards) || (a->cs_in > G::NC ? a->cs_in : G::NC) * 2 > 2 * G::WPG * G::NC)
+            return RNVP_E_UNSUPPORTED;
+        if constexpr (!WREG) {
+            if (dry) return RNVP_OK;
+            k_conv_band2<T, NT, TM, CS, HF, false, false, 1, true><<<ng, 512, shm, s>>>(*a, sh, per);
+            RNVP_LAUNCH_CHECK();
+            return RNVP_OK;
+        }
+        return RNVP_E_UNSUPPORTED;
+    }
+    if (dry) return RNVP_OK;
     if (a->pro_bn_relu) {
         switch (nops) {
             case 0: k_conv_band2<T, NT, TM, CS, HF, WREG, true, 0><<<ng, 512, shm, s>>>(*a, sh, per); break;
@@ -465,9 +543,16 @@ int launch_band2(const rnvp_conv_args* a, hipStream_t s) {
 }
 
 template <typename T, int CS>
-int dispatch_band2_cs(const rnvp_conv_args* a, hipStream_t s) {
+int dispatch_band2_cs(const rnvp_conv_args* a, hipStream_t s, bool dry) {
     const long long M = (long long)a->B * a->H * a->W;
     const long long b256 = (M + 255) / 256;
+    if (a->bp) {   // the prologue's registers: weights read from LDS per step (WREG = false)
+        if (a->n <= 32) {
+            if (b256 >= 512) return launch_band2<T, 2, 2, CS, 1, false>(a, s, dry);
+            return launch_band2<T, 2, 1, CS, 1, false>(a, s, dry);
+        }
+        return launch_band2<T, 4, 2, CS, 2, false>(a, s, dry);
+    }
     // <= 32 outputs: every wave holds both channel tiles of its pixels and
     // the weights in registers (k-loop LDS reads: the activation fragments
     // only); 256-pixel bands while that leaves >= 2 bands per workgroup.
@@ -475,19 +560,19 @@ int dispatch_band2_cs(const rnvp_conv_args* a, hipStream_t s) {
     // step (in registers they would take 144 VGPRs).
     constexpr bool WR = CS <= 32;   // 36-72 VGPRs of weights (64 channels: 144)
     if (a->n <= 32) {
-        if (b256 >= 512) return launch_band2<T, 2, 2, CS, 1, WR>(a, s);
-        return launch_band2<T, 2, 1, CS, 1, WR>(a, s);
+        if (b256 >= 512) return launch_band2<T, 2, 2, CS, 1, WR>(a, s, dry);
+        return launch_band2<T, 2, 1, CS, 1, WR>(a, s, dry);
     }
-    return launch_band2<T, 4, 2, CS, 2, false>(a, s);
+    return launch_band2<T, 4, 2, CS, 2, false>(a, s, dry);
 }
 
 template <typename T>
-int dispatch_band2(const rnvp_conv_args* a, hipStream_t s) {
+int dispatch_band2(const rnvp_conv_args* a, hipStream_t s, bool dry) {
     switch (a->cs_in) {
-        case 8: return dispatch_band2_cs<T, 8>(a, s);
-        case 16: return dispatch_band2_cs<T, 16>(a, s);
-        case 32: return dispatch_band2_cs<T, 32>(a, s);
-        case 64: return dispatch_band2_cs<T, 64>(a, s);
+        case 8: return dispatch_band2_cs<T, 8>(a, s, dry);
+        case 16: return dispatch_band2_cs<T, 16>(a, s, dry);
+        case 32: return dispatch_band2_cs<T, 32>(a, s, dry);
+        case 64: return dispatch_band2_cs<T, 64>(a, s, dry);
         default: return RNVP_E_UNSUPPORTED;
     }
 }
@@ -496,11 +581,11 @@ int dispatch_band2(const rnvp_conv_args* a, hipStream_t s) {
 
 // 3x3, 17..64 outputs, cs_in <= 64 with a fixed chunk column per thread,
 // 32k <= M < 2^21: the persistent band kernel (RNVP_E_UNSUPPORTED otherwise)
-int rnvp_conv_band2_launch(const rnvp_conv_args* a, hipStream_t s) {
+int rnvp_conv_band2_launch(const rnvp_conv_args* a, hipStream_t s, bool dry) {
     const long long M = (long long)a->B * a->H * a->W;
     if (a->ks != 3 || a->n <= 16 || a->n > 64 || a->cs_in > 64 || a->cs_out > 64) return RNVP_E_UNSUPPORTED;
     if (M < 32768 || M >= (1ll << 21)) return RNVP_E_UNSUPPORTED;
     // bf16 (the fp32 parity mode keeps the one-band-per-workgroup kernel)
     if (a->dtype != RNVP_BF16) return RNVP_E_UNSUPPORTED;
-    return dispatch_band2<bf16_t>(a, s);
+    return dispatch_band2<bf16_t>(a, s, dry);
 }

@@ -443,4 +443,4 @@ int rnvp_s1_fanout_launch(const rnvp_group_kargs& g, int klass, int grid, int ld
 
 // persistent band kernel for the wide-scale 3x3 convs (conv_band.hip):
 // RNVP_E_UNSUPPORTED outside 3x3 / 17..64 outputs / cs_in <= 64 / 32k <= M < 2^21
-int rnvp_conv_band2_launch(const rnvp_conv_args* a, hipStream_t s);
+int rnvp_conv_band2_launch(const rnvp_conv_args* a, hipStream_t s, bool dry = false);

@@ -94,9 +94,9 @@ def test_link_arguments_checked_without_launch():
 def test_bn_fold_support_query_without_launch():
     """rnvp_conv2d_check answers the engine's fold question on the host: a
     BatchNorm-backward prologue (bp) runs on the deep family's data-gradient
-    tiles and the wide scales' streaming 1x1 -- accepted where it pays,
-    refused (UNSUPPORTED) for the band 3x3, the 4-wave 1x1 tiles or a forced
-    non-deep variant, INVALID without the
+    tiles and the wide scales' streaming 1x1 and band 3x3 -- accepted where
+    it pays, refused (UNSUPPORTED) for the 16384-pixel 4-wave 1x1 tiles or a
+    forced non-deep variant, INVALID without the
     BatchNorm input; the coupling shard count mirrors the header's."""
     from realnvp_hip import _lib, engine
     L = _lib._Lib()
@@ -126,7 +126,8 @@ def test_bn_fold_support_query_without_launch():
     # wide scales: the streaming 1x1 (bf16) folds a data gradient with the ReLU/BN epilogue
     assert L.conv2d_check(ctypes.byref(args(64, 32, 64, 1, epi=True))) == 0
     assert L.conv2d_check(ctypes.byref(args(64, 32, 64, 1))) == -2
-    assert L.conv2d_check(ctypes.byref(args(64, 32, 64, 3, epi=True))) == -2   # the band 3x3 has no prologue
+    assert L.conv2d_check(ctypes.byref(args(64, 32, 64, 3, epi=True))) == 0    # the band 3x3
+    assert L.conv2d_check(ctypes.byref(args(64, 32, 64, 3))) == -2             # (with the ReLU/BN epilogue only)
     assert L.conv2d_check(ctypes.byref(args(64, 8, 256, 3, variant=1))) == -2
     assert L.conv2d_check(ctypes.byref(args(64, 8, 256, 3, bp_x=False))) == -1
     assert L.conv2d_check(ctypes.byref(args(64, 32, 64, 1, bp=0))) == 0

@@ -28,9 +28,9 @@ CASES = [
     ("ckbd", 24, 256, 8, 64, "bf16", 8),     # s4: 3x3 + 4-wave 1x1 (M = 4096)
     ("chan", 96, 512, 4, 64, "bf16", 8),
     ("ckbd", 12, 128, 16, 64, "bf16", 4),    # s3: 3x3 only (16384-pixel 1x1 keeps its apply)
-    ("ckbd", 6, 64, 32, 64, "bf16", 4),      # s2: the streaming 1x1
+    ("ckbd", 6, 64, 32, 64, "bf16", 8),      # s2: the streaming 1x1 and the band 3x3
     ("ckbd", 6, 64, 32, 64, "fp32", 0),      # (bf16 only)
-    ("ckbd", 3, 32, 64, 16, "bf16", 4),      # s1
+    ("ckbd", 3, 32, 64, 16, "bf16", 8),      # s1
 ]
 
 

@@ -14,7 +14,7 @@ trip disappear.
   side output (dL/dt), the epilogue's BatchNorm sums and the parameter
   gradients; 1x1 and 3x3, both data-gradient tile configurations, fp32 and
   bf16 (bf16 with and without the fragment-major weight image), and the wide
-  scales' streaming 1x1 (bf16).
+  scales' streaming 1x1 and band 3x3 (bf16).
 * test_coupling_fold_matches_unfolded: whole deep-scale couplings (drop-in
   module, forward + backward) with the fold on and off: the fold really
   happened (fewer BatchNorm-apply launches), outputs and every gradient agree
@@ -49,9 +49,11 @@ BP_CASES = [
     (64, 8, 8, 256, 256, 3, 0),
     (64, 16, 16, 128, 128, 3, 0),
     (64, 16, 16, 128, 64, 1, 0),
-    # the wide scales' streaming 1x1 (tuned dispatch, bf16)
+    # the wide scales' streaming 1x1 and band 3x3 (tuned dispatch, bf16)
     (64, 32, 32, 64, 64, 1, -1),
     (16, 64, 64, 32, 32, 1, -1),
+    (64, 32, 32, 64, 64, 3, -1),
+    (16, 64, 64, 32, 32, 3, -1),
 ]
 
 
@@ -65,7 +67,7 @@ def test_bp_conv_matches_apply_then_conv(case, dtype, frag):
     if frag and dtype == "fp32":
         pytest.skip("fragment-major weight images are bf16")
     if case[6] < 0 and (frag or dtype == "fp32"):
-        pytest.skip("the streaming 1x1 is bf16, row-major weights")
+        pytest.skip("the streaming 1x1 / band 3x3 are bf16, row-major weights")
     L = _lib.lib()
     B, H, W, Ci, Co, ks, cfg = case
     M = B * H * W
@@ -161,7 +163,7 @@ DEEP_CASES = [
     ("s4_chan_m1024", "chan", 96, 512, 4, 64),
     ("s4_ckbd_m4096", "ckbd", 24, 256, 8, 64),
     ("s3_ckbd_m16384", "ckbd", 12, 128, 16, 64),
-    # wide scales: only the streaming 1x1 data gradients fold (bf16)
+    # wide scales: the streaming 1x1 and band 3x3 data gradients fold (bf16)
     ("s2_ckbd_m65536", "ckbd", 6, 64, 32, 64),
     ("s1_ckbd_m65536", "ckbd", 3, 32, 64, 16),
 ]
@@ -204,8 +206,8 @@ def test_coupling_fold_matches_unfolded(case, dtype):
     _, _, _, mid, size, B = case
     M = B * size * size
     small = M <= 1024
-    if M > 16384:   # wide: res_block.1 into the streaming 1x1 (bf16 only)
-        want = 4 if dtype == "bf16" else 0
+    if M > 16384:   # wide: res_block.1 / .4 into the streaming 1x1 / band 3x3 (bf16 only)
+        want = 8 if dtype == "bf16" else 0
     else:
         want = 4 * (int(M <= 4096) + int(not (small and dtype == "fp32")))
     assert f1 == want, (f1, want)
