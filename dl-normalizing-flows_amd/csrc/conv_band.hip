@@ -514,13 +514,10 @@ int launch_band2(const rnvp_conv_args* a, hipStream_t s, bool dry) {
         if (a->pro_bn_relu || !a->epi_relu_bn_bwd || nops != 1 || !a->bp_bn.sums || !a->bp_sums ||
             !fits(a->bp_bn.shards) || !fits(a->bp_shards) || (a->cs_in > G::NC ? a->cs_in : G::NC) * 2 > 2 * G::WPG * G::NC)
             return RNVP_E_UNSUPPORTED;
-        if constexpr (!WREG) {
-            if (dry) return RNVP_OK;
-            k_conv_band2<T, NT, TM, CS, HF, false, false, 1, true><<<ng, 512, shm, s>>>(*a, sh, per);
-            RNVP_LAUNCH_CHECK();
-            return RNVP_OK;
-        }
-        return RNVP_E_UNSUPPORTED;
+        if (dry) return RNVP_OK;
+        k_conv_band2<T, NT, TM, CS, HF, WREG, false, 1, true><<<ng, 512, shm, s>>>(*a, sh, per);
+        RNVP_LAUNCH_CHECK();
+        return RNVP_OK;
     }
     if (dry) return RNVP_OK;
     if (a->pro_bn_relu) {
@@ -546,10 +543,11 @@ template <typename T, int CS>
 int dispatch_band2_cs(const rnvp_conv_args* a, hipStream_t s, bool dry) {
     const long long M = (long long)a->B * a->H * a->W;
     const long long b256 = (M + 255) / 256;
-    if (a->bp) {   // the prologue's registers: weights read from LDS per step (WREG = false)
+    if (a->bp) {   // the prologue's staging at half width per operand: the weights stay in registers
+        constexpr bool WRB = CS <= 32;
         if (a->n <= 32) {
-            if (b256 >= 512) return launch_band2<T, 2, 2, CS, 1, false>(a, s, dry);
-            return launch_band2<T, 2, 1, CS, 1, false>(a, s, dry);
+            if (b256 >= 512) return launch_band2<T, 2, 2, CS, 1, WRB>(a, s, dry);
+            return launch_band2<T, 2, 1, CS, 1, WRB>(a, s, dry);
         }
         return launch_band2<T, 4, 2, CS, 2, false>(a, s, dry);
     }
