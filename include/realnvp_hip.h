@@ -155,8 +155,9 @@ typedef struct rnvp_conv_args {
      * 16 rows with zeros).  The bf16 3x3 deep-scale kernels read it instead of
      * w: each weight load of a wave is one contiguous KiB in MFMA lane order. */
     const void* w_frag;
-    /* optional BatchNorm-backward prologue (bp = 1; data-gradient convs of
-     * the deep family only, see rnvp_conv2d_check): x is the gradient g of
+    /* optional BatchNorm-backward prologue (bp = 1; bf16/fp32 data-gradient
+     * convs on the deep-scale tiles, bf16 ones on the wide scales' streaming
+     * 1x1 and band 3x3 kernels -- see rnvp_conv2d_check): x is the gradient g of
      * BatchNorm bp_bn's OUTPUT (the producing dgrad's relu/BN epilogue
      * output), bp_x that BatchNorm's saved input t (both [M][cs_in]), and the
      * conv's operand is dL/dt = gamma rstd (g - k1 - xhat k2) with
