@@ -339,6 +339,72 @@ __global__ void k_reverse(rnvp_coupling_args a) {
     }
 }
 
+// backward of k_reverse (the inverse is differentiable in the reference:
+// modules_realnvp.py:284-291): for a transformed element y = (v' - sh) E with
+// v' = v sd + rm (running out_bn statistics, sd = sqrt(rv + eps)), E =
+// exp(-lr), lr = scale tanh(r) + shift:  dv = gy sd E, d sh = -gy E,
+// d lr = -gy y + gl (gl: the gradient of the returned log_diag_J = lr), d r =
+// d lr scale (1 - tanh^2 r); kept elements pass gy through.  d sh / d r go to
+// the net's output gradient (a.gst, NHWC), the scale / shift partials to the
+// sharded gscale_part (folded by the in part's reduction, k_in_bwd_red).
+template <typename T>
+__global__ __launch_bounds__(256) void k_reverse_bwd(rnvp_coupling_args a, int TP) {
+    extern __shared__ double dsm[];
+    __shared__ double redl[16];
+    const Geo g = geo(a);
+    const Tile t = tile_of(g, TP);
+    T* st = (T*)dsm;                                  // [tp][cs_st]
+    T* gs = st + t.tp * a.cs_st;                      // [tp][cs_gst]
+    const int total = g.C * t.tp;
+    tile_copy_in<T>(a.st, t.m0, t.tp, a.cs_st, st);
+    for (int e = threadIdx.x; e < t.tp * a.cs_gst; e += blockDim.x) stv(&gs[e], 0.f);
+    __syncthreads();
+    const float sc = a.scale[0], ss = a.scale_shift[0];
+    double gsc = 0.0, gss = 0.0;
+    for (int e = threadIdx.x; e < total; e += blockDim.x) {
+        const int c = e / t.tp, pl = e - c * t.tp, p = t.p0 + pl;
+        const long long idx = ((long long)t.b * g.C + c) * g.HW + p;
+        bool tr;
+        int cb;
+        if (g.kind == 0) {
+            tr = !ckbd_m(g, p);
+            cb = c;
+        } else {
+            tr = c >= g.on_base && c < g.on_base + g.Cb;
+            cb = c - g.on_base;
+        }
+        const float gy = a.gz[idx];
+        if (!tr) {
+            a.gx[idx] = gy;
+            continue;
+        }
+        float v = a.x[idx], sd = 1.f;
+        if (a.coupling_bn) {
+            sd = expf(0.5f * logf(a.out_rvar[cb] + a.eps));
+            v = v * sd + a.out_rmean[cb];
+        }
+        const float sh = ldv(&st[pl * a.cs_st + cb]), r = ldv(&st[pl * a.cs_st + g.Cb + cb]);
+        const float th = tanhf(r);
+        const float ex = expf(-(sc * th + ss));
+        const float y = (v - sh) * ex;
+        const float gl = a.gl_full ? a.gl_full[idx] : 0.f;
+        const float glr = -gy * y + gl;
+        a.gx[idx] = gy * sd * ex;
+        stv(&gs[pl * a.cs_gst + cb], -gy * ex);
+        stv(&gs[pl * a.cs_gst + g.Cb + cb], glr * sc * (1.f - th * th));
+        gsc += (double)glr * th;
+        gss += glr;
+    }
+    const float dsc = (float)block_sum(gsc, redl);   // (barriers also publish gs)
+    const float dss = (float)block_sum(gss, redl);
+    tile_copy_out<T>(gs, t.m0, t.tp, a.cs_gst, a.gst);
+    if (threadIdx.x == 0 && (dsc != 0.f || dss != 0.f)) {
+        double* sp = a.gscale_part + 2 * (blockIdx.x % RNVP_COUPLING_SHARDS);
+        atomicAdd(sp, (double)dsc);
+        atomicAdd(sp + 1, (double)dss);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // out part, backward
 // ---------------------------------------------------------------------------
@@ -817,6 +883,24 @@ extern "C" int rnvp_coupling_reverse(const rnvp_coupling_args* a, void* stream) 
     hipStream_t s = (hipStream_t)stream;
     if (a->dtype == RNVP_F32) k_reverse<float><<<rnvp_grid(n, 256, 2048), 256, 0, s>>>(*a);
     else k_reverse<bf16_t><<<rnvp_grid(n, 256, 2048), 256, 0, s>>>(*a);
+    RNVP_LAUNCH_CHECK();
+    return RNVP_OK;
+}
+
+extern "C" int rnvp_coupling_reverse_bwd(const rnvp_coupling_args* a, void* stream) {
+    int st = check(a);
+    if (st) return st;
+    if (!a->st || !a->gz || !a->gx || !a->gst || !a->gscale_part || !a->scale || !a->scale_shift) return RNVP_E_INVALID;
+    const int Cb = cb_of(a);
+    if (a->cs_gst < 2 * Cb || a->cs_st < 2 * Cb) return RNVP_E_INVALID;
+    if (a->coupling_bn && (!a->out_rmean || !a->out_rvar)) return RNVP_E_INVALID;
+    if (a->B == 0) return RNVP_OK;
+    const TileCfg tc = tile_cfg(a);
+    const int esz = a->dtype == RNVP_F32 ? 4 : 2;
+    const size_t shm = (size_t)tc.TP * (a->cs_st + a->cs_gst) * esz;
+    hipStream_t s = (hipStream_t)stream;
+    if (a->dtype == RNVP_F32) k_reverse_bwd<float><<<tc.grid, 256, shm, s>>>(*a, tc.TP);
+    else k_reverse_bwd<bf16_t><<<tc.grid, 256, shm, s>>>(*a, tc.TP);
     RNVP_LAUNCH_CHECK();
     return RNVP_OK;
 }

@@ -169,6 +169,7 @@ _SIGS = {
     "rnvp_coupling_in_fwd": (i32, [C.POINTER(CouplingArgs), vp]),
     "rnvp_coupling_out_fwd": (i32, [C.POINTER(CouplingArgs), vp]),
     "rnvp_coupling_reverse": (i32, [C.POINTER(CouplingArgs), vp]),
+    "rnvp_coupling_reverse_bwd": (i32, [C.POINTER(CouplingArgs), vp]),
     "rnvp_coupling_out_bwd": (i32, [C.POINTER(CouplingArgs), vp]),
     "rnvp_coupling_in_bwd": (i32, [C.POINTER(CouplingArgs), vp]),
     "rnvp_link_nclass": (i32, [i32, i32]),

@@ -652,6 +652,7 @@ class CouplingEngine:
         a.z = out.data_ptr()
         a.ldj_full = ldj.data_ptr() if want_ldj else None
         L.coupling_reverse(C.byref(a), s)
+        sv["x"] = x          # (the input, for a backward through the inverse)
         return out, ldj
 
 
@@ -878,7 +879,7 @@ class CouplingEngine:
             e[0] = "folded"
 
     def backward(self, sv, gz, gl_full, gl_sample, grad_block, gx=None, side=None, after=None, zero_at_end=False,
-                 defer=None, opt=None):
+                 defer=None, opt=None, reverse=False):
         """Returns dL/dx; parameter gradients are written into grad_block
         (flat fp32, zeroed by the caller; scale/shift grads accumulate).
 
@@ -902,7 +903,11 @@ class CouplingEngine:
         (rnvp_weight_norm_bwd_adam: dv/dg/dbias, Adam on every conv row, the
         new norms and the next step's packed images); "defer": only the
         weight gradients run here -- the caller runs the parameter pass over
-        this coupling's slabs later (param_pass_info) and zeroes its sums."""
+        this coupling's slabs later (param_pass_info) and zeroes its sums.
+
+        reverse: sv comes from reverse(..., saved=sv): the backward of the
+        inverse pass (rnvp_coupling_reverse_bwd in place of the out part's
+        backward; gl_full is the gradient of the returned log_diag_J)."""
         L = _lib.lib()
         x = sv["x"]
         B, H, W, dtype, training = sv["B"], sv["H"], sv["W"], sv["dtype"], sv["training"]
@@ -936,8 +941,13 @@ class CouplingEngine:
         a.gscale_part = sar.ptr("gscale_part")
         n_el, esz = x.numel(), DTYPES[dtype][1]
         cs_st = chan_stride(self.P.buf_ch["st"])
-        # (reduction: gz, u) + apply: gz, u, x read, gx written; st read, gst written
-        _launch("coupling", 24 * n_el + esz * B * H * W * 2 * cs_st, 0.0, L.coupling_out_bwd, C.byref(a), s)
+        if reverse:
+            # gz, x (, gl) read, gx written; st read, gst written
+            _launch("coupling", (16 if gl_full is not None else 12) * n_el + esz * B * H * W * 2 * cs_st, 0.0,
+                    L.coupling_reverse_bwd, C.byref(a), s)
+        else:
+            # (reduction: gz, u) + apply: gz, u, x read, gx written; st read, gst written
+            _launch("coupling", 24 * n_el + esz * B * H * W * 2 * cs_st, 0.0, L.coupling_out_bwd, C.byref(a), s)
 
         self._net_backward(sv, sc, ws, T, training, gp, s)
         # in_bn backward closes the critical path (dL/dx of the coupling) ...

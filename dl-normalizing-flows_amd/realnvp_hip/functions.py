@@ -70,28 +70,51 @@ def coupling_apply(mod, x, full_ldj):
     return _Coupling.apply(x, mod, mod.training, mod.compute_dtype, full_ldj, *params)
 
 
-_REVERSE_WARNED = [False]
+
+
+class _CouplingReverse(torch.autograd.Function):
+    """The inverse pass with a backward (modules_realnvp.py:284-291 is plain
+    torch in the reference, so differentiable): the forward keeps its saved
+    arena (net activations, in_bn batch sums) for rnvp_coupling_reverse_bwd +
+    the net's and the in part's backward."""
+    @staticmethod
+    def forward(ctx, x, mod, training, dtype, *params):
+        eng = mod.engine()
+        B, _, H, W = x.shape
+        sv = eng.saved(B, H, W, dtype, x.device, training)
+        out, ldj = eng.reverse(x, training, dtype, saved=sv)
+        ctx.eng, ctx.sv = eng, sv
+        ctx.mark_non_differentiable()
+        return out, ldj
+
+    @staticmethod
+    def backward(ctx, gz, gl):
+        eng, sv = ctx.eng, ctx.sv
+        x = sv["x"]
+        gz = torch.zeros_like(x) if gz is None else gz.contiguous()
+        gl = None if gl is None else gl.contiguous()
+        grad_block = torch.zeros(eng.n_params, device=x.device, dtype=torch.float32)
+        gx = eng.backward(sv, gz, gl, None, grad_block, reverse=True)
+        grads = []
+        for (off, cnt), p in zip(eng.layout.values(), eng.params()):
+            grads.append(grad_block[off:off + cnt].view_as(p) if p.requires_grad else None)
+        ctx.sv = None
+        eng.release(sv)
+        return (gx, None, None, None) + tuple(grads)
 
 
 def coupling_reverse(mod, x):
     """Inverse pass (modules_realnvp.py:284-291, 345-351).  Returns (x, log_diag_J)
-    where log_diag_J is the masked log_rescale, as the reference returns."""
+    where log_diag_J is the masked log_rescale, as the reference returns.
+    Differentiable (x and the parameters) when autograd wants it; under
+    torch.no_grad() (the sampling path, train.py:253-259) it keeps no state."""
     _check_device(x, type(mod).__name__)
-    if torch.is_grad_enabled() and x.requires_grad:
-        # the engine's inverse has no backward: refuse an input that asks for
-        # a gradient rather than return outputs that silently carry none
-        raise RuntimeError("%s(reverse=True): the MI355X engine's inverse pass is not differentiable with respect "
-                           "to its input; run it under torch.no_grad() (as train.py:253-259 does)"
-                           % type(mod).__name__)
-    if torch.is_grad_enabled() and not _REVERSE_WARNED[0] and any(p.requires_grad for p in mod.parameters()):
-        # the reference's RealNVP.sample()/g() work without no_grad on a model
-        # with trainable parameters: do the same, once telling the caller that
-        # the outputs are detached
-        _REVERSE_WARNED[0] = True
-        warnings.warn("%s(reverse=True) runs without autograd on the MI355X engine: the outputs carry no gradient "
-                      "with respect to the parameters" % type(mod).__name__, stacklevel=3)
+    x = x.contiguous()
+    if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in mod.engine().params())):
+        params = tuple(mod.engine().params())
+        return _CouplingReverse.apply(x, mod, mod.training, mod.compute_dtype, *params)
     with torch.no_grad():
-        out, ldj = mod.engine().reverse(x.contiguous(), mod.training, mod.compute_dtype)
+        out, ldj = mod.engine().reverse(x, mod.training, mod.compute_dtype)
     return out, ldj
 
 

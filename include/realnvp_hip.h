@@ -381,6 +381,13 @@ typedef struct rnvp_coupling_args {
 int rnvp_coupling_in_fwd(const rnvp_coupling_args* a, void* stream);   /* in_sums must be zeroed */
 int rnvp_coupling_out_fwd(const rnvp_coupling_args* a, void* stream);  /* out_sums must be zeroed */
 int rnvp_coupling_reverse(const rnvp_coupling_args* a, void* stream);  /* z = inverse(x) */
+/* backward of rnvp_coupling_reverse (training or eval; the out_bn inverse uses
+ * the running statistics, modules_realnvp.py:284-291): from gz = dL/dz and
+ * gl_full = dL/dlog_diag_J (or NULL) writes gx's direct part, the net output
+ * gradient gst and the scale / scale_shift partials into gscale_part (which
+ * rnvp_coupling_in_bwd folds into g_scale / g_scale_shift); the net backward
+ * and rnvp_coupling_in_bwd then run as after rnvp_coupling_out_bwd. */
+int rnvp_coupling_reverse_bwd(const rnvp_coupling_args* a, void* stream);
 int rnvp_coupling_out_bwd(const rnvp_coupling_args* a, void* stream);  /* bwd_sums zeroed; writes gx, gst */
 int rnvp_coupling_in_bwd(const rnvp_coupling_args* a, void* stream);   /* in_bwd_sums zeroed; gx += */
 

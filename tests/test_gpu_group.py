@@ -50,12 +50,13 @@ def _inputs(kind, cio, mid, size, B, seed=0):
 _ORACLE = {}
 
 
-def _oracle(case, mode):
+def _oracle(case, mode, training=True, reverse=False):
     """The CPU oracle of the same coupling step: mode "f64" (the truth),
     "f32" (the reference's own precision), "emu" / "emu_wide" (the engine's
-    bf16 rounding points, fp32 / fp64 conv accumulation).  Returns (y, ldj,
-    dL/dx, {name: gradient}) in float64."""
-    key = (case, mode)
+    bf16 rounding points, fp32 / fp64 conv accumulation); training / reverse
+    as the coupling's own arguments.  Returns (y, ldj, dL/dx, {name:
+    gradient}) in float64."""
+    key = (case, mode, training, reverse)
     if key not in _ORACLE:
         import realnvp_oracle as O
         from realnvp_bf16emu import Emu, _R
@@ -74,7 +75,7 @@ def _oracle(case, mode):
         try:
             xx = x.to(dt).requires_grad_(True)
             fn = O.checkerboard_coupling if kind == "ckbd" else O.channelwise_coupling
-            y, ldj = fn(S, "", xx, 1.0 if kind == "ckbd" else 0.0, hp, training=True)
+            y, ldj = fn(S, "", xx, 1.0 if kind == "ckbd" else 0.0, hp, training=training, reverse=reverse)
             grads = torch.autograd.grad((y * gy.to(dt) + ldj * gl.to(dt)).sum(), [xx] + [S[n] for n in names],
                                         allow_unused=True)
         finally:
@@ -84,7 +85,7 @@ def _oracle(case, mode):
     return _ORACLE[key]
 
 
-def _check_vs_oracle(case, dtype, got):
+def _check_vs_oracle(case, dtype, got, training=True, reverse=False):
     """Every gradient tensor and dL/dx of one launch schedule against the
     oracle, with test_deep_coupling_vs_reference's allowance: fp32 -- within
     5e-3 of the float64 truth or 3x the fp32 reference's own error, at most
@@ -97,10 +98,11 @@ def _check_vs_oracle(case, dtype, got):
     Zero-expectation gradients (a bias feeding a BatchNorm) are measured
     against 1e-3 (bf16: 1e-2) of the largest gradient norm."""
     y, ldj, gx, grads = got
+    o = lambda mode: _oracle(case, mode, training, reverse)  # noqa: E731
     if dtype == "fp32":
-        tgt, others, k, floor = _oracle(case, "f64"), [_oracle(case, "f32")], 3.0, 1e-3
+        tgt, others, k, floor = o("f64"), [o("f32")], 3.0, 1e-3
     else:
-        tgt, others, k, floor = _oracle(case, "emu"), [_oracle(case, "emu_wide"), _oracle(case, "f32")], 2.0, 1e-2
+        tgt, others, k, floor = o("emu"), [o("emu_wide"), o("f32")], 2.0, 1e-2
     ty, tl, tgx, tg = tgt
     gmax = max(float(v.norm()) for v in tg.values())
     ratio, info = [], []
@@ -118,7 +120,7 @@ def _check_vs_oracle(case, dtype, got):
     for i in np.argsort(-ratio)[:6]:
         print("%.2f  %-45s ours %.3g  other %.3g" % ((ratio[i],) + info[i]))
     assert (ratio > 1).mean() <= 0.05 and ratio.max() < 10, (float((ratio > 1).mean()), float(ratio.max()))
-    fy = float((y.double().cpu() - ty).norm() / ty.norm())
+    fy = float((y.detach().double().cpu() - ty).norm() / ty.norm())
     assert fy < (1e-5 if dtype == "fp32" else 1e-2), fy
 
 

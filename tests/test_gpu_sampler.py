@@ -89,17 +89,16 @@ def test_sampler_built_before_trainer_follows_moved_weights():
 
 def test_reverse_without_no_grad_on_a_trainable_model():
     """The reference's g() works without torch.no_grad() on a model whose
-    parameters require grad: the inverse runs detached with a
-    warning; an input that requires grad is refused."""
+    parameters require grad, and is differentiable there (plain torch,
+    modules_realnvp.py:284-291): the engine's inverse too -- same values as
+    under no_grad, outputs that carry a gradient, an input that requires grad
+    accepted (the gradients themselves: tests/test_gpu_reverse.py)."""
     model = make_model(32, 8, 1).eval()
     z = torch.randn(2, 3, 32, 32, device=DEV)
-    with pytest.warns(UserWarning):
-        import realnvp_hip.functions as F
-        F._REVERSE_WARNED[0] = False
-        x = model.g(z)
+    x = model.g(z)
     with torch.no_grad():
         ref = model.g(z)
-    assert not x.requires_grad and torch.equal(x, ref)
+    assert x.requires_grad and torch.equal(x.detach(), ref)
     mod = next(model.couplings())
-    with pytest.raises(RuntimeError):
-        mod(torch.randn(2, 3, 32, 32, device=DEV, requires_grad=True), reverse=True)
+    y, _ = mod(torch.randn(2, 3, 32, 32, device=DEV, requires_grad=True), reverse=True)
+    y.sum().backward()
