@@ -61,6 +61,12 @@ template <> struct WtCfg<1> { static constexpr int TCO = 128, TCI = 128, KS = 1,
 // loop is not load-latency bound)
 #define WT_SMALL_DEPTH 2
 #endif
+#ifndef WT_SPLIT_MIN_M
+// mixed-class groups over at least this many pixels launch per class (below;
+// config 1: scales 1-2, 19.35 -> 19.11 ms/step; from 262144: 19.16; every
+// size: 19.80 -- the deep scales' small launches lose, gpurun_out/splitab)
+#define WT_SPLIT_MIN_M 65536
+#endif
 template <> struct WtCfg<2> { static constexpr int TCO = 32, TCI = 32, KS = 3, WCO = 2, WCI = 2, WTG = 2, NX = 4, DEPTH = WT_SMALL_DEPTH, BALL = 1; };
 template <> struct WtCfg<3> { static constexpr int TCO = 64, TCI = 64, KS = 1, WCO = 2, WCI = 4, WTG = 1, NX = 2, DEPTH = WT_SMALL_DEPTH, BALL = 1; };
 
@@ -88,8 +94,15 @@ __host__ __device__ inline size_t wt_stage_bytes(int c, int H, int W, bool ko) {
     else x = (size_t)wt_npr(WT_SP / W, H) * (W + 2) * wt_pitch(tci, ko);
     return dy + x;
 }
+// 2 stages; the prologue's BN table + fp64 scratch (24 B per ci) alias the
+// second stage buffer, which is first written after the barrier that follows
+// every thread's table read (so the 1x1 64-channel class fits two
+// workgroups per CU: 2 x 80 KB)
+#ifndef WT_TABLE_ALIAS
+#define WT_TABLE_ALIAS 1
+#endif
 __host__ __device__ inline size_t wt_lds_bytes(int c, int H, int W, bool ko) {
-    return 2 * wt_stage_bytes(c, H, W, ko) + 24 * (size_t)wt_tci(c);   // 2 stages + BN table + fp64 scratch
+    return 2 * wt_stage_bytes(c, H, W, ko) + (WT_TABLE_ALIAS ? 0 : 24 * (size_t)wt_tci(c));
 }
 
 // the k -> pixel order of one 32-pixel k-step: lane group gq's B/A fragment
@@ -159,7 +172,7 @@ __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int 
     const int xrows = KS == 3 ? NPR * PW : WT_SP;               // staged x positions per stage
     const int xtot = xrows * CPI;                               // x chunks per stage
     const unsigned sbytes = (unsigned)wt_stage_bytes(CLS, H, W, KO);
-    float* bnp = (float*)(lds + 2 * sbytes);                    // scale [TCI] | shift [TCI] | fp64 scratch [2 TCI]
+    float* bnp = (float*)(lds + (WT_TABLE_ALIAS ? 1 : 2) * sbytes);                      // scale [TCI] | shift [TCI] | fp64 scratch [2 TCI] (stage buffer 1)
     // LDS-space base: stage addresses in 32-bit arithmetic (generic-pointer
     // offsets compiled to 64-bit multiply-adds per operand read)
     RNVP_LDS char* const L3 = (RNVP_LDS char*)lds;
@@ -244,12 +257,17 @@ __device__ __forceinline__ void wt_body(const WtConv& cv, int cot, int cit, int 
             }
         } else if (al) {
             // aligned stages: p0 + the chunk's invariant offset; al 1 also
-            // checks the row against the image (first / last stage of an image)
+            // checks the row against the image (first / last stage of an
+            // image).  The halo rows are bounded by the tensor, not by the
+            // slab: a slab may end inside an image, and the row below its
+            // last stage belongs to the next slab's pixels (bounding it by
+            // the slab's end dropped that row's tap contributions: ~7 % of
+            // the 3x3 weight gradient at 64x64 images, 2048-pixel slabs)
             const int om = (p0 / W) % H;
 #pragma unroll
             for (int u = 0; u < NX; ++u) {
                 const bool rowok = al == 2 || (unsigned)(om + xrow[u]) < (unsigned)H;
-                const bool ok = ((xinv >> u) & 1u) & rowok & (p0 + xrel[u] < me);
+                const bool ok = ((xinv >> u) & 1u) & rowok & (p0 + xrel[u] < M);
                 rx[SL][u] = __builtin_amdgcn_raw_buffer_load_b128(XR, ok ? ((p0 + xrel[u]) * cs + ci0 + cch * 8) * 2 : OOB,
                                                                   0, 0);
                 m |= (unsigned)ok << u;
@@ -566,14 +584,36 @@ int rnvp_wgrad_tap_launch(rnvp_wgrad_group* g, hipStream_t s) {
     }
     // ONE launch for the group -- the class kernel (its own register budget)
     // when every conv has the same class, else the all-class kernel (the
-    // largest class's 207 VGPRs for every task).  One launch per class
-    // serialises the launches on the stream and measured 0.3 ms/step slower
-    // (profiles/r4_wgrad_split.txt).  The conflict-free k order where every
-    // conv's wider rows fit LDS.
-    bool ko = true;
-    for (int c = 0; c < g->n_conv; ++c) ko = ko && wt_lds_bytes(g->conv[c].cls, H, W, true) <= 160 * 1024;
+    // largest class's VGPRs for every task) -- or, from WT_SPLIT_MIN_M pixels
+    // up, one class kernel per class present, back to back: at the wide
+    // scales the all-class kernel's register budget costs more than the
+    // extra launch (scale 1: 290 us grouped vs 134 + 94 us per class,
+    // tools/conv_microbench.py "wgrad s1 group"); at the deep scales one
+    // launch per class measured 0.3 ms/step slower (profiles/r4_wgrad_split.txt).
+    // The conflict-free k order where every conv's wider rows fit LDS.
     bool one_class = true;
     for (int c = 1; c < g->n_conv; ++c) one_class = one_class && g->conv[c].cls == g->conv[0].cls;
+    if (!one_class && M >= WT_SPLIT_MIN_M) {
+        for (int cls = 0; cls < 4; ++cls) {
+            rnvp_wgrad_group sg = *g;
+            sg.n_conv = 0;
+            for (int c = 0; c < g->n_conv; ++c)
+                if (g->conv[c].cls == cls) sg.conv[sg.n_conv++] = g->conv[c];
+            if (sg.n_conv == 0) continue;
+            const bool ko = wt_lds_bytes(cls, H, W, true) <= 160 * 1024;
+            long long tasks = 0;
+            for (int c = 0; c < sg.n_conv; ++c) {
+                sg.conv[c].task0 = (int)tasks;
+                tasks += wt_tasks(sg.conv[c], cls);
+            }
+            if (tasks > (1ll << 30)) return RNVP_E_INVALID;
+            hipLaunchKernelGGL(wt_kernel(cls, ko), dim3((unsigned)tasks), dim3(WT_NT), wt_lds_bytes(cls, H, W, ko), s, sg);
+            RNVP_LAUNCH_CHECK();
+        }
+        return RNVP_OK;
+    }
+    bool ko = true;
+    for (int c = 0; c < g->n_conv; ++c) ko = ko && wt_lds_bytes(g->conv[c].cls, H, W, true) <= 160 * 1024;
     long long tasks = 0;
     size_t shm = 0;
     for (int c = 0; c < g->n_conv; ++c) {

@@ -516,6 +516,11 @@ def _wgrad_case(B, H, W, cin, cout, ks, dtype, pro, seed=0):
 
 WGRAD_CASES = [
     ("small_pro", 4, 16, 16, 24, 40, 3, True),
+    # the wide scales' 32-channel 3x3 tile class at config 1's image widths
+    ("s1_3x3_w64", 16, 64, 64, 32, 32, 3, True),
+    ("s1_3x3_w64_b64", 64, 64, 64, 32, 32, 3, True),
+    ("s1_3x3_w32", 16, 32, 32, 32, 32, 3, True),
+    ("s1_3x3_w64_nopro", 16, 64, 64, 32, 32, 3, False),
     ("deep_1024", 16, 2, 2, 1024, 1024, 3, True),
     ("m_2pow22", 256, 128, 128, 8, 8, 3, False),      # config 4 scale 1: M = 2^22
     ("m_above_2pow22", 257, 128, 128, 8, 16, 1, True),
@@ -542,3 +547,80 @@ def test_grouped_wgrad_vs_torch(case, dtype):
     M = B * H * W
     tolb = tol * max(1.0, (M / 2.0 ** 18) ** 0.5)
     assert rel(gotb.cpu(), refb.cpu()) < tolb, rel(gotb.cpu(), refb.cpu())
+
+
+MIXED_WGRAD = [
+    # B, H, W, [(ks, cin, cout, pro)] -- one grouped launch over tile classes
+    (16, 64, 64, [(3, 32, 32, True), (1, 32, 32, True), (1, 32, 6, True), (3, 7, 32, False), (1, 64, 64, True)]),
+    (64, 32, 32, [(3, 64, 64, True), (1, 64, 64, True), (1, 64, 12, False)]),
+    (64, 8, 8, [(3, 256, 256, True), (1, 256, 256, True), (1, 32, 32, True)]),
+]
+
+
+@pytest.mark.parametrize("case", MIXED_WGRAD, ids=["m65536_s1", "m65536_s2", "m4096_deep"])
+def test_grouped_wgrad_mixed_classes(case):
+    """One rnvp_conv2d_wgrad_grouped call over convs of different tile
+    classes (3x3 / 1x1, 32 / 64 / 128+ channels), bf16: from 65536 pixels up
+    the launcher runs one class kernel per class (wgrad_tap.hip
+    WT_SPLIT_MIN_M), below it the all-class kernel -- every conv's dW and
+    bias gradient against torch's weight gradient in float64."""
+    from realnvp_hip import _lib
+    from realnvp_hip._lib import BNSrc, WgradGroup
+    from realnvp_hip.engine import stat_shards
+    from realnvp_hip.net import chan_stride, round_up
+    B, H, W, convs = case
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    M = B * H * W
+    L = _lib.lib()
+    nz = int(L.wgrad_slabs(M))
+    nrep = int(L.wgrad_replicas(nz))
+    grp = WgradGroup()
+    grp.dtype, grp.B, grp.H, grp.W, grp.n_conv = 1, B, H, W, len(convs)
+    keep, refs = [], []
+    for i, (ks, cin, cout, pro) in enumerate(convs):
+        csi, cso = chan_stride(cin), chan_stride(cout)
+        kp = round_up(ks * ks * csi, 64)
+        x = torch.zeros(M, csi, device=DEV, dtype=torch.bfloat16)
+        x[:, :cin] = torch.randn(M, cin, device=DEV, generator=gen).to(torch.bfloat16)
+        dy = torch.zeros(M, cso, device=DEV, dtype=torch.bfloat16)
+        dy[:, :cout] = torch.randn(M, cout, device=DEV, generator=gen).to(torch.bfloat16)
+        ws = torch.zeros(nrep, cout, kp, device=DEV)
+        wsb = torch.zeros(nrep, cout, device=DEV)
+        c = grp.conv[i]
+        c.x, c.cs_in, c.cin, c.ks = x.data_ptr(), csi, cin, ks
+        act = x[:, :cin].double()
+        if pro:
+            xf = x[:, :cin].double()
+            sh = stat_shards(M)
+            sums = torch.zeros(sh, 2, cin, dtype=torch.float64, device=DEV)
+            sums[0, 0], sums[0, 1] = xf.sum(0), (xf * xf).sum(0)
+            gam = torch.rand(cin, device=DEV, generator=gen) + 0.5
+            bet = torch.randn(cin, device=DEV, generator=gen) * 0.3
+            keep += [sums, gam, bet]
+            c.pro_bn_relu = 1
+            c.pro = BNSrc(sums.data_ptr(), float(M), None, None, gam.data_ptr(), bet.data_ptr(), 1e-5, sh)
+            mean = sums[0, 0] / M
+            var = (sums[0, 1] / M - mean * mean).clamp_min(0)
+            rstd = (1.0 / torch.sqrt(var + 1e-5)).float().double()
+            scale = (gam.double() * rstd).float().double()
+            shift = (bet.double() - mean.float().double() * gam.double() * rstd).float().double()
+            act = torch.relu(xf * scale + shift).to(torch.bfloat16).double()
+        c.dy, c.cs_dy, c.n = dy.data_ptr(), cso, cout
+        c.ws, c.wsb, c.kp, c.nz, c.nrep = ws.data_ptr(), wsb.data_ptr(), kp, nz, nrep
+        keep += [x, dy]
+        refs.append((ws, wsb, act, dy, ks, cin, cout, csi, kp))
+    L.conv2d_wgrad_grouped(C.byref(grp), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    errs = []
+    for i, (ws, wsb, act, dy, ks, cin, cout, csi, kp) in enumerate(refs):
+        a4 = act.reshape(B, H, W, cin).permute(0, 3, 1, 2)
+        d4 = dy[:, :cout].double().reshape(B, H, W, cout).permute(0, 3, 1, 2)
+        ref = torch.nn.grad.conv2d_weight(a4, (cout, cin, ks, ks), d4, padding=ks // 2)
+        refp = torch.zeros(cout, kp, dtype=torch.float64, device=DEV)
+        for ky in range(ks):
+            for kx in range(ks):
+                base = (ky * ks + kx) * csi
+                refp[:, base:base + cin] = ref[:, :, ky, kx]
+        errs.append((i, rel(ws.sum(0).double().cpu(), refp.cpu()), rel(wsb.sum(0).double().cpu(), d4.sum((0, 2, 3)).cpu())))
+    print(errs)
+    assert all(e < 1e-4 and eb < 1e-4 for _, e, eb in errs), errs

@@ -59,7 +59,9 @@ def frag_major(w):
 
 
 def conv_case(B, H, W, cin, cout, ks, pro=False, stats=False, residual=False, acc=False, dgrad_epi=False,
-              dtype="bf16", wgrad=False, variant=0, fm=False):
+              dtype="bf16", wgrad=False, variant=0, fm=False, group=None):
+    """group (wgrad only): the kernel sizes of a grouped launch's convs (each
+    its own dW slabs, same x / dy) -- e.g. a scale-1 coupling's 5 3x3 + 14 1x1"""
     dev = "cuda"
     tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
     esz = 2 if dtype == "bf16" else 4
@@ -82,19 +84,26 @@ def conv_case(B, H, W, cin, cout, ks, pro=False, stats=False, residual=False, ac
     if wgrad:
         nz = int(L.wgrad_slabs(M))
         nrep = int(L.wgrad_replicas(nz))
-        dw = torch.zeros(nrep, cout, kp, device=dev)
+        kss = list(group) if group else [ks]
+        dws = []
         a = WgradGroup()
         a.dtype = 1 if dtype == "bf16" else 0
-        a.B, a.H, a.W, a.n_conv = B, H, W, 1
-        c = a.conv[0]
-        c.x, c.cs_in, c.cin, c.ks = x.data_ptr(), csi, cin, ks
-        if pro:
-            c.pro_bn_relu = 1
-            c.pro = BNSrc(sums_in.data_ptr(), float(M), None, None, gam.data_ptr(), bet.data_ptr(), 1e-5, sh)
-        c.dy, c.cs_dy, c.n = y.data_ptr(), cso, cout
-        c.ws, c.kp, c.nz, c.nrep = dw.data_ptr(), kp, nz, nrep
+        a.B, a.H, a.W, a.n_conv = B, H, W, len(kss)
+        for i, k in enumerate(kss):
+            kpk = round_up(k * k * csi, 64)
+            dws.append(torch.zeros(nrep, cout, kpk, device=dev))
+            c = a.conv[i]
+            c.x, c.cs_in, c.cin, c.ks = x.data_ptr(), csi, cin, k
+            if pro:
+                c.pro_bn_relu = 1
+                c.pro = BNSrc(sums_in.data_ptr(), float(M), None, None, gam.data_ptr(), bet.data_ptr(), 1e-5, sh)
+            c.dy, c.cs_dy, c.n = y.data_ptr(), cso, cout
+            c.ws, c.kp, c.nz, c.nrep = dws[-1].data_ptr(), kpk, nz, nrep
         fn = lambda: L.conv2d_wgrad_grouped(C.byref(a), torch.cuda.current_stream().cuda_stream)  # noqa: E731
-        nbytes = esz * M * (csi + cso) + 4 * cout * ks * ks * cin
+        nbytes = sum(esz * M * (csi + cso) + 4 * cout * k * k * cin for k in kss)
+        flops = sum(2.0 * M * cout * k * k * cin for k in kss)
+        us = bench(fn)
+        return us, nbytes / us / 1e3, flops / us / 1e6
     else:
         a = ConvArgs()
         a.dtype = 1 if dtype == "bf16" else 0
@@ -163,6 +172,10 @@ CASES = [
     ("s2c 1x1 64->64 pro+stats", 64, 32, 32, 64, 64, 1, dict(pro=True, stats=True)),
     ("wgrad s1 1x1 32", 64, 64, 64, 32, 32, 1, dict(pro=True, wgrad=True)),
     ("wgrad s1 3x3 32", 64, 64, 64, 32, 32, 3, dict(pro=True, wgrad=True)),
+    ("wgrad s1 group 1x1 x14", 64, 64, 64, 32, 32, 1, dict(pro=True, wgrad=True, group=[1] * 14)),
+    ("wgrad s1 group 3x3 x5", 64, 64, 64, 32, 32, 3, dict(pro=True, wgrad=True, group=[3] * 5)),
+    ("wgrad s1 group 5 3x3 + 14 1x1", 64, 64, 64, 32, 32, 3, dict(pro=True, wgrad=True, group=[3] * 5 + [1] * 14)),
+    ("wgrad s2 group 5 3x3 + 14 1x1", 64, 32, 32, 64, 64, 3, dict(pro=True, wgrad=True, group=[3] * 5 + [1] * 14)),
     ("wgrad s2 3x3 64", 64, 32, 32, 64, 64, 3, dict(pro=True, wgrad=True)),
     ("wgrad s3 3x3 128", 64, 16, 16, 128, 128, 3, dict(pro=True, wgrad=True)),
     ("wgrad s5 3x3 512", 64, 4, 4, 512, 512, 3, dict(pro=True, wgrad=True)),
