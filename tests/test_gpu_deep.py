@@ -521,6 +521,19 @@ WGRAD_CASES = [
     ("s1_3x3_w64_b64", 64, 64, 64, 32, 32, 3, True),
     ("s1_3x3_w32", 16, 32, 32, 32, 32, 3, True),
     ("s1_3x3_w64_nopro", 16, 64, 64, 32, 32, 3, False),
+    # every config-1 scale at its full batch (slabs ending inside an image at
+    # s1 / s2), config 4's 128-channel 3x3 at 64x64, and the unaligned stage
+    # layout (H*W = 320: stages straddle images, a slab ends mid-image)
+    ("c1_s1_1x1", 64, 64, 64, 32, 32, 1, True),
+    ("c1_s1_in_3x3", 64, 64, 64, 7, 32, 3, False),
+    ("c1_s2_3x3", 64, 32, 32, 64, 64, 3, True),
+    ("c1_s2_1x1", 64, 32, 32, 64, 64, 1, True),
+    ("c1_s3_3x3", 64, 16, 16, 128, 128, 3, True),
+    ("c1_s4_3x3", 64, 8, 8, 256, 256, 3, True),
+    ("c1_s5_3x3", 64, 4, 4, 512, 512, 3, True),
+    ("c4_s2_3x3_w64", 64, 64, 64, 128, 128, 3, True),
+    ("unaligned_slab_mid", 13, 5, 64, 32, 32, 3, True),
+    ("unaligned_h3", 8, 3, 32, 32, 32, 3, True),
     ("deep_1024", 16, 2, 2, 1024, 1024, 3, True),
     ("m_2pow22", 256, 128, 128, 8, 8, 3, False),      # config 4 scale 1: M = 2^22
     ("m_above_2pow22", 257, 128, 128, 8, 16, 1, True),
