@@ -61,6 +61,16 @@ template <> struct WtCfg<1> { static constexpr int TCO = 128, TCI = 128, KS = 1,
 // loop is not load-latency bound)
 #define WT_SMALL_DEPTH 2
 #endif
+#ifndef WT_BALANCE
+// one-class launches in atomic mode re-slab for the device's slots (wt_balance)
+#define WT_BALANCE 1
+#endif
+#ifndef WT_WG_OVERHEAD
+#define WT_WG_OVERHEAD 2    // a workgroup's table prologue + epilogue, in stages
+#endif
+#ifndef WT_MIN_STAGES
+#define WT_MIN_STAGES 4
+#endif
 #ifndef WT_SPLIT_MIN_M
 // mixed-class groups over at least this many pixels launch per class (below;
 // config 1: scales 1-2, 19.35 -> 19.11 ms/step; from 262144: 19.16; every
@@ -555,6 +565,58 @@ long long wt_tasks(const rnvp_wgrad_conv& v, int cls) {
 // profiles/r4_wgrad_ab.txt)
 int wt_class(const rnvp_wgrad_conv& v, int H, int W) { return wt_class_base(v.ks, v.cs_in, v.cs_dy); }
 
+// compute units of the current device (queried once, before any capture: the
+// first launch is a warm-up step)
+int wt_cus() {
+    static int n = 0;
+    if (n == 0) {
+        int d = 0, v = 0;
+        n = (hipGetDevice(&d) == hipSuccess &&
+             hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && v > 0) ? v : 256;
+    }
+    return n;
+}
+
+// workgroups of a class kernel resident per CU: registers (the 3x3 and
+// 128-wide classes take > 128 VGPRs: 2 waves per SIMD = one 8-wave
+// workgroup; the 1x1 64-wide class 108) and LDS
+int wt_wg_per_cu(int cls, size_t lds) {
+    const int reg = cls == 3 ? 2 : 1;
+    const int l = lds > 0 ? (int)((160 * 1024) / lds) : reg;
+    return l < reg ? (l < 1 ? 1 : l) : reg;
+}
+
+// Slab size of a one-class launch whose convs accumulate atomically into
+// their replicas (nrep < nz: the slab count is then free): the stages per
+// slab that minimise rounds x (stages + WT_WG_OVERHEAD) over the device's
+// resident-workgroup slots.  The engine's 2048-pixel slabs leave scale 2's
+// 3x3 launch at 160 workgroups on 256 CUs and scale 1's at 2.5 rounds.
+void wt_balance(rnvp_wgrad_group& sg, int cls, long long M, size_t lds) {
+    long long t1 = 0;
+    int nrep = 1, sps0 = 1;
+    for (int c = 0; c < sg.n_conv; ++c) {
+        const rnvp_wgrad_conv& v = sg.conv[c];
+        if (v.nrep >= v.nz) return;                                   // plain stores: one slab per replica
+        t1 += (long long)((v.n + wt_tco(cls) - 1) / wt_tco(cls)) * v.tk;
+        nrep = v.nrep > nrep ? v.nrep : nrep;
+        sps0 = (int)(v.m_per_slab / WT_SP) > sps0 ? (int)(v.m_per_slab / WT_SP) : sps0;
+    }
+    const long long S = (M + WT_SP - 1) / WT_SP;
+    const long long slots = (long long)wt_cus() * wt_wg_per_cu(cls, lds);
+    long long best = -1, best_cost = 0;
+    for (long long sps = 2ll * sps0 < S ? 2ll * sps0 : S; sps >= WT_MIN_STAGES; --sps) {
+        const long long nz = (S + sps - 1) / sps;
+        if (nz <= nrep || nz * t1 > (1ll << 28)) continue;           // stay atomic
+        const long long cost = ((nz * t1 + slots - 1) / slots) * (sps + WT_WG_OVERHEAD);
+        if (best < 0 || cost < best_cost) { best = sps; best_cost = cost; }
+    }
+    if (best < 0) return;
+    for (int c = 0; c < sg.n_conv; ++c) {
+        sg.conv[c].nz = (int)((S + best - 1) / best);
+        sg.conv[c].m_per_slab = best * WT_SP;
+    }
+}
+
 }  // namespace
 
 // Launch of the tap-shared kernel for a bf16 group; RNVP_E_UNSUPPORTED when a
@@ -593,7 +655,7 @@ int rnvp_wgrad_tap_launch(rnvp_wgrad_group* g, hipStream_t s) {
     // The conflict-free k order where every conv's wider rows fit LDS.
     bool one_class = true;
     for (int c = 1; c < g->n_conv; ++c) one_class = one_class && g->conv[c].cls == g->conv[0].cls;
-    if (!one_class && M >= WT_SPLIT_MIN_M) {
+    if (M >= WT_SPLIT_MIN_M) {    // (a one-class group takes this path too: its slabs re-balanced)
         for (int cls = 0; cls < 4; ++cls) {
             rnvp_wgrad_group sg = *g;
             sg.n_conv = 0;
@@ -601,6 +663,7 @@ int rnvp_wgrad_tap_launch(rnvp_wgrad_group* g, hipStream_t s) {
                 if (g->conv[c].cls == cls) sg.conv[sg.n_conv++] = g->conv[c];
             if (sg.n_conv == 0) continue;
             const bool ko = wt_lds_bytes(cls, H, W, true) <= 160 * 1024;
+            if (WT_BALANCE) wt_balance(sg, cls, M, wt_lds_bytes(cls, H, W, ko));
             long long tasks = 0;
             for (int c = 0; c < sg.n_conv; ++c) {
                 sg.conv[c].task0 = (int)tasks;
