@@ -8,14 +8,16 @@ batch 64 -- the shape bench.py times; train.py:176-207 is the loop).
   noise stream (Philox seed) give, per 10-step window, the run-to-run scatter
   of the bits/dim curve (a per-window standard deviation of five runs,
   bounded below by its RMS over the curve: five samples make a noisy
-  estimate, and the scatter grows along the curve); the bf16 run (a sixth
-  noise seed) must stay within 3x the deviation such a further run has from
-  the fp32 runs' mean (scatter x sqrt(1 + 1/5)) in every window, and its
-  final bits/dim must be as low as the fp32 runs' within the same allowance.
-  (Measured: the fp32 runs scatter by 0.003-0.04 bpd per window, RMS ~0.02,
-  while the curve falls from 6.4 to 2.5 bpd over the 200 steps; the bf16
-  run's largest window deviation 0.03-0.05, transient -- bf16 and fp32 are
-  different roundings of a chaotic trajectory.)
+  estimate, and the scatter grows along the curve).  Three bf16 runs (further
+  noise seeds): their mean curve must stay within 3x the deviation two such
+  means have when both precisions train alike (scatter x sqrt(1/5 + 1/3)) in
+  every window, its final bits/dim as low as the fp32 mean's within that
+  allowance, and every single bf16 run within 4x a further run's deviation
+  (scatter x sqrt(1 + 1/5)).  (Measured: the fp32 runs scatter by 0.003-0.04
+  bpd per window, RMS ~0.02, while the curve falls from 6.4 to 2.5 bpd over
+  the 200 steps; single bf16 runs end 2.53-2.63 against fp32 runs' 2.50-2.57
+  -- bf16 and fp32 are different roundings of a chaotic trajectory, so one
+  bf16 run is one sample of that scatter, not a measurement of a bias.)
 * test_graph_replay_equals_eager_step: one captured + replayed bf16 step
   against the same step run eagerly from the same state: the same per-sample
   log-prob, gradient arena, parameters and Adam moments up to the rounding
@@ -80,27 +82,35 @@ def _train_curve(dtype, seed, batches, steps=200, window=10):
 
 
 NF32 = 5
+NB16 = 3
 
 
 def test_bf16_training_tracks_fp32():
     imgs = structured_images(8 * B).to(DEV)
     batches = [imgs[i * B:(i + 1) * B].contiguous() for i in range(8)]
     f32 = np.stack([_train_curve("fp32", 1000 + s, batches) for s in range(NF32)])
-    b16 = _train_curve("bf16", 1000 + NF32, batches)
+    b16 = np.stack([_train_curve("bf16", 1000 + NF32 + s, batches) for s in range(NB16)])
     mu, sd = f32.mean(axis=0), f32.std(axis=0, ddof=1)
+    mb = b16.mean(axis=0)
     # a few runs give a noisy per-window estimate: the curve's pooled (RMS)
-    # scatter bounds every window's from below; a further run deviates from the
-    # mean of NF32 runs by sd * sqrt(1 + 1 / NF32) -- 3x that is the allowance
-    pooled = float(np.sqrt(np.mean(sd ** 2)))
-    allow = 3 * np.sqrt(1 + 1 / NF32) * np.maximum(np.maximum(sd, pooled), 2e-3)
+    # scatter bounds every window's from below.  The mean of NB16 bf16 runs
+    # deviates from the mean of NF32 fp32 runs by sd * sqrt(1/NF32 + 1/NB16)
+    # when both precisions train alike -- 3x that is the allowance; a single
+    # bf16 run deviates by sd * sqrt(1 + 1/NF32) -- 4x that for each run
+    scat = np.maximum(np.maximum(sd, float(np.sqrt(np.mean(sd ** 2)))), 2e-3)
+    allow_mean = 3 * np.sqrt(1 / NF32 + 1 / NB16) * scat
+    allow_run = 4 * np.sqrt(1 + 1 / NF32) * scat
     print("fp32 bpd windows", np.round(f32, 4).tolist())
     print("bf16 bpd windows", np.round(b16, 4).tolist())
     print("scatter (fp32 sd)", np.round(sd, 5).tolist())
     # the curves go somewhere: training lowers bits/dim on this data
     assert f32[:, -1].max() < f32[:, 0].min() - 0.2, f32[:, [0, -1]]
-    dev = np.abs(b16 - mu) / allow
+    dev = np.abs(mb - mu) / allow_mean
+    print("bf16 mean deviation / allowance", np.round(dev, 2).tolist())
     assert (dev <= 1).all(), (np.round(dev, 2).tolist())
-    assert b16[-1] <= f32[:, -1].max() + allow[-1]
+    assert mb[-1] <= mu[-1] + allow_mean[-1]
+    devr = np.abs(b16 - mu) / allow_run
+    assert (devr <= 1).all(), (np.round(devr, 2).tolist())
 
 
 def _state(tr):
