@@ -1648,19 +1648,33 @@ __global__ __launch_bounds__(256) void k_wn_wd(const rnvp_wn_desc* __restrict__ 
     const int ng = (ncc + 7) / 8;
     const float r_kg = 1.0f / (float)(kk * ng), r_g = 1.0f / (float)ng;
     const RNVP_GLOBAL T* wf = (const RNVP_GLOBAL T*)d.wf;
-    for (int q = threadIdx.x; q < nco * kk * ng; q += 256) {
-        const int c = fdiv_small(q, r_kg), r = q - c * (kk * ng), tap = fdiv_small(r, r_g), c8 = (r - tap * ng) * 8;
-        const RNVP_GLOBAL T* src = wf + (long long)(co0 + c) * d.kp_f + tap * d.cs_in + ci0 + c8;
-        float f[8];
-        const u32x4 v0 = *(const RNVP_GLOBAL u32x4*)src;
-        unpack(v0, f, T());
-        if constexpr (sizeof(T) == 4) {
-            const u32x4 v1 = *(const RNVP_GLOBAL u32x4*)(src + 4);
-            unpack(v1, f + 4, T());
+    // WD_U items' loads issued before any is used (a latency-bound loop
+    // otherwise: one 16-byte load in flight per thread); a clamped duplicate
+    // past the end reloads the thread's first item and is not stored
+    constexpr int WD_U = 4, NV = sizeof(T) == 4 ? 2 : 1;
+    const int nit = nco * kk * ng;
+    for (int q0 = threadIdx.x; q0 < nit; q0 += WD_U * 256) {
+        u32x4 v[WD_U][NV];
+#pragma unroll
+        for (int u = 0; u < WD_U; ++u) {
+            const int q = q0 + u * 256 < nit ? q0 + u * 256 : q0;
+            const int c = fdiv_small(q, r_kg), r = q - c * (kk * ng), tap = fdiv_small(r, r_g), c8 = (r - tap * ng) * 8;
+            const RNVP_GLOBAL T* src = wf + (long long)(co0 + c) * d.kp_f + tap * d.cs_in + ci0 + c8;
+#pragma unroll
+            for (int h = 0; h < NV; ++h) v[u][h] = *(const RNVP_GLOBAL u32x4*)(src + 4 * h);
         }
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-            if (c8 + e < ncc) tile[c * TP + (c8 + e) * kk + tap] = f[e];
+        for (int u = 0; u < WD_U; ++u) {
+            const int q = q0 + u * 256;
+            if (q >= nit) break;
+            const int c = fdiv_small(q, r_kg), r = q - c * (kk * ng), tap = fdiv_small(r, r_g), c8 = (r - tap * ng) * 8;
+            float f[8];
+            unpack(v[u][0], f, T());
+            if constexpr (NV == 2) unpack(v[u][1], f + 4, T());
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                if (c8 + e < ncc) tile[c * TP + (c8 + e) * kk + tap] = f[e];
+        }
     }
     __syncthreads();
     wn_frag_tile<T>(d, co0, ci0, nco, ncc, [&](int c, int ci, int tap) { return tile[c * TP + ci * kk + tap]; });
