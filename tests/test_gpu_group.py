@@ -156,6 +156,7 @@ CASES = [
     # members sharing one input tile
     ("s2_ckbd_m65536", "ckbd", 6, 64, 32, 64),
     ("s1_ckbd_m65536", "ckbd", 3, 32, 64, 16),
+    ("s1_ckbd_m262144", "ckbd", 3, 32, 64, 64),    # config 1's scale 1 at its full batch
 ]
 
 

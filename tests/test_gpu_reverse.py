@@ -28,6 +28,7 @@ CASES = [
     ("ckbd", 3, 32, 64, 16),     # wide-scale kernels (M = 65536: band / stream families)
     ("ckbd", 12, 128, 16, 16),   # deep family
     ("chan", 12, 64, 16, 8),
+    ("ckbd", 3, 32, 64, 64),     # config 1's scale 1 at its full batch (M = 262144)
 ]
 
 
