@@ -157,6 +157,7 @@ CASES = [
     ("s2_ckbd_m65536", "ckbd", 6, 64, 32, 64),
     ("s1_ckbd_m65536", "ckbd", 3, 32, 64, 16),
     ("s1_ckbd_m262144", "ckbd", 3, 32, 64, 64),    # config 1's scale 1 at its full batch
+    ("s1_chan_m65536", "chan", 12, 64, 32, 64),     # ... and its channelwise couplings
 ]
 
 
